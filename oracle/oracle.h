@@ -1,0 +1,34 @@
+/* oracle.h — CPU restatement of the reference path.  TEST INFRASTRUCTURE ONLY (see oracle.c). */
+#ifndef SMLU_ORACLE_H
+#define SMLU_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct oracle_lu {
+  int64_t n, nnzL, nnzU;
+  int64_t *Lp, *Li, *Up, *Ui;
+  double *Lx, *Ux;
+} oracle_lu;
+
+/* All indices 0-based.  p, q: new -> old. */
+int oracle_rowscale(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
+                    double* Rs);
+oracle_lu* oracle_lu_fixed(int64_t n, const int64_t* colptr, const int64_t* rowval,
+                           const double* nzval, const double* Rs, const int64_t* p,
+                           const int64_t* q, int* status);
+void oracle_lu_free(oracle_lu* F);
+int64_t oracle_lu_nnz(const oracle_lu* F, int which);
+void oracle_lu_export(const oracle_lu* F, int64_t* Lp, int64_t* Li, double* Lx, int64_t* Up,
+                      int64_t* Ui, double* Ux);
+int oracle_lsolve(int64_t n, const int64_t* Lp, const int64_t* Li, const double* Lx, double* x);
+int oracle_rsolve(int64_t n, const int64_t* Up, const int64_t* Ui, const double* Ux, double* x);
+int oracle_ldiv(const oracle_lu* F, const double* Rs, const int64_t* p, const int64_t* q,
+                const double* b, double* x);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

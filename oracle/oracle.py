@@ -1,0 +1,262 @@
+"""CPU oracle for the smlu parity tests.  TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg import
+this module, and only as the checker.  The product path (``smlu`` + ``libsmlu.so``) never
+imports, links or executes anything under ``oracle/``.
+
+Contents
+--------
+* ctypes binding of ``liboracle.so`` (oracle.c): UMFPACK-style SUM row scaling, fixed-pivot
+  left-looking sparse LU of ``(Rs .* A)[p, q]``, CSC triangular solves and ``ldiv!``
+  (reference ``src/SharedMemSparseLU.jl:286-392``).
+* :class:`ChunkedSolve` — a verbatim-semantics numpy restatement of the reference's dense
+  chunk solve layout: ``get_chunking_parameters`` (:101-149), ``allocate_chunks`` (:151-178),
+  ``fill_chunks!`` (:180-243, rectangular chunks store the NEGATED values), ``lsolve!``
+  (:349-367, ``trsv!('L','N','U')`` + ``gemm!`` with alpha = beta = 1) and ``rsolve!``
+  (:374-392, chunks walked from the back).
+* :func:`test_matrix` — the reference's FE-like fixture generator (test/runtests.jl:12-21),
+  restated over a numpy Generator (Julia's MersenneTwister stream is not reproduced).
+
+Parity pinning: no reference outputs exist (no Julia, no UMFPACK in this image, nothing
+committed in the reference's tests).  The oracle is pinned by (i) the reference's own test
+checks restated in tests/test_oracle.py (solution vectors vs. independent solvers at the
+reference tolerances 1e-12 / 1e-10, test/runtests.jl:25-26), (ii) the UMFPACK contract
+``L*U == (Rs.*A)[p,q]`` (src/SharedMemSparseLU.jl:305-316) and (iii) LAPACK known answers:
+with scipy's partial-pivoting row order, the fixed-pivot oracle reproduces scipy.linalg.lu's
+L and U.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import scipy.linalg as sla
+import scipy.sparse as sp
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_f64p = ctypes.POINTER(ctypes.c_double)
+
+
+def build():
+    """Compile liboracle.so (gcc) if missing or stale."""
+    so = os.path.join(_HERE, "liboracle.so")
+    src = os.path.join(_HERE, "oracle.c")
+    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE])
+    return so
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        so = build()
+        L = ctypes.CDLL(so)
+        L.oracle_rowscale.argtypes = [ctypes.c_int64, _i64p, _i64p, _f64p, _f64p]
+        L.oracle_lu_fixed.restype = ctypes.c_void_p
+        L.oracle_lu_fixed.argtypes = [ctypes.c_int64, _i64p, _i64p, _f64p, _f64p, _i64p, _i64p,
+                                      ctypes.POINTER(ctypes.c_int)]
+        L.oracle_lu_free.argtypes = [ctypes.c_void_p]
+        L.oracle_lu_nnz.restype = ctypes.c_int64
+        L.oracle_lu_nnz.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.oracle_lu_export.argtypes = [ctypes.c_void_p, _i64p, _i64p, _f64p, _i64p, _i64p, _f64p]
+        L.oracle_ldiv.argtypes = [ctypes.c_void_p, _f64p, _i64p, _i64p, _f64p, _f64p]
+        _LIB = L
+    return _LIB
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def _csc(A):
+    A = sp.csc_matrix(A)
+    A.sort_indices()
+    A.sum_duplicates()
+    return (A, np.ascontiguousarray(A.indptr, dtype=np.int64),
+            np.ascontiguousarray(A.indices, dtype=np.int64),
+            np.ascontiguousarray(A.data, dtype=np.float64))
+
+
+def rowscale(A):
+    """Rs[i] = 1/sum_j |a_ij| (1 for an empty row) — UMFPACK SUM scaling."""
+    A, cp, ri, x = _csc(A)
+    n = A.shape[0]
+    Rs = np.empty(n)
+    lib().oracle_rowscale(n, _p(cp, _i64p), _p(ri, _i64p), _p(x, _f64p), _p(Rs, _f64p))
+    return Rs
+
+
+class OracleLU:
+    """Fixed-pivot LU: L*U == (Rs .* A)[p, q] with the given 0-based p, q (new -> old)."""
+
+    def __init__(self, A, p, q, Rs=None):
+        A, cp, ri, x = _csc(A)
+        n = A.shape[0]
+        self.n = n
+        self.Rs = np.ascontiguousarray(rowscale(A) if Rs is None else Rs, dtype=np.float64)
+        self.p = np.ascontiguousarray(p, dtype=np.int64)
+        self.q = np.ascontiguousarray(q, dtype=np.int64)
+        st = ctypes.c_int(0)
+        h = lib().oracle_lu_fixed(n, _p(cp, _i64p), _p(ri, _i64p), _p(x, _f64p),
+                                  _p(self.Rs, _f64p), _p(self.p, _i64p), _p(self.q, _i64p),
+                                  ctypes.byref(st))
+        if not h:
+            raise MemoryError("oracle_lu_fixed failed")
+        self.status = st.value
+        try:
+            nl = lib().oracle_lu_nnz(h, 0)
+            nu = lib().oracle_lu_nnz(h, 1)
+            Lp = np.empty(n + 1, np.int64); Li = np.empty(nl, np.int64); Lx = np.empty(nl)
+            Up = np.empty(n + 1, np.int64); Ui = np.empty(nu, np.int64); Ux = np.empty(nu)
+            lib().oracle_lu_export(h, _p(Lp, _i64p), _p(Li, _i64p), _p(Lx, _f64p),
+                                   _p(Up, _i64p), _p(Ui, _i64p), _p(Ux, _f64p))
+        finally:
+            lib().oracle_lu_free(h)
+        self.L = sp.csc_matrix((Lx, Li, Lp), shape=(n, n))
+        self.U = sp.csc_matrix((Ux, Ui, Up), shape=(n, n))
+
+    def lsolve(self, x):
+        """In-place L \\ x (reference lsolve!, src/SharedMemSparseLU.jl:349)."""
+        x[:] = _csc_lsolve(self.L, x)
+        return x
+
+    def rsolve(self, x):
+        """In-place U \\ x (reference rsolve!, src/SharedMemSparseLU.jl:374)."""
+        x[:] = _csc_rsolve(self.U, x)
+        return x
+
+    def ldiv(self, x, b):
+        """ldiv!(x, F, b) (src/SharedMemSparseLU.jl:286-342); x may be b."""
+        wrk = self.Rs[self.p] * b[self.p]
+        wrk = _csc_lsolve(self.L, wrk)
+        wrk = _csc_rsolve(self.U, wrk)
+        x[self.q] = wrk
+        return x
+
+
+def _csc_lsolve(L, b):
+    x = np.array(b, dtype=np.float64, copy=True)
+    Lp, Li, Lx = L.indptr, L.indices, L.data
+    for j in range(L.shape[0]):
+        s, e = Lp[j], Lp[j + 1]
+        rows = Li[s:e]
+        m = rows != j
+        x[rows[m]] -= Lx[s:e][m] * x[j]
+    return x
+
+
+def _csc_rsolve(U, b):
+    x = np.array(b, dtype=np.float64, copy=True)
+    Up, Ui, Ux = U.indptr, U.indices, U.data
+    for j in range(U.shape[0] - 1, -1, -1):
+        s, e = Up[j], Up[j + 1]
+        x[j] /= Ux[e - 1]
+        x[Ui[s:e - 1]] -= Ux[s:e - 1] * x[j]
+    return x
+
+
+# --------------------------------------------------------------------------------------
+# Verbatim-semantics restatement of the reference's chunked solve (small n only)
+# --------------------------------------------------------------------------------------
+class ChunkedSolve:
+    """Dense-chunk blocked triangular solves exactly as the reference lays them out.
+
+    L, U: scipy CSC factors following UMFPACK's conventions (L: unit diagonal stored first,
+    max row last in each column; U: min row first, diagonal last).  Indices here are 0-based;
+    the reference's 1-based ranges are shifted by one.
+    """
+
+    def __init__(self, L, U, chunk_size=None):
+        L = sp.csc_matrix(L); U = sp.csc_matrix(U)
+        L.sort_indices(); U.sort_indices()
+        m = L.shape[0]
+        n = U.shape[1]
+        cs = 8 if chunk_size is None else chunk_size      # :67-70
+        cs = min(cs, n)                                   # :72 (clamped with A.n)
+        self.m, self.n, self.chunk_size = m, n, cs
+        self.total_chunks = (m + cs - 1) // cs            # :108 (uses m, quirk Q1)
+        T = self.total_chunks
+        self.lcols, self.lrows, self.ucols, self.urows = [], [], [], []
+        for chunk in range(1, T + 1):                     # :111-123
+            colmin = (chunk - 1) * cs + 1
+            colmax = min(m, chunk * cs)
+            # maximum(L_rowval[L_colptr[j+1]-1] for j in cols): last (= max) row, 1-based
+            rmax = max(L.indices[L.indptr[j + 1] - 1] + 1 for j in range(colmin - 1, colmax))
+            self.lcols.append((colmin, colmax))
+            self.lrows.append((colmax + 1, rmax))
+        for chunk in range(1, T + 1):                     # :132-144 (from the back, Q2)
+            colmin = (T - chunk) * cs + 1
+            colmax = min(m, (T - chunk + 1) * cs)
+            rmin = min(U.indices[U.indptr[j]] + 1 for j in range(colmin - 1, colmax))
+            self.ucols.append((colmin, colmax))
+            self.urows.append((rmin, colmin - 1))
+        # allocate_chunks (:151-178) + fill_chunks! (:180-243)
+        self.Lchunks, self.Uchunks = [], []
+        for c in range(T):
+            cmin, cmax = self.lcols[c]
+            rmin, rmax = self.lrows[c]
+            tri = np.zeros((cmax - cmin + 1, cmax - cmin + 1))
+            rect = np.zeros((max(rmax - rmin + 1, 0), cmax - cmin + 1))
+            for col in range(cmin, cmax + 1):
+                for jj in range(L.indptr[col - 1], L.indptr[col]):
+                    row = L.indices[jj] + 1
+                    if row <= cmax:
+                        tri[row - cmin, col - cmin] = L.data[jj]
+                    else:
+                        rect[row - rmin, col - cmin] = -L.data[jj]      # negated (:207, Q3)
+            self.Lchunks += [tri, rect]
+        for c in range(T):
+            cmin, cmax = self.ucols[c]
+            rmin, rmax = self.urows[c]
+            tri = np.zeros((cmax - cmin + 1, cmax - cmin + 1))
+            rect = np.zeros((max(rmax - rmin + 1, 0), cmax - cmin + 1))
+            for col in range(cmin, cmax + 1):
+                for jj in range(U.indptr[col - 1], U.indptr[col]):
+                    row = U.indices[jj] + 1
+                    if row >= cmin:
+                        tri[row - cmin, col - cmin] = U.data[jj]
+                    else:
+                        rect[row - rmin, col - cmin] = -U.data[jj]      # negated (:238, Q3)
+            self.Uchunks += [tri, rect]
+
+    def lsolve(self, x):
+        """lsolve! (:349-367): trsv!('L','N','U') on the diagonal chunk, then gemm! into rows."""
+        for c in range(self.total_chunks):
+            cmin, cmax = self.lcols[c]
+            rmin, rmax = self.lrows[c]
+            xs = x[cmin - 1:cmax]
+            xs[:] = sla.solve_triangular(self.Lchunks[2 * c], xs, lower=True, unit_diagonal=True)
+            if rmax >= rmin:
+                x[rmin - 1:rmax] += self.Lchunks[2 * c + 1] @ xs
+        return x
+
+    def rsolve(self, x):
+        """rsolve! (:374-392): chunks from the back, trsv!('U','N','N') then gemm!."""
+        for c in range(self.total_chunks):
+            cmin, cmax = self.ucols[c]
+            rmin, rmax = self.urows[c]
+            xs = x[cmin - 1:cmax]
+            xs[:] = sla.solve_triangular(self.Uchunks[2 * c], xs, lower=False)
+            if rmax >= rmin:
+                x[rmin - 1:rmax] += self.Uchunks[2 * c + 1] @ xs
+        return x
+
+
+# --------------------------------------------------------------------------------------
+# Reference fixtures
+# --------------------------------------------------------------------------------------
+def test_matrix(rng, nel=6, ngr=5):
+    """test/runtests.jl:12-21: element blocks written with `.=` (assignment, later elements
+    overwrite shared corners), n = nel*(ngr-1)+1."""
+    n = nel * (ngr - 1) + 1
+    mat = np.zeros((n, n))
+    for iel in range(1, nel + 1):
+        imin = (iel - 1) * (ngr - 1) + 1
+        imax = iel * (ngr - 1) + 1
+        mat[imin - 1:imax, imin - 1:imax] = rng.random((ngr, ngr))
+    return sp.csc_matrix(mat)

@@ -1,0 +1,45 @@
+// device.hpp — types shared by the host schedule (smlu.cpp) and the gfx950 kernels
+// (kernels.hip).  One record per supernode (front) and one per GEMM region.
+#pragma once
+#include <cstdint>
+
+namespace smlu {
+
+// Front s is the dense M x M matrix (M = ns + nu) over index set [first, first+ns) U R_s.
+// It lives in three column-major pieces:
+//   columns [0, ns)            : L panel   store[Loff + j*M + i]        (ld M)
+//   rows [0, ns),  cols >= ns  : U12       store[Uoff + (j-ns)*ns + i]  (ld ns)
+//   rows >= ns,    cols >= ns  : F22       scratch[Foff + (j-ns)*nu + (i-ns)] (ld nu)
+struct SNode {
+  int64_t first;
+  int64_t Loff, Uoff, Foff;   // Foff = -1 when nu == 0
+  int64_t rowptr;             // into rows[] / relmap[] (nu entries)
+  int64_t voff;               // front vector offset for the solves (M doubles)
+  int32_t ns, nu;
+  int32_t parent, nb;         // nb = panel width of the blocked path (0 = LDS path)
+  int32_t mode;               // 0 = LDS front kernel, 1 = blocked + full-candidate pivoting,
+                              // 2 = blocked + diagonal-tile pivoting with growth check
+  int32_t chbeg, chend;       // children in chlist[chbeg, chend)
+  int32_t level;
+};
+
+// C(m x n, ldc) -= A(m x k, lda) * B(k x n, ldb), column-major; tiles of 64 x 64 numbered
+// from tile0 within one launch (tasks sorted by tile0).
+struct GemmTask {
+  const double* A;
+  const double* B;
+  double* C;
+  int32_t m, n, k;
+  int32_t lda, ldb, ldc;
+  int32_t tiles_m;
+  int64_t tile0;
+};
+
+// Per-launch front lists for the blocked path: front id + first workgroup index.
+struct FrontTile {
+  int32_t s;
+  int32_t pad;
+  int64_t wg0;
+};
+
+}  // namespace smlu

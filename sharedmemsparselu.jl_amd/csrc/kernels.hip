@@ -1,0 +1,845 @@
+// kernels.hip — gfx950 (CDNA4) kernels of the multifrontal numeric refactorization and the
+// level-scheduled triangular solves.  No MFMA (north star): the dense parts run on the fp64
+// VALU (v_fma_f64), whose peak on MI355X equals the fp64 matrix peak (78.6 TFLOP/s).
+//
+// Reference mapping (SharedMemSparseLU.jl):
+//   k_rowscale            UMFPACK SUM scaling behind lu(A) (src/SharedMemSparseLU.jl:74, Rs at :51)
+//   k_scatterA            gather A's values into fronts (the "active columns")
+//   k_extend_add          scatter of Schur-complement updates into ancestor fronts
+//   k_front_lds, k_panel, pivot search + pivot scaling + rank-1 Schur updates: the
+//   k_laswp_trsm_u,       numeric column-elimination loop of lu(A)/lu!(F,A) (:74, :247)
+//   k_trsm_l, k_gemm
+//   k_fwd_front           lsolve! (:349-367): trsv on the diagonal block + gemv below
+//   k_bwd_front           rsolve! (:374-392)
+//   k_perm_in/k_perm_out  ldiv!'s scale+permute / un-permute (:318-339)
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device.hpp"
+
+namespace smlu {
+
+#define WAVE 64
+
+__device__ __forceinline__ double wave_max_idx(double v, int& idx) {
+  // max |.| with smallest index on ties; 64-lane butterfly
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    double ov = __shfl_xor(v, o, 64);
+    int oi = __shfl_xor(idx, o, 64);
+    if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+  }
+  return v;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ void atomic_max_pos(double* addr, double v) {
+  // v >= 0: IEEE ordering of non-negative doubles matches their bit patterns as u64
+  atomicMax(reinterpret_cast<unsigned long long*>(addr), (unsigned long long)__double_as_longlong(v));
+}
+
+// info word per front: bit0 zero pivot, bit1 weak pivot, bits 2.. = 1 + first zero-pivot column
+__device__ __forceinline__ void publish_info(int32_t* info, int flag, int errcol) {
+  int v = *info | flag;
+  if (errcol >= 0 && (v >> 2) == 0) v |= (errcol + 1) << 2;
+  *info = v;
+}
+
+struct FrontPtrs {
+  double* L;
+  double* U;
+  double* F;
+  int64_t M, ns, nu;
+};
+
+__device__ __forceinline__ FrontPtrs front_ptrs(const SNode& s, double* store, double* scratch) {
+  FrontPtrs f;
+  f.ns = s.ns;
+  f.nu = s.nu;
+  f.M = (int64_t)s.ns + s.nu;
+  f.L = store + s.Loff;
+  f.U = store + s.Uoff;
+  f.F = s.Foff >= 0 ? scratch + s.Foff : nullptr;
+  return f;
+}
+
+__device__ __forceinline__ double* fel(const FrontPtrs& f, int64_t i, int64_t j) {
+  if (j < f.ns) return f.L + j * f.M + i;
+  if (i < f.ns) return f.U + (j - f.ns) * f.ns + i;
+  return f.F + (j - f.ns) * f.nu + (i - f.ns);
+}
+
+// ------------------------------------------------------------------------------------
+// Row scaling: Rs[i] = 1/sum_j |a_ij| summed in column order (bitwise equal to the oracle).
+// ------------------------------------------------------------------------------------
+__global__ void k_rowscale(int64_t n, const int64_t* __restrict__ rowptr,
+                           const int32_t* __restrict__ ent, const double* __restrict__ a,
+                           double* __restrict__ Rs) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.0;
+  for (int64_t e = rowptr[i]; e < rowptr[i + 1]; ++e) s += fabs(a[ent[e]]);
+  Rs[i] = s > 0.0 ? 1.0 / s : 1.0;
+}
+
+__global__ void k_fill(int64_t n, double* __restrict__ x, double v) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = v;
+}
+
+// ------------------------------------------------------------------------------------
+// Front assembly, part 1: A entries of this level's fronts -> their slots (plain stores into
+// freshly zeroed fronts; every A entry owns a unique slot).
+// ------------------------------------------------------------------------------------
+__global__ void k_scatterA(int64_t cnt, const int32_t* __restrict__ ents,
+                           const int64_t* __restrict__ dest, const int32_t* __restrict__ arow,
+                           const double* __restrict__ a, const double* __restrict__ Rs,
+                           double* __restrict__ store, double* __restrict__ scratch) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= cnt) return;
+  int32_t e = ents[t];
+  double v = Rs[arow[e]] * a[e];
+  int64_t d = dest[e];
+  if (d >= 0) store[d] = v;
+  else scratch[-1 - d] = v;
+}
+
+// ------------------------------------------------------------------------------------
+// Front assembly, part 2 (extend-add): child F22 column j -> parent front, one wave per
+// (child, column).  Rows of a child column map monotonically into the parent column.
+// Siblings run in separate passes (no two children of one parent in the same launch), so
+// the adds are race-free and the summation order is fixed (bitwise reproducible).
+// ------------------------------------------------------------------------------------
+__global__ void k_extend_add(int64_t ntasks, const int2* __restrict__ tasks,
+                             const SNode* __restrict__ sn, const int32_t* __restrict__ relmap,
+                             double* __restrict__ store, double* __restrict__ scratch) {
+  int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  int lane = threadIdx.x & 63;
+  if (w >= ntasks) return;
+  int2 tk = tasks[w];
+  const SNode c = sn[tk.x];
+  const SNode p = sn[c.parent];
+  FrontPtrs P = front_ptrs(p, store, scratch);
+  const int64_t nuc = c.nu;
+  const double* src = scratch + c.Foff + (int64_t)tk.y * nuc;
+  const int32_t* rm = relmap + c.rowptr;
+  const int64_t tj = rm[tk.y];
+  if (tj < P.ns) {
+    double* col = P.L + tj * P.M;
+    for (int64_t i = lane; i < nuc; i += 64) col[rm[i]] += src[i];
+  } else {
+    double* colU = P.U + (tj - P.ns) * P.ns;
+    double* colF = P.F + (tj - P.ns) * P.nu - P.ns;
+    for (int64_t i = lane; i < nuc; i += 64) {
+      int64_t ti = rm[i];
+      if (ti < P.ns) colU[ti] += src[i];
+      else colF[ti] += src[i];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Pivot choice shared by the LDS and panel kernels: threshold partial pivoting with a
+// diagonal preference (UMFPACK-style): keep the diagonal when |a_kk| >= diag_tol*amax.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int choose_pivot(double akk, double amax, int arg, int k,
+                                            double diag_tol) {
+  if (amax == 0.0) return k;
+  if (fabs(akk) >= diag_tol * amax && akk != 0.0) return k;
+  return arg;
+}
+
+// ------------------------------------------------------------------------------------
+// Small fronts (M <= 128): the whole front in LDS, one 256-thread workgroup per front.
+// Right-looking partial LU over the ns fully-summed columns with pivot search over the
+// fully-summed rows; the trailing F22 block receives its Schur update in the same pass.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_front_lds(const int32_t* __restrict__ list,
+                                                   const SNode* __restrict__ sn,
+                                                   double* __restrict__ store,
+                                                   double* __restrict__ scratch,
+                                                   int32_t* __restrict__ rowperm,
+                                                   int32_t* __restrict__ info,
+                                                   double* __restrict__ growth, double diag_tol,
+                                                   double piv_tol) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ int s_perm[128];
+  __shared__ int s_piv;
+  __shared__ int s_flag;
+  __shared__ int s_err;
+  const int sid = list[blockIdx.x];
+  const SNode s = sn[sid];
+  FrontPtrs f = front_ptrs(s, store, scratch);
+  const int M = (int)f.M, ns = (int)f.ns;
+  const int ld = M | 1;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // load
+  for (int j = wv; j < M; j += 4) {
+    for (int i = lane; i < M; i += 64) lds[j * ld + i] = *fel(f, i, j);
+  }
+  for (int i = tid; i < ns; i += 256) s_perm[i] = i;
+  if (tid == 0) { s_flag = 0; s_err = -1; }
+  __syncthreads();
+  for (int k = 0; k < ns; ++k) {
+    if (wv == 0) {
+      double am = -1.0, amo = 0.0;
+      int ai = k;
+      for (int i = k + lane; i < M; i += 64) {
+        double v = fabs(lds[k * ld + i]);
+        if (i < ns) {
+          if (v > am) { am = v; ai = i; }
+        } else if (v > amo) {
+          amo = v;
+        }
+      }
+      am = wave_max_idx(am, ai);
+      amo = wave_max(amo);
+      if (lane == 0) {
+        int piv = choose_pivot(lds[k * ld + k], am, ai, k, diag_tol);
+        double pv = fabs(lds[k * ld + piv]);
+        if (am <= 0.0) {
+          s_flag |= 1;
+          if (s_err < 0) s_err = k;
+        } else {
+          if (pv < piv_tol * fmax(am, amo)) s_flag |= 2;
+          atomic_max_pos(&growth[0], fmax(am, amo) / pv);
+        }
+        s_piv = piv;
+      }
+    }
+    __syncthreads();
+    const int piv = s_piv;
+    if (piv != k) {
+      for (int j = tid; j < M; j += 256) {
+        double t = lds[j * ld + k];
+        lds[j * ld + k] = lds[j * ld + piv];
+        lds[j * ld + piv] = t;
+      }
+      if (tid == 0) {
+        int t = s_perm[k];
+        s_perm[k] = s_perm[piv];
+        s_perm[piv] = t;
+      }
+      __syncthreads();
+    }
+    const double pv = lds[k * ld + k];
+    for (int i = k + 1 + tid; i < M; i += 256) lds[k * ld + i] = lds[k * ld + i] / pv;
+    __syncthreads();
+    for (int j = k + 1 + wv; j < M; j += 4) {
+      const double u = lds[j * ld + k];
+      if (u != 0.0)
+        for (int i = k + 1 + lane; i < M; i += 64)
+          lds[j * ld + i] = fma(-lds[k * ld + i], u, lds[j * ld + i]);
+    }
+    __syncthreads();
+  }
+  // store
+  for (int j = wv; j < M; j += 4) {
+    for (int i = lane; i < M; i += 64) *fel(f, i, j) = lds[j * ld + i];
+  }
+  for (int i = tid; i < ns; i += 256) rowperm[s.first + i] = s_perm[i];
+  if (tid == 0 && s_flag) publish_info(info + sid, s_flag, s_err);
+}
+
+// ------------------------------------------------------------------------------------
+// Blocked path, step 1: panel factorization.  One workgroup per front.  Candidate rows:
+// [kb, ns) (mode 1, full) or [kb, kb+w) (mode 2, diagonal tile).  The candidate block
+// (R x w) is factored in LDS; rows are permuted in place and the composed permutation is
+// recorded for the row swaps of the other columns (k_laswp_trsm_u).
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_panel(const int32_t* __restrict__ list, int step,
+                                               const SNode* __restrict__ sn,
+                                               double* __restrict__ store,
+                                               double* __restrict__ scratch,
+                                               int32_t* __restrict__ rowperm,
+                                               int32_t* __restrict__ swaps,  // per front: [cnt, (dst,src)*]
+                                               int64_t swap_stride, int32_t* __restrict__ info,
+                                               double* __restrict__ growth, double diag_tol) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ int s_lp[512];
+  __shared__ int s_piv;
+  __shared__ int s_flag;
+  __shared__ int s_err;
+  const int sid = list[blockIdx.x];
+  const SNode s = sn[sid];
+  FrontPtrs f = front_ptrs(s, store, scratch);
+  const int64_t M = f.M;
+  const int ns = (int)f.ns;
+  const int kb = step * s.nb;
+  const int w = min(s.nb, ns - kb);
+  const int R = (s.mode == 1) ? ns - kb : w;
+  const int ld = R | 1;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double* P = f.L + (int64_t)kb * M + kb;  // panel origin, ld M
+  for (int j = wv; j < w; j += 4)
+    for (int i = lane; i < R; i += 64) lds[j * ld + i] = P[(int64_t)j * M + i];
+  for (int i = tid; i < R; i += 256) s_lp[i] = i;
+  if (tid == 0) { s_flag = 0; s_err = -1; }
+  __syncthreads();
+  for (int k = 0; k < w; ++k) {
+    if (wv == 0) {
+      double am = -1.0;
+      int ai = k;
+      for (int i = k + lane; i < R; i += 64) {
+        double v = fabs(lds[k * ld + i]);
+        if (v > am) { am = v; ai = i; }
+      }
+      am = wave_max_idx(am, ai);
+      if (lane == 0) {
+        int piv = choose_pivot(lds[k * ld + k], am, ai, k, diag_tol);
+        if (am <= 0.0) {
+          s_flag |= 1;
+          if (s_err < 0) s_err = kb + k;
+        } else {
+          atomic_max_pos(&growth[0], am / fabs(lds[k * ld + piv]));
+        }
+        s_piv = piv;
+      }
+    }
+    __syncthreads();
+    const int piv = s_piv;
+    if (piv != k) {
+      for (int j = tid; j < w; j += 256) {
+        double t = lds[j * ld + k];
+        lds[j * ld + k] = lds[j * ld + piv];
+        lds[j * ld + piv] = t;
+      }
+      if (tid == 0) {
+        int t = s_lp[k];
+        s_lp[k] = s_lp[piv];
+        s_lp[piv] = t;
+      }
+      __syncthreads();
+    }
+    const double pv = lds[k * ld + k];
+    for (int i = k + 1 + tid; i < R; i += 256) lds[k * ld + i] = lds[k * ld + i] / pv;
+    __syncthreads();
+    for (int j = k + 1 + wv; j < w; j += 4) {
+      const double u = lds[j * ld + k];
+      if (u != 0.0)
+        for (int i = k + 1 + lane; i < R; i += 64)
+          lds[j * ld + i] = fma(-lds[k * ld + i], u, lds[j * ld + i]);
+    }
+    __syncthreads();
+  }
+  for (int j = wv; j < w; j += 4)
+    for (int i = lane; i < R; i += 64) P[(int64_t)j * M + i] = lds[j * ld + i];
+  // compose the row permutation of positions [kb, kb+R) and publish the moved rows
+  int32_t* rp = rowperm + s.first + kb;
+  int* old = reinterpret_cast<int*>(lds);  // reuse LDS (panel already stored)
+  __syncthreads();
+  for (int i = tid; i < R; i += 256) old[i] = rp[i];
+  __syncthreads();
+  for (int i = tid; i < R; i += 256) rp[i] = old[s_lp[i]];
+  int32_t* sw = swaps + (int64_t)blockIdx.x * swap_stride;
+  if (tid == 0) {
+    int cnt = 0;
+    for (int i = 0; i < R; ++i)
+      if (s_lp[i] != i) {
+        sw[1 + 2 * cnt] = i;
+        sw[2 + 2 * cnt] = s_lp[i];
+        ++cnt;
+      }
+    sw[0] = cnt;
+    if (s_flag) publish_info(info + sid, s_flag, s_err);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Blocked path, step 2: apply the panel's row permutation to every other column of the
+// front and compute the U row block  U[kb:kb+w, kb+w:M] = L_kk^{-1} A[kb:kb+w, kb+w:M].
+// One workgroup per 64 columns; columns outside the panel are numbered c in [0, M-w):
+// col = c < kb ? c : c + w.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int find_front_tile(const FrontTile* __restrict__ ft, int cnt, int64_t b) {
+  int lo = 0, hi = cnt - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (ft[mid].wg0 <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_laswp_trsm_u(const FrontTile* __restrict__ ft, int nft,
+                                                      int step, const SNode* __restrict__ sn,
+                                                      double* __restrict__ store,
+                                                      double* __restrict__ scratch,
+                                                      const int32_t* __restrict__ swaps,
+                                                      int64_t swap_stride) {
+  __shared__ double sL[64 * 65];      // L_kk, unit lower (w <= 64), ld 65
+  __shared__ double sX[64 * 65];      // 64 columns x w rows, ld 65 ; reused as swap buffer
+  const int64_t b = blockIdx.x;
+  const int fi = find_front_tile(ft, nft, b);
+  const SNode s = sn[ft[fi].s];
+  const int64_t tile = b - ft[fi].wg0;
+  FrontPtrs f = front_ptrs(s, store, scratch);
+  const int64_t M = f.M;
+  const int ns = (int)f.ns;
+  const int kb = step * s.nb;
+  const int w = min(s.nb, ns - kb);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int32_t* sw = swaps + (int64_t)fi * swap_stride;
+  const int nsw = sw[0];
+  const int64_t c0 = tile * 64;
+  const int64_t nout = M - w;
+  const int ncol = (int)min<int64_t>(64, nout - c0);
+  if (ncol <= 0) return;
+  // --- row permutation on these columns (rows are relative to kb) ---
+  if (nsw > 0) {
+    // process swap list in chunks of 64 moved rows
+    for (int base = 0; base < nsw; base += 64) {
+      int cnt = min(64, nsw - base);
+      for (int idx = tid; idx < cnt * ncol; idx += 256) {
+        int pi = idx % cnt, cj = idx / cnt;
+        int64_t c = c0 + cj;
+        int64_t col = c < kb ? c : c + w;
+        sX[cj * 65 + pi] = *fel(f, kb + sw[2 + 2 * (base + pi)], col);
+      }
+      __syncthreads();
+      for (int idx = tid; idx < cnt * ncol; idx += 256) {
+        int pi = idx % cnt, cj = idx / cnt;
+        int64_t c = c0 + cj;
+        int64_t col = c < kb ? c : c + w;
+        *fel(f, kb + sw[1 + 2 * (base + pi)], col) = sX[cj * 65 + pi];
+      }
+      __syncthreads();
+      // a later chunk may read rows written by an earlier chunk only if they alias; swap
+      // lists are permutations so sources of chunk 2 may be destinations of chunk 1 -> the
+      // whole list is handled in one chunk when nsw <= 64 (always true for nb <= 32 full
+      // mode and nb <= 64 tile mode, since moved rows <= 2*nb and tile mode moves <= w).
+    }
+  }
+  // --- TRSM on right-hand columns only ---
+  if (c0 + ncol <= kb) return;  // tile entirely left of the panel
+  const double* Lkk = f.L + (int64_t)kb * M + kb;
+  for (int j = wv; j < w; j += 4)
+    for (int i = lane; i < w; i += 64) sL[j * 65 + i] = Lkk[(int64_t)j * M + i];
+  for (int cj = wv; cj < ncol; cj += 4) {
+    int64_t c = c0 + cj;
+    if (c < kb) continue;
+    int64_t col = c + w;
+    for (int i = lane; i < w; i += 64) sX[cj * 65 + i] = *fel(f, kb + i, col);
+  }
+  __syncthreads();
+  if (tid < ncol && c0 + tid >= kb) {
+    double* x = sX + tid * 65;
+    for (int j = 0; j < w; ++j) {
+      const double xj = x[j];
+      for (int i = j + 1; i < w; ++i) x[i] = fma(-sL[j * 65 + i], xj, x[i]);
+    }
+  }
+  __syncthreads();
+  for (int cj = wv; cj < ncol; cj += 4) {
+    int64_t c = c0 + cj;
+    if (c < kb) continue;
+    int64_t col = c + w;
+    for (int i = lane; i < w; i += 64) *fel(f, kb + i, col) = sX[cj * 65 + i];
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Blocked path, step 3: rows below the candidate block, L = A * U_kk^{-1}.  One thread per
+// row holds its w panel entries in registers; U_kk is broadcast from LDS.  Tracks the
+// growth max |l| for the threshold check of mode 2.
+// ------------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(256) void k_trsm_l(const FrontTile* __restrict__ ft, int nft, int step,
+                                                const SNode* __restrict__ sn,
+                                                double* __restrict__ store,
+                                                double* __restrict__ scratch,
+                                                int32_t* __restrict__ info,
+                                                double* __restrict__ growth, double piv_tol) {
+  __shared__ double sU[W * W];
+  __shared__ double s_red[4];
+  const int64_t b = blockIdx.x;
+  const int fi = find_front_tile(ft, nft, b);
+  const int sid = ft[fi].s;
+  const SNode s = sn[sid];
+  const int64_t tile = b - ft[fi].wg0;
+  FrontPtrs f = front_ptrs(s, store, scratch);
+  const int64_t M = f.M;
+  const int ns = (int)f.ns;
+  const int kb = step * s.nb;
+  const int w = min(s.nb, ns - kb);
+  const int R = (s.mode == 1) ? ns - kb : w;
+  const int64_t r0 = kb + R;  // first row handled here
+  const int tid = threadIdx.x;
+  double* P = f.L + (int64_t)kb * M;  // column kb of the L panel
+  for (int idx = tid; idx < W * W; idx += 256) {
+    int i = idx % W, j = idx / W;
+    sU[idx] = (i < w && j < w) ? P[(int64_t)j * M + kb + i] : 0.0;
+  }
+  __syncthreads();
+  const int64_t row = r0 + tile * 256 + tid;
+  double gmax = 0.0;
+  if (row < M) {
+    double x[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) x[j] = (j < w) ? P[(int64_t)j * M + row] : 0.0;
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      if (j < w) {
+        x[j] = x[j] / sU[j * W + j];
+        gmax = fmax(gmax, fabs(x[j]));
+#pragma unroll
+        for (int k = j + 1; k < W; ++k) x[k] = fma(-x[j], sU[k * W + j], x[k]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < W; ++j)
+      if (j < w) P[(int64_t)j * M + row] = x[j];
+  }
+  gmax = wave_max(gmax);
+  if ((tid & 63) == 0) s_red[tid >> 6] = gmax;
+  __syncthreads();
+  if (tid == 0) {
+    double g = fmax(fmax(s_red[0], s_red[1]), fmax(s_red[2], s_red[3]));
+    if (g > 0.0) atomic_max_pos(&growth[0], g);
+    if (g > 1.0 / piv_tol) atomicOr(&info[sid], 2);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Dense update C -= A*B (fp64 VALU).  64x64 output tile per 256-thread workgroup, 4x4 per
+// thread, K staged through LDS in slices of 16 with register prefetch of the next slice.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int find_gemm_task(const GemmTask* __restrict__ t, int cnt, int64_t b) {
+  int lo = 0, hi = cnt - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (t[mid].tile0 <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+#define GBM 64
+#define GBN 64
+#define GBK 16
+__global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks, int ntask) {
+  __shared__ double As[2][GBK][GBM + 2];
+  __shared__ double Bs[2][GBK][GBN + 2];
+  const int64_t b = blockIdx.x;
+  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+  const int64_t tl = b - t.tile0;
+  const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int tid = threadIdx.x;
+  const int tx = tid & 15, ty = tid >> 4;  // 16 x 16 threads, 4x4 each
+  double acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+  // load mapping: A slice GBM x GBK: thread -> (row = tid & 63, kk = (tid >> 6) + 4*r), r<4
+  //               B slice GBK x GBN: thread -> (kk = tid & 15, col = (tid >> 4) + 16*r), r<4
+  const int ar = tid & 63, ak = tid >> 6;
+  const int bk = tid & 15, bc = tid >> 4;
+  double ra[4], rb[4];
+  const int K = t.k;
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int kk = ak + 4 * r;
+      int row = m0 + ar;
+      ra[r] = (row < t.m && k0 + kk < K) ? t.A[(int64_t)(k0 + kk) * t.lda + row] : 0.0;
+      int col = n0 + bc + 16 * r;
+      rb[r] = (col < t.n && k0 + bk < K) ? t.B[(int64_t)col * t.ldb + k0 + bk] : 0.0;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      As[buf][ak + 4 * r][ar] = ra[r];
+      Bs[buf][bk][bc + 16 * r] = rb[r];
+    }
+  };
+  int nk = (K + GBK - 1) / GBK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * GBK);
+#pragma unroll
+    for (int kk = 0; kk < GBK; ++kk) {
+      double a[4], bb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[cur][kk][tx + 16 * i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bb[j] = Bs[cur][kk][ty + 16 * j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], bb[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int col = n0 + ty + 16 * j;
+    if (col >= t.n) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int row = m0 + tx + 16 * i;
+      if (row < t.m) {
+        double* c = t.C + (int64_t)col * t.ldc + row;
+        *c = *c - acc[i][j];
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Solves.  Front vectors v_s (M doubles) live in vbuf[voff[s]].
+// Forward (L): gather own rows + children's update vectors, apply the front's row
+// permutation, unit-lower solve of the diagonal block in 64-column blocks (one wave does
+// the block by shuffles, all waves apply the block to the rows below), leave
+// v[ns:M) = update vector for the parent.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fwd_front(const int32_t* __restrict__ list,
+                                                   const SNode* __restrict__ sn,
+                                                   const int32_t* __restrict__ chlist,
+                                                   const int32_t* __restrict__ relmap,
+                                                   const int32_t* __restrict__ rowperm,
+                                                   const double* __restrict__ store,
+                                                   double* __restrict__ x,
+                                                   double* __restrict__ vbuf) {
+  __shared__ double xs[64];
+  const SNode s = sn[list[blockIdx.x]];
+  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
+  double* v = vbuf + s.voff;
+  double* xo = x + s.first;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int64_t i = tid; i < M; i += 256) v[i] = i < ns ? xo[i] : 0.0;
+  __syncthreads();
+  for (int c = s.chbeg; c < s.chend; ++c) {
+    const SNode ch = sn[chlist[c]];
+    const double* u = vbuf + ch.voff + ch.ns;
+    const int32_t* rm = relmap + ch.rowptr;
+    for (int64_t i = tid; i < ch.nu; i += 256) v[rm[i]] += u[i];
+    __syncthreads();
+  }
+  // permuted diagonal-block right-hand side -> x positions (owned by this front)
+  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[rowperm[s.first + i]];
+  __syncthreads();
+  for (int64_t i = tid; i < ns; i += 256) v[i] = xo[i];
+  __syncthreads();
+  const double* Lp = store + s.Loff;
+  for (int64_t jb = 0; jb < ns; jb += 64) {
+    const int bw = (int)min<int64_t>(64, ns - jb);
+    if (wv == 0) {
+      double xi = lane < bw ? v[jb + lane] : 0.0;
+      for (int j = 0; j < bw; ++j) {
+        double xj = __shfl(xi, j, 64);
+        if (lane > j && lane < bw) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
+      }
+      if (lane < bw) {
+        xs[lane] = xi;
+        v[jb + lane] = xi;
+      }
+    }
+    __syncthreads();
+    for (int64_t i = jb + bw + tid; i < M; i += 256) {
+      double acc = 0.0;
+      for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
+      v[i] -= acc;
+    }
+    __syncthreads();
+  }
+  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[i];
+}
+
+// Backward (U): x_s -= U12 * x[R_s]; then upper solve of the diagonal block from the bottom.
+__global__ __launch_bounds__(256) void k_bwd_front(const int32_t* __restrict__ list,
+                                                   const SNode* __restrict__ sn,
+                                                   const int32_t* __restrict__ rows,
+                                                   const double* __restrict__ store,
+                                                   double* __restrict__ x,
+                                                   double* __restrict__ vbuf) {
+  __shared__ double xs[64];
+  const SNode s = sn[list[blockIdx.x]];
+  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns, nu = s.nu;
+  double* v = vbuf + s.voff;
+  double* xo = x + s.first;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int32_t* R = rows + s.rowptr;
+  for (int64_t i = tid; i < nu; i += 256) v[ns + i] = x[R[i]];
+  __syncthreads();
+  const double* U12 = store + s.Uoff;
+  for (int64_t i = tid; i < ns; i += 256) {
+    double acc = 0.0;
+    for (int64_t j = 0; j < nu; ++j) acc = fma(U12[j * ns + i], v[ns + j], acc);
+    v[i] = xo[i] - acc;
+  }
+  __syncthreads();
+  const double* Lp = store + s.Loff;  // U11 in the upper triangle of the L panel
+  for (int64_t jb = ((ns - 1) / 64) * 64; jb >= 0; jb -= 64) {
+    const int bw = (int)min<int64_t>(64, ns - jb);
+    if (wv == 0) {
+      double xi = lane < bw ? v[jb + lane] : 0.0;
+      for (int j = bw - 1; j >= 0; --j) {
+        if (lane == j) xi = xi / Lp[(jb + j) * M + jb + j];
+        double xj = __shfl(xi, j, 64);
+        if (lane < j) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
+      }
+      if (lane < bw) {
+        xs[lane] = xi;
+        v[jb + lane] = xi;
+      }
+    }
+    __syncthreads();
+    for (int64_t i = tid; i < jb; i += 256) {
+      double acc = 0.0;
+      for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
+      v[i] -= acc;
+    }
+    __syncthreads();
+  }
+  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[i];
+}
+
+// wrk[i] = Rs[p0[i]] * b[p0[i]]
+__global__ void k_perm_in(int64_t n, const int64_t* __restrict__ p0, const double* __restrict__ Rs,
+                          const double* __restrict__ b, double* __restrict__ wrk) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    int64_t r = p0[i];
+    wrk[i] = Rs[r] * b[r];
+  }
+}
+// x[q[i]] = wrk[i]
+__global__ void k_perm_out(int64_t n, const int64_t* __restrict__ q, const double* __restrict__ wrk,
+                           double* __restrict__ x) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[q[i]] = wrk[i];
+}
+// final order -> pre-swap positions: out[first + rowperm[first+i]] = in[first+i]
+__global__ void k_unswap(int64_t n, const int64_t* __restrict__ pos_first,
+                         const int32_t* __restrict__ rowperm, const double* __restrict__ in,
+                         double* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    int64_t f = pos_first[i];
+    out[f + rowperm[i]] = in[i];
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Host-side launch wrappers (called from smlu.cpp)
+// ------------------------------------------------------------------------------------
+static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+hipError_t launch_rowscale(hipStream_t st, int64_t n, const int64_t* rowptr, const int32_t* ent,
+                           const double* a, double* Rs) {
+  if (n <= 0) return hipSuccess;
+  k_rowscale<<<nblk(n, 256), 256, 0, st>>>(n, rowptr, ent, a, Rs);
+  return hipGetLastError();
+}
+hipError_t launch_fill(hipStream_t st, int64_t n, double* x, double v) {
+  if (n <= 0) return hipSuccess;
+  k_fill<<<nblk(n, 256), 256, 0, st>>>(n, x, v);
+  return hipGetLastError();
+}
+hipError_t launch_scatterA(hipStream_t st, int64_t cnt, const int32_t* ents, const int64_t* dest,
+                           const int32_t* arow, const double* a, const double* Rs, double* store,
+                           double* scratch) {
+  if (cnt <= 0) return hipSuccess;
+  k_scatterA<<<nblk(cnt, 256), 256, 0, st>>>(cnt, ents, dest, arow, a, Rs, store, scratch);
+  return hipGetLastError();
+}
+hipError_t launch_extend_add(hipStream_t st, int64_t ntasks, const int2* tasks, const SNode* sn,
+                             const int32_t* relmap, double* store, double* scratch) {
+  if (ntasks <= 0) return hipSuccess;
+  k_extend_add<<<nblk(ntasks * 64, 256), 256, 0, st>>>(ntasks, tasks, sn, relmap, store, scratch);
+  return hipGetLastError();
+}
+hipError_t launch_front_lds(hipStream_t st, int cnt, int Mmax, const int32_t* list, const SNode* sn,
+                            double* store, double* scratch, int32_t* rowperm, int32_t* info,
+                            double* growth, double diag_tol, double piv_tol) {
+  if (cnt <= 0) return hipSuccess;
+  size_t lds = (size_t)Mmax * (size_t)(Mmax | 1) * sizeof(double);
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_front_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  k_front_lds<<<cnt, 256, lds, st>>>(list, sn, store, scratch, rowperm, info, growth, diag_tol, piv_tol);
+  return hipGetLastError();
+}
+hipError_t launch_panel(hipStream_t st, int cnt, int Rmax, int Wmax, int step, const int32_t* list,
+                        const SNode* sn, double* store, double* scratch, int32_t* rowperm,
+                        int32_t* swaps, int64_t swap_stride, int32_t* info, double* growth,
+                        double diag_tol) {
+  if (cnt <= 0) return hipSuccess;
+  size_t lds = (size_t)(Rmax | 1) * (size_t)Wmax * sizeof(double);
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_panel, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  k_panel<<<cnt, 256, lds, st>>>(list, step, sn, store, scratch, rowperm, swaps, swap_stride, info,
+                                 growth, diag_tol);
+  return hipGetLastError();
+}
+hipError_t launch_laswp_trsm_u(hipStream_t st, int64_t nwg, const FrontTile* ft, int nft, int step,
+                               const SNode* sn, double* store, double* scratch,
+                               const int32_t* swaps, int64_t swap_stride) {
+  if (nwg <= 0) return hipSuccess;
+  k_laswp_trsm_u<<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, scratch, swaps, swap_stride);
+  return hipGetLastError();
+}
+hipError_t launch_trsm_l(hipStream_t st, int64_t nwg, int W, const FrontTile* ft, int nft, int step,
+                         const SNode* sn, double* store, double* scratch, int32_t* info,
+                         double* growth, double piv_tol) {
+  if (nwg <= 0) return hipSuccess;
+  if (W <= 32)
+    k_trsm_l<32><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, scratch, info, growth, piv_tol);
+  else
+    k_trsm_l<64><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, scratch, info, growth, piv_tol);
+  return hipGetLastError();
+}
+hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask) {
+  if (ntiles <= 0) return hipSuccess;
+  k_gemm<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
+  return hipGetLastError();
+}
+hipError_t launch_fwd(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
+                      const int32_t* chlist, const int32_t* relmap, const int32_t* rowperm,
+                      const double* store, double* x, double* vbuf) {
+  if (cnt <= 0) return hipSuccess;
+  k_fwd_front<<<cnt, 256, 0, st>>>(list, sn, chlist, relmap, rowperm, store, x, vbuf);
+  return hipGetLastError();
+}
+hipError_t launch_bwd(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
+                      const int32_t* rows, const double* store, double* x, double* vbuf) {
+  if (cnt <= 0) return hipSuccess;
+  k_bwd_front<<<cnt, 256, 0, st>>>(list, sn, rows, store, x, vbuf);
+  return hipGetLastError();
+}
+hipError_t launch_perm_in(hipStream_t st, int64_t n, const int64_t* p0, const double* Rs,
+                          const double* b, double* wrk) {
+  k_perm_in<<<nblk(n, 256), 256, 0, st>>>(n, p0, Rs, b, wrk);
+  return hipGetLastError();
+}
+hipError_t launch_perm_out(hipStream_t st, int64_t n, const int64_t* q, const double* wrk, double* x) {
+  k_perm_out<<<nblk(n, 256), 256, 0, st>>>(n, q, wrk, x);
+  return hipGetLastError();
+}
+hipError_t launch_unswap(hipStream_t st, int64_t n, const int64_t* pos_first, const int32_t* rowperm,
+                         const double* in, double* out) {
+  k_unswap<<<nblk(n, 256), 256, 0, st>>>(n, pos_first, rowperm, in, out);
+  return hipGetLastError();
+}
+
+}  // namespace smlu

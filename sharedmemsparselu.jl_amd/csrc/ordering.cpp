@@ -1,0 +1,221 @@
+// ordering.cpp — fill-reducing orderings for the host symbolic phase.
+//
+// The reference gets its column order from UMFPACK (AMD on A+A' under the symmetric
+// strategy, COLAMD otherwise; called at src/SharedMemSparseLU.jl:74).  For a GPU
+// multifrontal factorization a nested-dissection order is the better fit: it yields a
+// balanced, shallow assembly tree (few levels -> few launches) whose top fronts are large
+// dense blocks.  Two variants:
+//   * geometric ND for structured grids (caller passes the grid shape), planar separators;
+//   * graph ND from BFS level structures (George's automatic nested dissection) with the
+//     separator trimmed to the level vertices that touch the next level.
+#include <algorithm>
+#include <cstdint>
+#include <functional>
+#include <numeric>
+#include <vector>
+
+#include "plan.hpp"
+
+namespace smlu {
+
+Graph build_sym_graph(int64_t n, const int64_t* colptr, const int32_t* rowval) {
+  Graph g;
+  g.n = n;
+  std::vector<int64_t> deg(n + 1, 0);
+  for (int64_t c = 0; c < n; ++c)
+    for (int64_t e = colptr[c]; e < colptr[c + 1]; ++e) {
+      int64_t r = rowval[e];
+      if (r == c) continue;
+      deg[r]++;
+      deg[c]++;
+    }
+  g.ptr.assign(n + 1, 0);
+  for (int64_t i = 0; i < n; ++i) g.ptr[i + 1] = g.ptr[i] + deg[i];
+  std::vector<int32_t> tmp(g.ptr[n]);
+  std::vector<int64_t> pos(g.ptr.begin(), g.ptr.end() - 1);
+  for (int64_t c = 0; c < n; ++c)
+    for (int64_t e = colptr[c]; e < colptr[c + 1]; ++e) {
+      int64_t r = rowval[e];
+      if (r == c) continue;
+      tmp[pos[r]++] = (int32_t)c;
+      tmp[pos[c]++] = (int32_t)r;
+    }
+  // sort + dedupe each row
+  std::vector<int64_t> nptr(n + 1, 0);
+  int64_t w = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    auto b = tmp.begin() + g.ptr[i], e = tmp.begin() + g.ptr[i + 1];
+    std::sort(b, e);
+    auto last = std::unique(b, e);
+    nptr[i] = w;
+    for (auto it = b; it != last; ++it) tmp[w++] = *it;
+  }
+  nptr[n] = w;
+  tmp.resize(w);
+  g.ptr.swap(nptr);
+  g.adj.swap(tmp);
+  return g;
+}
+
+// ---------------------------------------------------------------------------------------
+// Geometric nested dissection on an nx x ny x nz grid (vertex v = i + nx*(j + ny*k)).
+// Split the longest side at its middle plane; order(left), order(right), then the plane.
+// ---------------------------------------------------------------------------------------
+std::vector<int64_t> order_geometric_nd(int64_t nx, int64_t ny, int64_t nz, int64_t leaf) {
+  std::vector<int64_t> perm;
+  perm.reserve(nx * ny * nz);
+  struct Box { int64_t lo[3], hi[3]; };
+  auto emit = [&](const Box& b) {
+    for (int64_t k = b.lo[2]; k < b.hi[2]; ++k)
+      for (int64_t j = b.lo[1]; j < b.hi[1]; ++j)
+        for (int64_t i = b.lo[0]; i < b.hi[0]; ++i) perm.push_back(i + nx * (j + ny * k));
+  };
+  std::function<void(const Box&)> rec = [&](const Box& b) {
+    int64_t len[3] = {b.hi[0] - b.lo[0], b.hi[1] - b.lo[1], b.hi[2] - b.lo[2]};
+    if (len[0] <= 0 || len[1] <= 0 || len[2] <= 0) return;
+    int64_t vol = len[0] * len[1] * len[2];
+    int d = 0;
+    for (int t = 1; t < 3; ++t)
+      if (len[t] > len[d]) d = t;
+    if (vol <= leaf || len[d] < 3) { emit(b); return; }
+    int64_t mid = b.lo[d] + len[d] / 2;
+    Box L = b, R = b, S = b;
+    L.hi[d] = mid;
+    R.lo[d] = mid + 1;
+    S.lo[d] = mid;
+    S.hi[d] = mid + 1;
+    rec(L);
+    rec(R);
+    emit(S);
+  };
+  Box all{{0, 0, 0}, {nx, ny, nz}};
+  rec(all);
+  return perm;
+}
+
+// ---------------------------------------------------------------------------------------
+// Graph nested dissection from BFS level structures.
+// ---------------------------------------------------------------------------------------
+namespace {
+struct NDState {
+  const Graph& g;
+  std::vector<int32_t> stamp;   // membership of the current vertex subset
+  std::vector<int32_t> level;
+  std::vector<int64_t> out;
+  int32_t cur = 0;
+  explicit NDState(const Graph& gg) : g(gg), stamp(gg.n, -1), level(gg.n, -1) {}
+
+  // BFS inside subset marked `tag`; returns vertices in BFS order and level offsets.
+  void bfs(int32_t root, int32_t tag, std::vector<int32_t>& order, std::vector<int64_t>& lptr) {
+    order.clear();
+    lptr.clear();
+    order.push_back(root);
+    level[root] = 0;
+    lptr.push_back(0);
+    size_t head = 0;
+    int32_t curlev = 0;
+    while (head < order.size()) {
+      int32_t v = order[head];
+      if (level[v] != curlev) { lptr.push_back((int64_t)head); curlev = level[v]; }
+      ++head;
+      for (int64_t e = g.ptr[v]; e < g.ptr[v + 1]; ++e) {
+        int32_t u = g.adj[e];
+        if (stamp[u] != tag || level[u] >= 0) continue;
+        level[u] = level[v] + 1;
+        order.push_back(u);
+      }
+    }
+    lptr.push_back((int64_t)order.size());
+  }
+  void clear_levels(const std::vector<int32_t>& order) {
+    for (auto v : order) level[v] = -1;
+  }
+
+  void run(std::vector<int32_t> V, int depth, int64_t leafsz) {
+    if ((int64_t)V.size() <= leafsz || depth > 400) {
+      for (auto v : V) out.push_back(v);
+      return;
+    }
+    int32_t tag = ++cur;
+    for (auto v : V) stamp[v] = tag;
+    std::vector<int32_t> order;
+    std::vector<int64_t> lptr;
+    // connected components
+    {
+      std::vector<std::vector<int32_t>> comps;
+      for (auto v : V) {
+        if (level[v] >= 0) continue;
+        bfs(v, tag, order, lptr);
+        comps.emplace_back(order.begin(), order.end());
+      }
+      for (auto& c : comps) clear_levels(c);
+      if (comps.size() > 1) {
+        for (auto& c : comps) run(std::move(c), depth + 1, leafsz);
+        return;
+      }
+    }
+    // pseudo-peripheral root
+    int32_t root = V[0];
+    int64_t ecc = -1;
+    for (int it = 0; it < 6; ++it) {
+      bfs(root, tag, order, lptr);
+      int64_t h = (int64_t)lptr.size() - 2;
+      clear_levels(order);
+      if (h <= ecc) break;
+      ecc = h;
+      // min-degree vertex in the last level
+      int32_t best = order[lptr[lptr.size() - 2]];
+      int64_t bd = INT64_MAX;
+      for (int64_t t = lptr[lptr.size() - 2]; t < lptr.back(); ++t) {
+        int32_t v = order[t];
+        int64_t d = g.ptr[v + 1] - g.ptr[v];
+        if (d < bd) { bd = d; best = v; }
+      }
+      root = best;
+    }
+    bfs(root, tag, order, lptr);
+    int64_t nlev = (int64_t)lptr.size() - 1;
+    if (nlev < 3) {  // (nearly) a clique: no useful separator
+      clear_levels(order);
+      for (auto v : V) out.push_back(v);
+      return;
+    }
+    // middle level: first level whose cumulative count reaches half
+    int64_t half = (int64_t)V.size() / 2, m = 1;
+    for (m = 1; m < nlev - 1; ++m)
+      if (lptr[m + 1] >= half) break;
+    // separator: vertices of level m adjacent to level m+1
+    std::vector<int32_t> A, B, S;
+    for (int64_t t = 0; t < lptr[m]; ++t) A.push_back(order[t]);
+    for (int64_t t = lptr[m]; t < lptr[m + 1]; ++t) {
+      int32_t v = order[t];
+      bool touches = false;
+      for (int64_t e = g.ptr[v]; e < g.ptr[v + 1] && !touches; ++e) {
+        int32_t u = g.adj[e];
+        if (stamp[u] == tag && level[u] == m + 1) touches = true;
+      }
+      (touches ? S : A).push_back(v);
+    }
+    for (int64_t t = lptr[m + 1]; t < lptr[nlev]; ++t) B.push_back(order[t]);
+    clear_levels(order);
+    if (A.empty() || B.empty()) {
+      for (auto v : V) out.push_back(v);
+      return;
+    }
+    run(std::move(A), depth + 1, leafsz);
+    run(std::move(B), depth + 1, leafsz);
+    for (auto v : S) out.push_back(v);
+  }
+};
+}  // namespace
+
+std::vector<int64_t> order_graph_nd(const Graph& g, int64_t leaf) {
+  NDState st(g);
+  st.out.reserve(g.n);
+  std::vector<int32_t> V(g.n);
+  std::iota(V.begin(), V.end(), 0);
+  st.run(std::move(V), 0, std::max<int64_t>(leaf, 1));
+  return st.out;
+}
+
+}  // namespace smlu

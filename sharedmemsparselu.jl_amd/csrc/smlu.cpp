@@ -1,0 +1,1069 @@
+// smlu.cpp — C-ABI of libsmlu.so (include/smlu.h): handle lifetime, the static launch
+// schedule of the multifrontal refactorization and solves, device memory, factor export.
+//
+// Reference surface (SharedMemSparseLU.jl, src/SharedMemSparseLU.jl):
+//   ParallelSparseLU(A, chunk_size)  :64-98   -> smlu_create
+//   lu!(F, A)                        :245-279 -> smlu_refactor / smlu_refactor_csc
+//   ldiv!(x, F, b)                   :286-342 -> smlu_solve
+//   lsolve!(F, x) / rsolve!(F, x)    :349-392 -> smlu_lsolve / smlu_rsolve
+//   F.L, F.U, F.p, F.q, F.Rs         :45-52   -> smlu_get_factors
+//   cleanup_ParallelSparseLU!        :31      -> smlu_destroy
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/smlu.h"
+#include "device.hpp"
+#include "plan.hpp"
+
+namespace smlu {
+hipError_t launch_rowscale(hipStream_t, int64_t, const int64_t*, const int32_t*, const double*, double*);
+hipError_t launch_fill(hipStream_t, int64_t, double*, double);
+hipError_t launch_scatterA(hipStream_t, int64_t, const int32_t*, const int64_t*, const int32_t*,
+                           const double*, const double*, double*, double*);
+hipError_t launch_extend_add(hipStream_t, int64_t, const int2*, const SNode*, const int32_t*, double*,
+                             double*);
+hipError_t launch_front_lds(hipStream_t, int, int, const int32_t*, const SNode*, double*, double*,
+                            int32_t*, int32_t*, double*, double, double);
+hipError_t launch_panel(hipStream_t, int, int, int, int, const int32_t*, const SNode*, double*, double*,
+                        int32_t*, int32_t*, int64_t, int32_t*, double*, double);
+hipError_t launch_laswp_trsm_u(hipStream_t, int64_t, const FrontTile*, int, int, const SNode*, double*,
+                               double*, const int32_t*, int64_t);
+hipError_t launch_trsm_l(hipStream_t, int64_t, int, const FrontTile*, int, int, const SNode*, double*,
+                         double*, int32_t*, double*, double);
+hipError_t launch_gemm(hipStream_t, int64_t, const GemmTask*, int);
+hipError_t launch_fwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
+                      const int32_t*, const double*, double*, double*);
+hipError_t launch_bwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*,
+                      double*, double*);
+hipError_t launch_perm_in(hipStream_t, int64_t, const int64_t*, const double*, const double*, double*);
+hipError_t launch_perm_out(hipStream_t, int64_t, const int64_t*, const double*, double*);
+hipError_t launch_unswap(hipStream_t, int64_t, const int64_t*, const int32_t*, const double*, double*);
+}  // namespace smlu
+
+using namespace smlu;
+
+namespace {
+
+constexpr int kSmallM = 128;     // fronts up to this order are factored whole in LDS
+constexpr int kFullPivNs = 512;  // blocked fronts up to this many pivots search all fully-summed rows
+constexpr int kNbFull = 32;
+constexpr int kNbTile = 64;
+constexpr int kSwapStride = 1 + 2 * 64;
+
+thread_local std::string g_last_error;
+
+enum Kind : int {
+  K_MEMSET_STORE, K_MEMSET_SCRATCH, K_SCATTER, K_EXTADD, K_FRONT_LDS, K_PANEL, K_TRSMU, K_TRSML,
+  K_GEMM, K_FWD, K_BWD, K_NKIND
+};
+const char* kKindName[K_NKIND] = {"memset", "memset", "assemble", "assemble", "small", "panel",
+                                  "trsm", "trsm", "gemm", "solve", "solve"};
+
+struct Launch {
+  int kind = 0;
+  int step = 0;
+  int64_t off = 0, cnt = 0, nwg = 0, aux = 0, aux2 = 0;
+  double flops = 0;
+};
+
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t alloc(size_t cnt) {
+    n = cnt;
+    if (cnt == 0) return hipSuccess;
+    return hipMalloc((void**)&p, cnt * sizeof(T));
+  }
+  hipError_t upload(const T* h, size_t cnt, hipStream_t st) {
+    hipError_t e = alloc(cnt);
+    if (e != hipSuccess || cnt == 0) return e;
+    return hipMemcpyAsync(p, h, cnt * sizeof(T), hipMemcpyHostToDevice, st);
+  }
+  void free() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+}  // namespace
+
+struct smlu_plan {
+  Plan plan;
+};
+
+struct smlu_handle {
+  smlu_opts opts{};
+  Plan plan;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int64_t errcol = -1;
+  bool have_numeric = false;
+  bool given_Rs = false;
+  // device buffers
+  DBuf<double> A, Rs, store, scratch, wrk, wrk2, vbuf, growth;
+  DBuf<int64_t> Arowptr, Adest, p0, q, posfirst;
+  DBuf<int32_t> Arow_ent, Arow, Alev_ent, rows, relmap, chlist, ilist, rowperm, rowperm0, info, swaps;
+  DBuf<SNode> sn;
+  DBuf<int2> xtasks;
+  DBuf<FrontTile> ftiles;
+  DBuf<GemmTask> gtasks;
+  // schedule
+  std::vector<Launch> fac, fwd, bwd;
+  std::vector<SNode> hsn;
+  double gemm_flops = 0, dense_flops = 0;
+  int64_t nlaunch = 0;
+  // stats
+  double refactor_ms = 0, solve_ms = 0, growth_max = 0;
+  int64_t weak = 0;
+  double kind_ms[K_NKIND] = {0};
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
+  std::vector<int> ev_kind;
+  int32_t* hinfo = nullptr;  // pinned
+  ~smlu_handle() { release_all(); }
+  void release_buffers() {
+    if (stream) (void)hipSetDevice(device);
+    DBuf<double>* d[] = {&A, &Rs, &store, &scratch, &wrk, &wrk2, &vbuf, &growth};
+    for (auto* b : d) b->free();
+    DBuf<int64_t>* l[] = {&Arowptr, &Adest, &p0, &q, &posfirst};
+    for (auto* b : l) b->free();
+    DBuf<int32_t>* i[] = {&Arow_ent, &Arow, &Alev_ent, &rows, &relmap, &chlist, &ilist, &rowperm, &rowperm0, &info, &swaps};
+    for (auto* b : i) b->free();
+    sn.free();
+    xtasks.free();
+    ftiles.free();
+    gtasks.free();
+  }
+  void release_all() {
+    release_buffers();
+    for (auto& e : ev_pool) {
+      (void)hipEventDestroy(e.first);
+      (void)hipEventDestroy(e.second);
+    }
+    ev_pool.clear();
+    ev_kind.clear();
+    if (hinfo) (void)hipHostFree(hinfo);
+    hinfo = nullptr;
+    if (stream) (void)hipStreamDestroy(stream);
+    stream = nullptr;
+  }
+};
+
+#define HIPCHK(expr)                                                                 \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess) {                                                          \
+      h->err = std::string("HIP error: ") + hipGetErrorString(_e) + " at " #expr;    \
+      g_last_error = h->err;                                                         \
+      return SMLU_ERR_HIP;                                                           \
+    }                                                                                \
+  } while (0)
+
+static int fail(smlu_handle* h, int code, const std::string& msg) {
+  if (h) h->err = msg;
+  g_last_error = msg;
+  return code;
+}
+
+static PlanOptions plan_opts(const smlu_opts& o) {
+  PlanOptions p;
+  p.ordering = o.ordering;
+  for (int i = 0; i < 3; ++i) p.grid[i] = o.grid[i];
+  p.relax = o.relax;
+  p.leaf_size = o.leaf_size > 0 ? o.leaf_size : 64;
+  return p;
+}
+
+static int check_device(smlu_handle* h) {
+  int cnt = 0;
+  hipError_t e = hipGetDeviceCount(&cnt);
+  if (e != hipSuccess || cnt <= 0)
+    return fail(h, SMLU_ERR_NODEVICE, "no HIP device visible (libsmlu has no CPU fallback)");
+  if (h->opts.device < 0 || h->opts.device >= cnt)
+    return fail(h, SMLU_ERR_NODEVICE, "opts.device out of range");
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, h->opts.device) != hipSuccess)
+    return fail(h, SMLU_ERR_NODEVICE, "hipGetDeviceProperties failed");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(h, SMLU_ERR_NODEVICE, std::string("device is ") + prop.gcnArchName + ", libsmlu is built for gfx950 only");
+  h->device = h->opts.device;
+  return SMLU_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Schedule construction (host, once per plan)
+// ---------------------------------------------------------------------------------------
+static int build_schedule(smlu_handle* h) {
+  Plan& P = h->plan;
+  const int64_t nsup = P.nsup;
+  hipStream_t st = h->stream;
+  // supernode records
+  h->hsn.resize(nsup);
+  int64_t voff = 0;
+  for (int64_t s = 0; s < nsup; ++s) {
+    SNode r{};
+    r.first = P.s_first[s];
+    r.Loff = P.Loff[s];
+    r.Uoff = P.Uoff[s];
+    r.Foff = P.Foff[s];
+    r.rowptr = P.s_rowptr[s];
+    r.voff = voff;
+    r.ns = (int32_t)P.ns(s);
+    r.nu = (int32_t)P.nu(s);
+    voff += P.M(s);
+    r.parent = (int32_t)P.s_parent[s];
+    int64_t M = P.M(s);
+    if (M <= kSmallM) { r.mode = 0; r.nb = 0; }
+    else if (r.ns <= kFullPivNs) { r.mode = 1; r.nb = kNbFull; }
+    else { r.mode = 2; r.nb = kNbTile; }
+    if (h->opts.pivot_tol <= 0) { /* no pivoting requested: tile mode never searches far */ }
+    r.chbeg = (int32_t)P.ch_ptr[s];
+    r.chend = (int32_t)P.ch_ptr[s + 1];
+    r.level = P.s_level[s];
+    h->hsn[s] = r;
+  }
+  // given (p,q): no pivoting on top of the caller's order -> tile mode pivots only if the
+  // diagonal is exactly zero; we force diag preference by a tiny diag tolerance at launch.
+  std::vector<int32_t> ilist;
+  std::vector<int2> xt;
+  std::vector<FrontTile> ft;
+  std::vector<GemmTask> gt;
+  double* store = h->store.p;
+  double* scratch = h->scratch.p;
+  h->fac.clear();
+  h->gemm_flops = 0;
+  h->dense_flops = P.flops;
+  int64_t max_list = 1;
+  for (int l = 0; l < P.nlevels; ++l) {
+    Launch L;
+    // zero this level's fronts
+    L = Launch();
+    L.kind = K_MEMSET_STORE;
+    L.off = P.lev_foff[l];
+    L.cnt = P.lev_foff[l + 1] - P.lev_foff[l];
+    if (L.cnt > 0) h->fac.push_back(L);
+    if (P.lev_ssize[l] > 0) {
+      L = Launch();
+      L.kind = K_MEMSET_SCRATCH;
+      L.off = P.lev_soff[l];
+      L.cnt = P.lev_ssize[l];
+      h->fac.push_back(L);
+    }
+    // A entries
+    L = Launch();
+    L.kind = K_SCATTER;
+    L.off = P.Alev_ptr[l];
+    L.cnt = P.Alev_ptr[l + 1] - P.Alev_ptr[l];
+    if (L.cnt > 0) h->fac.push_back(L);
+    // extend-add passes by child rank
+    int maxrank = -1;
+    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+      int64_t s = P.lev_sup[k];
+      maxrank = std::max<int>(maxrank, (int)(P.ch_ptr[s + 1] - P.ch_ptr[s]) - 1);
+    }
+    for (int r = 0; r <= maxrank; ++r) {
+      L = Launch();
+      L.kind = K_EXTADD;
+      L.off = (int64_t)xt.size();
+      for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+        int64_t s = P.lev_sup[k];
+        if (P.ch_ptr[s] + r >= P.ch_ptr[s + 1]) continue;
+        int64_t c = P.ch_list[P.ch_ptr[s] + r];
+        for (int64_t j = 0; j < P.nu(c); ++j) xt.push_back(make_int2((int)c, (int)j));
+      }
+      L.cnt = (int64_t)xt.size() - L.off;
+      if (L.cnt > 0) h->fac.push_back(L);
+    }
+    // small fronts
+    {
+      L = Launch();
+      L.kind = K_FRONT_LDS;
+      L.off = (int64_t)ilist.size();
+      int64_t Mmax = 0;
+      for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+        int64_t s = P.lev_sup[k];
+        if (h->hsn[s].mode != 0) continue;
+        ilist.push_back((int32_t)s);
+        Mmax = std::max(Mmax, P.M(s));
+      }
+      L.cnt = (int64_t)ilist.size() - L.off;
+      L.aux = Mmax;
+      if (L.cnt > 0) h->fac.push_back(L);
+      max_list = std::max(max_list, L.cnt);
+    }
+    // blocked fronts
+    std::vector<int64_t> big;
+    int64_t maxsteps = 0;
+    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+      int64_t s = P.lev_sup[k];
+      const SNode& r = h->hsn[s];
+      if (r.mode == 0) continue;
+      big.push_back(s);
+      maxsteps = std::max<int64_t>(maxsteps, (r.ns + r.nb - 1) / r.nb);
+    }
+    for (int64_t t = 0; t < maxsteps; ++t) {
+      std::vector<int64_t> act;
+      for (auto s : big) {
+        const SNode& r = h->hsn[s];
+        if (t * r.nb < r.ns) act.push_back(s);
+      }
+      if (act.empty()) continue;
+      max_list = std::max<int64_t>(max_list, (int64_t)act.size());
+      // panel
+      L = Launch();
+      L.kind = K_PANEL;
+      L.step = (int)t;
+      L.off = (int64_t)ilist.size();
+      int64_t Rmax = 1, Wmax = 1;
+      for (auto s : act) {
+        const SNode& r = h->hsn[s];
+        int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
+        int64_t R = r.mode == 1 ? r.ns - kb : w;
+        Rmax = std::max(Rmax, R);
+        Wmax = std::max(Wmax, w);
+        ilist.push_back((int32_t)s);
+      }
+      L.cnt = (int64_t)act.size();
+      L.aux = Rmax;
+      L.aux2 = Wmax;
+      h->fac.push_back(L);
+      // laswp + trsm_u
+      L = Launch();
+      L.kind = K_TRSMU;
+      L.step = (int)t;
+      L.off = (int64_t)ft.size();
+      int64_t wg = 0;
+      for (auto s : act) {
+        const SNode& r = h->hsn[s];
+        int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
+        ft.push_back(FrontTile{(int32_t)s, 0, wg});
+        wg += (M - w + 63) / 64;
+      }
+      L.cnt = (int64_t)act.size();
+      L.nwg = wg;
+      if (wg > 0) h->fac.push_back(L);
+      // trsm_l
+      L = Launch();
+      L.kind = K_TRSML;
+      L.step = (int)t;
+      L.off = (int64_t)ft.size();
+      wg = 0;
+      int64_t W = 32;
+      for (auto s : act) {
+        const SNode& r = h->hsn[s];
+        int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
+        int64_t R = r.mode == 1 ? r.ns - kb : w;
+        ft.push_back(FrontTile{(int32_t)s, 0, wg});
+        wg += (M - kb - R + 255) / 256;
+        W = std::max<int64_t>(W, w);
+      }
+      L.cnt = (int64_t)act.size();
+      L.nwg = wg;
+      L.aux = W;
+      if (wg > 0) h->fac.push_back(L);
+      // trailing update of the pivot part (R1: L panel, R2: U12)
+      L = Launch();
+      L.kind = K_GEMM;
+      L.step = (int)t;
+      L.off = (int64_t)gt.size();
+      int64_t tiles = 0;
+      for (auto s : act) {
+        const SNode& r = h->hsn[s];
+        int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
+        int64_t m1 = M - kb - w, n1 = r.ns - kb - w;
+        if (m1 > 0 && n1 > 0) {
+          GemmTask g{};
+          g.A = store + r.Loff + kb * M + kb + w;
+          g.B = store + r.Loff + (kb + w) * M + kb;
+          g.C = store + r.Loff + (kb + w) * M + kb + w;
+          g.m = (int)m1; g.n = (int)n1; g.k = (int)w;
+          g.lda = (int)M; g.ldb = (int)M; g.ldc = (int)M;
+          g.tiles_m = (int)((m1 + 63) / 64);
+          g.tile0 = tiles;
+          tiles += g.tiles_m * ((n1 + 63) / 64);
+          gt.push_back(g);
+          L.flops += 2.0 * m1 * n1 * w;
+        }
+        int64_t m2 = r.ns - kb - w, n2 = r.nu;
+        if (m2 > 0 && n2 > 0) {
+          GemmTask g{};
+          g.A = store + r.Loff + kb * M + kb + w;
+          g.B = store + r.Uoff + kb;
+          g.C = store + r.Uoff + kb + w;
+          g.m = (int)m2; g.n = (int)n2; g.k = (int)w;
+          g.lda = (int)M; g.ldb = r.ns; g.ldc = r.ns;
+          g.tiles_m = (int)((m2 + 63) / 64);
+          g.tile0 = tiles;
+          tiles += g.tiles_m * ((n2 + 63) / 64);
+          gt.push_back(g);
+          L.flops += 2.0 * m2 * n2 * w;
+        }
+      }
+      L.cnt = (int64_t)gt.size() - L.off;
+      L.nwg = tiles;
+      if (tiles > 0) { h->fac.push_back(L); h->gemm_flops += L.flops; }
+    }
+    // F22 -= L21 * U12 for the blocked fronts of this level
+    {
+      L = Launch();
+      L.kind = K_GEMM;
+      L.step = -1;
+      L.off = (int64_t)gt.size();
+      int64_t tiles = 0;
+      for (auto s : big) {
+        const SNode& r = h->hsn[s];
+        if (r.nu == 0) continue;
+        int64_t M = (int64_t)r.ns + r.nu;
+        GemmTask g{};
+        g.A = store + r.Loff + r.ns;
+        g.B = store + r.Uoff;
+        g.C = scratch + r.Foff;
+        g.m = r.nu; g.n = r.nu; g.k = r.ns;
+        g.lda = (int)M; g.ldb = r.ns; g.ldc = r.nu;
+        g.tiles_m = (r.nu + 63) / 64;
+        g.tile0 = tiles;
+        tiles += (int64_t)g.tiles_m * ((r.nu + 63) / 64);
+        gt.push_back(g);
+        L.flops += 2.0 * r.nu * (double)r.nu * r.ns;
+      }
+      L.cnt = (int64_t)gt.size() - L.off;
+      L.nwg = tiles;
+      if (tiles > 0) { h->fac.push_back(L); h->gemm_flops += L.flops; }
+    }
+  }
+  // solves: one launch per level, all fronts
+  h->fwd.clear();
+  h->bwd.clear();
+  for (int l = 0; l < P.nlevels; ++l) {
+    Launch L;
+    L.kind = K_FWD;
+    L.off = (int64_t)ilist.size();
+    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) ilist.push_back(P.lev_sup[k]);
+    L.cnt = P.lev_ptr[l + 1] - P.lev_ptr[l];
+    h->fwd.push_back(L);
+    L.kind = K_BWD;
+    h->bwd.push_back(L);
+  }
+  std::reverse(h->bwd.begin(), h->bwd.end());
+  h->nlaunch = (int64_t)h->fac.size();
+  // upload
+  HIPCHK(h->sn.upload(h->hsn.data(), h->hsn.size(), st));
+  HIPCHK(h->ilist.upload(ilist.data(), ilist.size(), st));
+  HIPCHK(h->xtasks.upload(xt.data(), xt.size(), st));
+  HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
+  HIPCHK(h->gtasks.upload(gt.data(), gt.size(), st));
+  HIPCHK(h->swaps.alloc((size_t)max_list * kSwapStride));
+  HIPCHK(h->vbuf.alloc((size_t)std::max<int64_t>(voff, 1)));
+  HIPCHK(hipStreamSynchronize(st));
+  return SMLU_OK;
+}
+
+static int setup_device(smlu_handle* h) {
+  Plan& P = h->plan;
+  HIPCHK(hipSetDevice(h->device));
+  if (!h->stream) HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  hipStream_t st = h->stream;
+  HIPCHK(h->A.alloc((size_t)std::max<int64_t>(P.nnzA, 1)));
+  HIPCHK(h->Rs.alloc((size_t)P.n));
+  HIPCHK(h->store.alloc((size_t)std::max<int64_t>(P.factor_size, 1)));
+  HIPCHK(h->scratch.alloc((size_t)std::max<int64_t>(P.scratch_size, 1)));
+  HIPCHK(h->wrk.alloc((size_t)P.n));
+  HIPCHK(h->wrk2.alloc((size_t)P.n));
+  HIPCHK(h->growth.alloc(1));
+  HIPCHK(h->Arowptr.upload(P.Arowptr.data(), P.Arowptr.size(), st));
+  HIPCHK(h->Arow_ent.upload(P.Arow_ent.data(), P.Arow_ent.size(), st));
+  HIPCHK(h->Arow.upload(P.Arow.data(), P.Arow.size(), st));
+  HIPCHK(h->Adest.upload(P.Adest.data(), P.Adest.size(), st));
+  HIPCHK(h->Alev_ent.upload(P.Alev_ent.data(), P.Alev_ent.size(), st));
+  HIPCHK(h->p0.upload(P.p0.data(), P.p0.size(), st));
+  HIPCHK(h->q.upload(P.q.data(), P.q.size(), st));
+  HIPCHK(h->rows.upload(P.s_rows.data(), P.s_rows.size(), st));
+  HIPCHK(h->relmap.upload(P.relmap.data(), P.relmap.size(), st));
+  HIPCHK(h->chlist.upload(P.ch_list.data(), P.ch_list.size(), st));
+  std::vector<int64_t> pf(P.n);
+  for (int64_t s = 0; s < P.nsup; ++s)
+    for (int64_t j = P.s_first[s]; j < P.s_first[s + 1]; ++j) pf[j] = P.s_first[s];
+  HIPCHK(h->posfirst.upload(pf.data(), pf.size(), st));
+  HIPCHK(h->rowperm.alloc((size_t)P.n));
+  {
+    std::vector<int32_t> id(P.n);
+    for (int64_t j = 0; j < P.n; ++j) id[j] = (int32_t)(j - pf[j]);
+    HIPCHK(h->rowperm0.upload(id.data(), id.size(), st));
+  }
+  HIPCHK(h->info.alloc((size_t)std::max<int64_t>(P.nsup, 1)));
+  if (h->hinfo) HIPCHK(hipHostFree(h->hinfo));
+  h->hinfo = nullptr;
+  HIPCHK(hipHostMalloc((void**)&h->hinfo, sizeof(int32_t) * std::max<int64_t>(P.nsup, 1), 0));
+  return build_schedule(h);
+}
+
+// --- event-timed execution (profile mode) ---
+struct Timer {
+  smlu_handle* h;
+  size_t used = 0;
+  explicit Timer(smlu_handle* hh) : h(hh) {}
+  hipError_t begin(int kind, hipEvent_t* stop) {
+    if (!h->opts.profile) { *stop = nullptr; return hipSuccess; }
+    if (used == h->ev_pool.size()) {
+      hipEvent_t a, b;
+      hipError_t e = hipEventCreate(&a);
+      if (e != hipSuccess) return e;
+      e = hipEventCreate(&b);
+      if (e != hipSuccess) return e;
+      h->ev_pool.push_back({a, b});
+      h->ev_kind.push_back(kind);
+    }
+    h->ev_kind[used] = kind;
+    *stop = h->ev_pool[used].second;
+    hipError_t e = hipEventRecord(h->ev_pool[used].first, h->stream);
+    ++used;
+    return e;
+  }
+  hipError_t end(hipEvent_t stop) { return stop ? hipEventRecord(stop, h->stream) : hipSuccess; }
+  void collect() {
+    for (size_t i = 0; i < used; ++i) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, h->ev_pool[i].first, h->ev_pool[i].second) == hipSuccess)
+        h->kind_ms[h->ev_kind[i]] += ms;
+    }
+  }
+};
+
+static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, double piv_tol) {
+  hipStream_t st = h->stream;
+  switch (L.kind) {
+    case K_MEMSET_STORE:
+      return hipMemsetAsync(h->store.p + L.off, 0, (size_t)L.cnt * sizeof(double), st);
+    case K_MEMSET_SCRATCH:
+      return hipMemsetAsync(h->scratch.p + L.off, 0, (size_t)L.cnt * sizeof(double), st);
+    case K_SCATTER:
+      return launch_scatterA(st, L.cnt, h->Alev_ent.p + L.off, h->Adest.p, h->Arow.p, h->A.p, h->Rs.p,
+                             h->store.p, h->scratch.p);
+    case K_EXTADD:
+      return launch_extend_add(st, L.cnt, h->xtasks.p + L.off, h->sn.p, h->relmap.p, h->store.p,
+                               h->scratch.p);
+    case K_FRONT_LDS:
+      return launch_front_lds(st, (int)L.cnt, (int)L.aux, h->ilist.p + L.off, h->sn.p, h->store.p,
+                              h->scratch.p, h->rowperm.p, h->info.p, h->growth.p, diag_tol, piv_tol);
+    case K_PANEL:
+      return launch_panel(st, (int)L.cnt, (int)L.aux, (int)L.aux2, L.step, h->ilist.p + L.off, h->sn.p,
+                          h->store.p, h->scratch.p, h->rowperm.p, h->swaps.p, kSwapStride, h->info.p,
+                          h->growth.p, diag_tol);
+    case K_TRSMU:
+      return launch_laswp_trsm_u(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p, h->store.p,
+                                 h->scratch.p, h->swaps.p, kSwapStride);
+    case K_TRSML:
+      return launch_trsm_l(st, L.nwg, (int)L.aux, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p,
+                           h->store.p, h->scratch.p, h->info.p, h->growth.p, piv_tol);
+    case K_GEMM:
+      return launch_gemm(st, L.nwg, h->gtasks.p + L.off, (int)L.cnt);
+  }
+  return hipErrorInvalidValue;
+}
+
+static int run_factor(smlu_handle* h) {
+  Plan& P = h->plan;
+  hipStream_t st = h->stream;
+  HIPCHK(hipSetDevice(h->device));
+  auto t0 = std::chrono::steady_clock::now();
+  for (auto& v : h->kind_ms) v = 0;
+  Timer tm(h);
+  HIPCHK(hipMemsetAsync(h->info.p, 0, sizeof(int32_t) * std::max<int64_t>(P.nsup, 1), st));
+  HIPCHK(hipMemsetAsync(h->growth.p, 0, sizeof(double), st));
+  // identity (local) row permutation; fronts overwrite their part
+  HIPCHK(hipMemcpyAsync(h->rowperm.p, h->rowperm0.p, sizeof(int32_t) * P.n, hipMemcpyDeviceToDevice, st));
+  if (!h->given_Rs) {
+    if (h->opts.scale) HIPCHK(launch_rowscale(st, P.n, h->Arowptr.p, h->Arow_ent.p, h->A.p, h->Rs.p));
+    else HIPCHK(launch_fill(st, P.n, h->Rs.p, 1.0));
+  }
+  // A given (p, q) order means "no pivoting on top": only a zero diagonal moves.
+  double diag_tol = P.given_order ? 0.0 : h->opts.diag_pivot_tol;
+  double piv_tol = h->opts.pivot_tol;
+  for (const Launch& L : h->fac) {
+    hipEvent_t stop;
+    HIPCHK(tm.begin(L.kind, &stop));
+    HIPCHK(run_launch(h, L, diag_tol, piv_tol));
+    HIPCHK(tm.end(stop));
+  }
+  HIPCHK(hipMemcpyAsync(h->hinfo, h->info.p, sizeof(int32_t) * P.nsup, hipMemcpyDeviceToHost, st));
+  double g = 0;
+  HIPCHK(hipMemcpyAsync(&g, h->growth.p, sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  tm.collect();
+  h->refactor_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  h->growth_max = g;
+  h->have_numeric = true;
+  h->weak = 0;
+  h->errcol = -1;
+  int rc = SMLU_OK;
+  for (int64_t s = 0; s < P.nsup; ++s) {
+    int32_t v = h->hinfo[s];
+    if (v & 2) h->weak++;
+    if ((v & 1) && rc != SMLU_SINGULAR) {
+      rc = SMLU_SINGULAR;
+      h->errcol = P.s_first[s] + ((v >> 2) > 0 ? (v >> 2) - 1 : 0);
+    }
+  }
+  if (rc == SMLU_SINGULAR) h->err = "matrix is singular (zero pivot column)";
+  return rc;
+}
+
+static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode) {
+  // mode 0: ldiv (b -> x); 1: lsolve in place on dx (final order); 2: rsolve in place
+  Plan& P = h->plan;
+  hipStream_t st = h->stream;
+  auto t0 = std::chrono::steady_clock::now();
+  Timer tm(h);
+  hipEvent_t stop;
+  HIPCHK(tm.begin(K_FWD, &stop));
+  double* w = h->wrk.p;
+  if (mode == 0) HIPCHK(launch_perm_in(st, P.n, h->p0.p, h->Rs.p, db, w));
+  if (mode == 1) HIPCHK(launch_unswap(st, P.n, h->posfirst.p, h->rowperm.p, dx, w));
+  if (mode == 2) HIPCHK(hipMemcpyAsync(w, dx, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st));
+  if (mode != 2)
+    for (const Launch& L : h->fwd)
+      HIPCHK(launch_fwd(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->chlist.p, h->relmap.p,
+                        h->rowperm.p, h->store.p, w, h->vbuf.p));
+  if (mode != 1)
+    for (const Launch& L : h->bwd)
+      HIPCHK(launch_bwd(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->rows.p, h->store.p, w, h->vbuf.p));
+  if (mode == 0) HIPCHK(launch_perm_out(st, P.n, h->q.p, w, dx));
+  else HIPCHK(hipMemcpyAsync(dx, w, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st));
+  HIPCHK(tm.end(stop));
+  HIPCHK(hipStreamSynchronize(st));
+  tm.collect();
+  h->solve_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return SMLU_OK;
+}
+
+static bool valid_opts(const smlu_opts* o) { return o && (o->index_base == 0 || o->index_base == 1); }
+
+static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
+                       const int64_t* p, const int64_t* q, const double* Rs, const smlu_opts* opts,
+                       smlu_handle** out) {
+  if (!out) return fail(nullptr, SMLU_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  if (n <= 0 || !colptr || (!rowval && n > 0) || !nzval)
+    return fail(nullptr, SMLU_ERR_ARG, "invalid matrix arguments");
+  std::unique_ptr<smlu_handle> h(new (std::nothrow) smlu_handle());
+  if (!h) return fail(nullptr, SMLU_ERR_ALLOC, "allocation failed");
+  if (opts) h->opts = *opts;
+  else smlu_default_opts(&h->opts);
+  if (!valid_opts(&h->opts)) return fail(nullptr, SMLU_ERR_ARG, "index_base must be 0 or 1");
+  if (h->opts.chunk_size <= 0 || h->opts.chunk_size > n) h->opts.chunk_size = std::min<int64_t>(8, n);
+  int rc = check_device(h.get());
+  if (rc != SMLU_OK) return rc;
+  std::string e;
+  try {
+    e = h->plan.build(n, colptr, rowval, h->opts.index_base, plan_opts(h->opts), p, q);
+  } catch (const std::bad_alloc&) {
+    return fail(nullptr, SMLU_ERR_ALLOC, "host allocation failed during analysis");
+  }
+  if (!e.empty()) return fail(nullptr, SMLU_ERR_ARG, e);
+  rc = setup_device(h.get());
+  if (rc != SMLU_OK) { g_last_error = h->err; return rc; }
+  hipStream_t st = h->stream;
+  {
+    smlu_handle* hp = h.get();
+    smlu_handle* h = hp;  // for HIPCHK
+    HIPCHK(hipMemcpyAsync(h->A.p, nzval, sizeof(double) * h->plan.nnzA, hipMemcpyHostToDevice, st));
+    if (Rs) {
+      HIPCHK(hipMemcpyAsync(h->Rs.p, Rs, sizeof(double) * n, hipMemcpyHostToDevice, st));
+      h->given_Rs = true;
+    }
+  }
+  rc = run_factor(h.get());
+  *out = h.release();
+  return rc;
+}
+
+// =========================================================================================
+// C-ABI
+// =========================================================================================
+extern "C" {
+
+void smlu_default_opts(smlu_opts* o) {
+  if (!o) return;
+  std::memset(o, 0, sizeof(*o));
+  o->chunk_size = 8;
+  o->index_base = 1;
+  o->ordering = SMLU_ORDER_AUTO;
+  o->scale = 1;
+  o->relax = 1;
+  o->pivot_tol = 0.1;
+  o->diag_pivot_tol = 0.1;
+  o->device = 0;
+  o->profile = 0;
+  o->leaf_size = 64;
+}
+
+int smlu_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
+                const smlu_opts* opts, smlu_handle** out) {
+  return create_impl(n, colptr, rowval, nzval, nullptr, nullptr, nullptr, opts, out);
+}
+
+int smlu_create_with_pivots(int64_t n, const int64_t* colptr, const int64_t* rowval,
+                            const double* nzval, const int64_t* p, const int64_t* q,
+                            const double* Rs, const smlu_opts* opts, smlu_handle** out) {
+  if (!p || !q) return fail(nullptr, SMLU_ERR_ARG, "p and q are required");
+  return create_impl(n, colptr, rowval, nzval, p, q, Rs, opts, out);
+}
+
+int smlu_refactor(smlu_handle* h, const double* nzval) {
+  if (!h || !nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipMemcpyAsync(h->A.p, nzval, sizeof(double) * h->plan.nnzA, hipMemcpyHostToDevice, h->stream));
+  return run_factor(h);
+}
+
+int smlu_refactor_device(smlu_handle* h, const double* d_nzval) {
+  if (!h || !d_nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  HIPCHK(hipSetDevice(h->device));
+  if (d_nzval != h->A.p)
+    HIPCHK(hipMemcpyAsync(h->A.p, d_nzval, sizeof(double) * h->plan.nnzA, hipMemcpyDeviceToDevice, h->stream));
+  return run_factor(h);
+}
+
+int smlu_refactor_csc(smlu_handle* h, int64_t n, const int64_t* colptr, const int64_t* rowval,
+                      const double* nzval) {
+  if (!h || !colptr || !rowval || !nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  const Plan& P = h->plan;
+  int base = h->opts.index_base;
+  bool same = (n == P.n);
+  for (int64_t j = 0; same && j <= n; ++j) same = (colptr[j] - base == P.Acolptr[j]);
+  for (int64_t e = 0; same && e < P.nnzA; ++e) same = (rowval[e] - base == P.Arow[e]);
+  if (same) return smlu_refactor(h, nzval);
+  // pattern changed: the reference re-chunks and re-allocates (src/SharedMemSparseLU.jl:265-273);
+  // here: re-analysis and re-allocation in place, keeping the options and the stream.
+  h->release_buffers();
+  h->have_numeric = false;
+  h->given_Rs = false;
+  h->plan = Plan();
+  std::string e;
+  try {
+    e = h->plan.build(n, colptr, rowval, base, plan_opts(h->opts));
+  } catch (const std::bad_alloc&) {
+    return fail(h, SMLU_ERR_ALLOC, "host allocation failed during analysis");
+  }
+  if (!e.empty()) return fail(h, SMLU_ERR_ARG, e);
+  int rc = setup_device(h);
+  if (rc != SMLU_OK) return rc;
+  HIPCHK(hipMemcpyAsync(h->A.p, nzval, sizeof(double) * h->plan.nnzA, hipMemcpyHostToDevice, h->stream));
+  return run_factor(h);
+}
+
+int smlu_solve_device(smlu_handle* h, const double* d_b, double* d_x) {
+  if (!h || !d_b || !d_x) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
+  HIPCHK(hipSetDevice(h->device));
+  return run_solve_dev(h, d_b, d_x, 0);
+}
+
+int smlu_solve(smlu_handle* h, const double* b, double* x) {
+  if (!h || !b || !x) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
+  HIPCHK(hipSetDevice(h->device));
+  int64_t n = h->plan.n;
+  HIPCHK(hipMemcpyAsync(h->wrk2.p, b, sizeof(double) * n, hipMemcpyHostToDevice, h->stream));
+  int rc = run_solve_dev(h, h->wrk2.p, h->wrk2.p, 0);
+  if (rc != SMLU_OK) return rc;
+  HIPCHK(hipMemcpyAsync(x, h->wrk2.p, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return SMLU_OK;
+}
+
+static int tri_solve_host(smlu_handle* h, double* x, int mode) {
+  if (!h || !x) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
+  HIPCHK(hipSetDevice(h->device));
+  int64_t n = h->plan.n;
+  HIPCHK(hipMemcpyAsync(h->wrk2.p, x, sizeof(double) * n, hipMemcpyHostToDevice, h->stream));
+  int rc = run_solve_dev(h, nullptr, h->wrk2.p, mode);
+  if (rc != SMLU_OK) return rc;
+  HIPCHK(hipMemcpyAsync(x, h->wrk2.p, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return SMLU_OK;
+}
+
+int smlu_lsolve(smlu_handle* h, double* x) { return tri_solve_host(h, x, 1); }
+int smlu_rsolve(smlu_handle* h, double* x) { return tri_solve_host(h, x, 2); }
+
+// ---- factor export ------------------------------------------------------------------
+struct Exported {
+  std::vector<int64_t> Lp, Li, Up, Ui, p, q;
+  std::vector<double> Lx, Ux;
+};
+
+static int export_factors(smlu_handle* h, Exported& X, bool values) {
+  const Plan& P = h->plan;
+  const int64_t n = P.n;
+  std::vector<double> store;
+  if (values) {
+    store.resize((size_t)P.factor_size);
+    HIPCHK(hipMemcpy(store.data(), h->store.p, sizeof(double) * P.factor_size, hipMemcpyDeviceToHost));
+  }
+  std::vector<int32_t> rp(n);
+  HIPCHK(hipMemcpy(rp.data(), h->rowperm.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  // final position of pre-swap position g: first + inv(rowperm)[g - first]
+  std::vector<int64_t> fin(n);
+  std::vector<char> swapped(P.nsup, 0);
+  for (int64_t s = 0; s < P.nsup; ++s) {
+    int64_t f = P.s_first[s];
+    for (int64_t i = f; i < P.s_first[s + 1]; ++i) {
+      fin[f + rp[i]] = i;
+      if (rp[i] != i - f) swapped[s] = 1;
+    }
+  }
+  X.p.resize(n);
+  X.q.assign(P.q.begin(), P.q.end());
+  for (int64_t s = 0; s < P.nsup; ++s) {
+    int64_t f = P.s_first[s];
+    for (int64_t i = f; i < P.s_first[s + 1]; ++i) X.p[i] = P.p0[f + rp[i]];
+  }
+  // Row lists per column (L) in final positions with values; U by rows then transposed.
+  X.Lp.assign(n + 1, 0);
+  std::vector<int64_t> Ucnt(n + 1, 0);
+  struct Ent { int64_t r; double v; };
+  std::vector<std::vector<Ent>> Lcols(n), Urows(n);
+  for (int64_t s = 0; s < P.nsup; ++s) {
+    const int64_t f = P.s_first[s], ns = P.ns(s), nu = P.nu(s), M = ns + nu;
+    const int32_t* R = P.s_rows.data() + P.s_rowptr[s];
+    const double* Lpn = values ? store.data() + P.Loff[s] : nullptr;
+    const double* U12 = values ? store.data() + P.Uoff[s] : nullptr;
+    for (int64_t jj = 0; jj < ns; ++jj) {
+      const int64_t j = f + jj;
+      // structure of column j: exact (t-supernode) unless this front swapped rows
+      int64_t last_own;
+      const int32_t* Rb;
+      int64_t Rn;
+      if (!swapped[s]) {
+        int64_t t = P.col2t[j];
+        last_own = P.t_first[t + 1] - 1;
+        Rb = P.t_rows.data() + P.t_rowptr[t];
+        Rn = P.t_rowptr[t + 1] - P.t_rowptr[t];
+      } else {
+        last_own = f + ns - 1;
+        Rb = R;
+        Rn = nu;
+      }
+      auto& Lc = Lcols[j];
+      Lc.reserve((size_t)(last_own - j + 1 + Rn));
+      Lc.push_back({j, 1.0});
+      for (int64_t i = j + 1; i <= last_own; ++i) {
+        double v = values ? Lpn[jj * M + (i - f)] : 0.0;
+        Lc.push_back({i, v});
+      }
+      // update rows: local index in front = ns + position in R_s
+      int64_t k = 0;
+      for (int64_t e = 0; e < Rn; ++e) {
+        int64_t g = Rb[e];
+        if (g <= f + ns - 1) {  // (exact structure may list rows inside the relaxed supernode)
+          double v = values ? Lpn[jj * M + (g - f)] : 0.0;
+          Lc.push_back({g, v});  // own positions: already final
+          continue;
+        }
+        while (R[k] < g) ++k;
+        double v = values ? Lpn[jj * M + ns + k] : 0.0;
+        Lc.push_back({fin[g], v});
+      }
+      // U row j: diag block columns j..last_own and update columns
+      auto& Ur = Urows[j];
+      for (int64_t c = j; c <= last_own; ++c) {
+        double v = values ? Lpn[(c - f) * M + jj] : 0.0;
+        Ur.push_back({c, v});
+      }
+      k = 0;
+      for (int64_t e = 0; e < Rn; ++e) {
+        int64_t g = Rb[e];
+        if (g <= f + ns - 1) {
+          double v = values ? Lpn[(g - f) * M + jj] : 0.0;
+          Ur.push_back({g, v});
+          continue;
+        }
+        while (R[k] < g) ++k;
+        double v = values ? U12[k * ns + jj] : 0.0;
+        Ur.push_back({g, v});
+      }
+    }
+  }
+  for (int64_t j = 0; j < n; ++j) {
+    auto& c = Lcols[j];
+    std::sort(c.begin() + 1, c.end(), [](const Ent& a, const Ent& b) { return a.r < b.r; });
+    X.Lp[j + 1] = X.Lp[j] + (int64_t)c.size();
+  }
+  X.Li.resize(X.Lp[n]);
+  X.Lx.resize(X.Lp[n]);
+  for (int64_t j = 0; j < n; ++j) {
+    int64_t o = X.Lp[j];
+    for (auto& e : Lcols[j]) { X.Li[o] = e.r; X.Lx[o] = e.v; ++o; }
+  }
+  // U: transpose rows -> CSC columns; rows within a column come out sorted (row-major sweep)
+  for (int64_t i = 0; i < n; ++i)
+    for (auto& e : Urows[i]) Ucnt[e.r + 1]++;
+  X.Up.assign(n + 1, 0);
+  for (int64_t j = 0; j < n; ++j) X.Up[j + 1] = X.Up[j] + Ucnt[j + 1];
+  X.Ui.resize(X.Up[n]);
+  X.Ux.resize(X.Up[n]);
+  std::vector<int64_t> pos(X.Up.begin(), X.Up.end() - 1);
+  for (int64_t i = 0; i < n; ++i)
+    for (auto& e : Urows[i]) {
+      X.Ui[pos[e.r]] = i;
+      X.Ux[pos[e.r]] = e.v;
+      pos[e.r]++;
+    }
+  return SMLU_OK;
+}
+
+int smlu_get_sizes(smlu_handle* h, int64_t* n, int64_t* nnzL, int64_t* nnzU) {
+  if (!h) return fail(h, SMLU_ERR_ARG, "NULL handle");
+  Exported X;
+  int rc = export_factors(h, X, false);
+  if (rc != SMLU_OK) return rc;
+  if (n) *n = h->plan.n;
+  if (nnzL) *nnzL = X.Lp[h->plan.n];
+  if (nnzU) *nnzU = X.Up[h->plan.n];
+  return SMLU_OK;
+}
+
+int smlu_get_factors(smlu_handle* h, int64_t* Lcolptr, int64_t* Lrowval, double* Lnzval,
+                     int64_t* Ucolptr, int64_t* Urowval, double* Unzval, int64_t* p, int64_t* q,
+                     double* Rs) {
+  if (!h) return fail(h, SMLU_ERR_ARG, "NULL handle");
+  if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  Exported X;
+  int rc = export_factors(h, X, true);
+  if (rc != SMLU_OK) return rc;
+  const int64_t n = h->plan.n, b = h->opts.index_base;
+  if (Lcolptr) for (int64_t j = 0; j <= n; ++j) Lcolptr[j] = X.Lp[j] + b;
+  if (Lrowval) for (size_t e = 0; e < X.Li.size(); ++e) Lrowval[e] = X.Li[e] + b;
+  if (Lnzval) std::memcpy(Lnzval, X.Lx.data(), sizeof(double) * X.Lx.size());
+  if (Ucolptr) for (int64_t j = 0; j <= n; ++j) Ucolptr[j] = X.Up[j] + b;
+  if (Urowval) for (size_t e = 0; e < X.Ui.size(); ++e) Urowval[e] = X.Ui[e] + b;
+  if (Unzval) std::memcpy(Unzval, X.Ux.data(), sizeof(double) * X.Ux.size());
+  if (p) for (int64_t i = 0; i < n; ++i) p[i] = X.p[i] + b;
+  if (q) for (int64_t i = 0; i < n; ++i) q[i] = X.q[i] + b;
+  if (Rs) HIPCHK(hipMemcpy(Rs, h->Rs.p, sizeof(double) * n, hipMemcpyDeviceToHost));
+  return SMLU_OK;
+}
+
+void smlu_destroy(smlu_handle* h) { delete h; }
+
+const char* smlu_last_error_string(const smlu_handle* h) {
+  if (h) return h->err.c_str();
+  return g_last_error.c_str();
+}
+
+int64_t smlu_last_error_col(const smlu_handle* h) { return h ? h->errcol : -1; }
+
+static double plan_stat(const Plan& P, const std::string& k) {
+  if (k == "n") return (double)P.n;
+  if (k == "nnzA") return (double)P.nnzA;
+  if (k == "nsuper") return (double)P.nsup;
+  if (k == "ntsuper") return (double)P.ntsup;
+  if (k == "nlevels") return (double)P.nlevels;
+  if (k == "nnzL") return P.nnzL;
+  if (k == "nnzU") return P.nnzU;
+  if (k == "nnzLU") return P.nnzL + P.nnzU - (double)P.n;  // one diagonal (U's) + unit L diag stored
+  if (k == "upd") return P.upd;
+  if (k == "dense_flops") return P.flops;
+  if (k == "stored") return P.stored;
+  if (k == "front_max") return (double)P.front_max;
+  if (k == "ns_max") return (double)P.ns_max;
+  if (k == "nu_max") return (double)P.nu_max;
+  if (k == "factor_bytes") return 8.0 * (double)P.factor_size;
+  if (k == "scratch_bytes") return 8.0 * (double)P.scratch_size;
+  if (k == "analysis_ms") return P.analysis_ms;
+  return std::numeric_limits<double>::quiet_NaN();
+}
+
+double smlu_stat(const smlu_handle* h, const char* key) {
+  if (!h || !key) return std::numeric_limits<double>::quiet_NaN();
+  std::string k(key);
+  if (k == "launches") return (double)h->nlaunch;
+  if (k == "refactor_ms_last") return h->refactor_ms;
+  if (k == "solve_ms_last") return h->solve_ms;
+  if (k == "growth_max") return h->growth_max;
+  if (k == "weak") return (double)h->weak;
+  if (k == "gemm_flops") return h->gemm_flops;
+  if (k.rfind("ms_", 0) == 0) {
+    std::string name = k.substr(3);
+    double t = 0;
+    bool found = false;
+    for (int i = 0; i < K_NKIND; ++i)
+      if (name == kKindName[i]) { t += h->kind_ms[i]; found = true; }
+    return found ? t : std::numeric_limits<double>::quiet_NaN();
+  }
+  return plan_stat(h->plan, k);
+}
+
+int smlu_plan_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const smlu_opts* opts,
+                     smlu_plan** out) {
+  if (!out || !colptr || n <= 0) return fail(nullptr, SMLU_ERR_ARG, "invalid arguments");
+  smlu_opts o;
+  if (opts) o = *opts;
+  else smlu_default_opts(&o);
+  if (!valid_opts(&o)) return fail(nullptr, SMLU_ERR_ARG, "index_base must be 0 or 1");
+  std::unique_ptr<smlu_plan> p(new smlu_plan());
+  std::string e = p->plan.build(n, colptr, rowval, o.index_base, plan_opts(o));
+  if (!e.empty()) return fail(nullptr, SMLU_ERR_ARG, e);
+  *out = p.release();
+  return SMLU_OK;
+}
+
+double smlu_plan_stat(const smlu_plan* plan, const char* key) {
+  if (!plan || !key) return std::numeric_limits<double>::quiet_NaN();
+  return plan_stat(plan->plan, key);
+}
+
+int smlu_plan_pattern(const smlu_plan* pl, int64_t* q, int64_t* Lcolptr, int64_t* Lrowval) {
+  if (!pl) return SMLU_ERR_ARG;
+  const Plan& P = pl->plan;
+  if (q) for (int64_t i = 0; i < P.n; ++i) q[i] = P.q[i];
+  if (Lcolptr || Lrowval) {
+    int64_t o = 0;
+    if (Lcolptr) Lcolptr[0] = 0;
+    for (int64_t j = 0; j < P.n; ++j) {
+      int64_t t = P.col2t[j], last = P.t_first[t + 1] - 1;
+      if (Lrowval) {
+        for (int64_t i = j; i <= last; ++i) Lrowval[o++] = i;
+        for (int64_t e = P.t_rowptr[t]; e < P.t_rowptr[t + 1]; ++e) Lrowval[o++] = P.t_rows[e];
+      } else {
+        o += last - j + 1 + P.t_rowptr[t + 1] - P.t_rowptr[t];
+      }
+      if (Lcolptr) Lcolptr[j + 1] = o;
+    }
+  }
+  return SMLU_OK;
+}
+
+int smlu_plan_supernodes(const smlu_plan* pl, int64_t* first, int64_t* parent, int64_t* level) {
+  if (!pl) return SMLU_ERR_ARG;
+  const Plan& P = pl->plan;
+  for (int64_t s = 0; s <= P.nsup; ++s)
+    if (first) first[s] = P.s_first[s];
+  for (int64_t s = 0; s < P.nsup; ++s) {
+    if (parent) parent[s] = P.s_parent[s];
+    if (level) level[s] = P.s_level[s];
+  }
+  return SMLU_OK;
+}
+
+void smlu_plan_destroy(smlu_plan* p) { delete p; }
+
+const char* smlu_version(void) { return "smlu 0.1.0 (gfx950, fp64, multifrontal)"; }
+
+}  // extern "C"

@@ -1,0 +1,129 @@
+"""ctypes binding of libsmlu.so (C-ABI declared in include/smlu.h).
+
+No torch types cross this boundary: plain pointers and int64 sizes, as a Julia ``ccall``
+shim would bind them.  The product never falls back to the CPU: if the
+library is missing, or no gfx950 device is visible, calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # sharedmemsparselu.jl_amd/
+LIB_PATH = os.path.join(_PKG, "libsmlu.so")
+
+i64 = ctypes.c_int64
+i32 = ctypes.c_int32
+f64 = ctypes.c_double
+i64p = ctypes.POINTER(ctypes.c_int64)
+f64p = ctypes.POINTER(ctypes.c_double)
+vp = ctypes.c_void_p
+
+SMLU_OK = 0
+SMLU_SINGULAR = 1
+SMLU_PIVOT_WEAK = 2
+SMLU_ERR_ARG = -1
+SMLU_ERR_PATTERN = -2
+SMLU_ERR_ALLOC = -3
+SMLU_ERR_HIP = -4
+SMLU_ERR_NODEVICE = -5
+SMLU_ERR_STATE = -6
+
+ORDER_AUTO, ORDER_NATURAL, ORDER_GEOMETRIC_ND, ORDER_GRAPH_ND, ORDER_GIVEN = range(5)
+
+
+class SmluOpts(ctypes.Structure):
+    _fields_ = [
+        ("chunk_size", i64),
+        ("index_base", i32),
+        ("ordering", i32),
+        ("grid", i64 * 3),
+        ("scale", i32),
+        ("relax", i32),
+        ("pivot_tol", f64),
+        ("diag_pivot_tol", f64),
+        ("device", i32),
+        ("profile", i32),
+        ("leaf_size", i64),
+    ]
+
+
+# exported symbols and their signatures (restype, argtypes); the CPU test-suite checks that
+# every function declared in include/smlu.h is present here and in the .so
+SIGNATURES = {
+    "smlu_default_opts": (None, [ctypes.POINTER(SmluOpts)]),
+    "smlu_create": (i32, [i64, vp, vp, vp, ctypes.POINTER(SmluOpts), ctypes.POINTER(vp)]),
+    "smlu_create_with_pivots": (i32, [i64, vp, vp, vp, vp, vp, vp, ctypes.POINTER(SmluOpts),
+                                      ctypes.POINTER(vp)]),
+    "smlu_refactor": (i32, [vp, vp]),
+    "smlu_refactor_device": (i32, [vp, vp]),
+    "smlu_refactor_csc": (i32, [vp, i64, vp, vp, vp]),
+    "smlu_solve": (i32, [vp, vp, vp]),
+    "smlu_solve_device": (i32, [vp, vp, vp]),
+    "smlu_lsolve": (i32, [vp, vp]),
+    "smlu_rsolve": (i32, [vp, vp]),
+    "smlu_get_sizes": (i32, [vp, i64p, i64p, i64p]),
+    "smlu_get_factors": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "smlu_destroy": (None, [vp]),
+    "smlu_last_error_string": (ctypes.c_char_p, [vp]),
+    "smlu_last_error_col": (i64, [vp]),
+    "smlu_stat": (f64, [vp, ctypes.c_char_p]),
+    "smlu_plan_create": (i32, [i64, vp, vp, ctypes.POINTER(SmluOpts), ctypes.POINTER(vp)]),
+    "smlu_plan_stat": (f64, [vp, ctypes.c_char_p]),
+    "smlu_plan_pattern": (i32, [vp, vp, vp, vp]),
+    "smlu_plan_supernodes": (i32, [vp, vp, vp, vp]),
+    "smlu_plan_destroy": (None, [vp]),
+    "smlu_version": (ctypes.c_char_p, []),
+}
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile libsmlu.so in-tree (hipcc --offload-arch=gfx950)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.check_call(["make", "-s", "-j8", "-C", _PKG])
+    return LIB_PATH
+
+
+def lib():
+    """Load libsmlu.so; raise (never fall back) when it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libsmlu.so not found at {LIB_PATH}; build it with `make -C {_PKG}` "
+                "(there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def default_opts(**kw) -> SmluOpts:
+    o = SmluOpts()
+    lib().smlu_default_opts(ctypes.byref(o))
+    for k, v in kw.items():
+        if k == "grid":
+            g = list(v) + [0] * (3 - len(v))
+            for i in range(3):
+                o.grid[i] = int(g[i])
+        else:
+            setattr(o, k, v)
+    return o
+
+
+def ptr(a):
+    """Raw data pointer of a numpy array (None for None)."""
+    if a is None:
+        return None
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def last_error(h=None) -> str:
+    s = lib().smlu_last_error_string(h)
+    return s.decode() if s else ""

@@ -1,0 +1,258 @@
+"""Python mirror of the reference's Julia surface (SharedMemSparseLU.jl, src/SharedMemSparseLU.jl).
+
+Julia name                          here                          reference
+----------------------------------  ----------------------------  -----------------------
+ParallelSparseLU(A, chunk_size)     ParallelSparseLU(A, cs)       :64-98
+lu!(F, A)                           lu_(F, A)                     :245-279
+ldiv!(x, F, b)                      ldiv_(x, F, b)                :286-342
+lsolve!(F, x), rsolve!(F, x)        lsolve_(F, x), rsolve_(F, x)  :349-392
+F.L F.U F.p F.q F.Rs                F.L F.U F.p F.q F.Rs          :45-52 (0-based here)
+cleanup_ParallelSparseLU!(F)        cleanup_ParallelSparseLU_(F)  :31 (exported, undefined there)
+DimensionMismatch                   DimensionMismatch             :288-290
+SingularException (UMFPACK)         SingularException             :74 / :247
+
+All numerics run on the MI355X through libsmlu.so; nothing here computes factors or solves.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import scipy.sparse as sp
+
+from . import _lib as C
+
+
+class DimensionMismatch(ValueError):
+    """Julia's DimensionMismatch (src/SharedMemSparseLU.jl:288-290)."""
+
+
+class SingularException(np.linalg.LinAlgError):
+    """UMFPACK's SingularException raised by lu(A)/lu!(F, A) with check=true."""
+
+    def __init__(self, col):
+        super().__init__(f"matrix is singular: zero pivot at column {col}")
+        self.info = col
+
+
+class SmluError(RuntimeError):
+    pass
+
+
+def _csc(A):
+    if not sp.issparse(A):
+        A = sp.csc_matrix(np.asarray(A, dtype=np.float64))
+    A = sp.csc_matrix(A, dtype=np.float64)
+    if not A.has_sorted_indices:
+        A = A.sorted_indices()
+    A.sum_duplicates()
+    return A
+
+
+def _check(rc, h=None):
+    if rc < 0:
+        raise SmluError(f"libsmlu error {rc}: {C.last_error(h)}")
+    return rc
+
+
+class ParallelSparseLU:
+    """LU factorisation of a square sparse matrix on the MI355X.
+
+    ``F.L * F.U == (F.Rs[:, None] * A)[F.p][:, F.q]`` (UMFPACK's relation quoted at
+    src/SharedMemSparseLU.jl:305-316), with 0-based ``p``/``q``.
+    """
+
+    def __init__(self, A, chunk_size=None, *, ordering="auto", grid=None, device=0,
+                 profile=False, p=None, q=None, Rs=None, pivot_tol=None, diag_pivot_tol=None,
+                 leaf_size=None, relax=True):
+        A = _csc(A)
+        m, n = A.shape
+        if m != n:
+            raise DimensionMismatch(f"matrix is not square: {m} x {n}")
+        if chunk_size is None:
+            chunk_size = 8                       # :67-70
+        chunk_size = min(int(chunk_size), n)     # :72
+        order = {"auto": C.ORDER_AUTO, "natural": C.ORDER_NATURAL, "nd": C.ORDER_GRAPH_ND,
+                 "geometric": C.ORDER_GEOMETRIC_ND, "given": C.ORDER_GIVEN}[ordering]
+        kw = dict(chunk_size=chunk_size, index_base=0, ordering=order, device=device,
+                  profile=1 if profile else 0, relax=1 if relax else 0)
+        if grid is not None:
+            kw["grid"] = grid
+            if ordering == "auto":
+                kw["ordering"] = C.ORDER_GEOMETRIC_ND
+        if pivot_tol is not None:
+            kw["pivot_tol"] = float(pivot_tol)
+        if diag_pivot_tol is not None:
+            kw["diag_pivot_tol"] = float(diag_pivot_tol)
+        if leaf_size is not None:
+            kw["leaf_size"] = int(leaf_size)
+        self._opts = C.default_opts(**kw)
+        self.m, self.n = m, n
+        self.chunk_size = chunk_size
+        self._colptr = np.ascontiguousarray(A.indptr, dtype=np.int64)
+        self._rowval = np.ascontiguousarray(A.indices, dtype=np.int64)
+        vals = np.ascontiguousarray(A.data, dtype=np.float64)
+        h = ctypes.c_void_p()
+        L = C.lib()
+        if p is not None or q is not None:
+            pp = np.ascontiguousarray(p, dtype=np.int64)
+            qq = np.ascontiguousarray(q, dtype=np.int64)
+            rs = None if Rs is None else np.ascontiguousarray(Rs, dtype=np.float64)
+            rc = L.smlu_create_with_pivots(n, C.ptr(self._colptr), C.ptr(self._rowval), C.ptr(vals),
+                                           C.ptr(pp), C.ptr(qq), C.ptr(rs), ctypes.byref(self._opts),
+                                           ctypes.byref(h))
+        else:
+            rc = L.smlu_create(n, C.ptr(self._colptr), C.ptr(self._rowval), C.ptr(vals),
+                               ctypes.byref(self._opts), ctypes.byref(h))
+        if rc < 0:
+            raise SmluError(f"smlu_create failed ({rc}): {C.last_error(None)}")
+        self._h = h
+        self._factors = None
+        if rc == C.SMLU_SINGULAR:
+            col = L.smlu_last_error_col(h)
+            self.close()
+            raise SingularException(col)
+
+    # ---- factor access (F.L, F.U, F.p, F.q, F.Rs) ----
+    def _download(self):
+        if self._factors is None:
+            L = C.lib()
+            n = self.n
+            nl, nu = ctypes.c_int64(), ctypes.c_int64()
+            _check(L.smlu_get_sizes(self._h, None, ctypes.byref(nl), ctypes.byref(nu)), self._h)
+            Lp = np.empty(n + 1, np.int64); Li = np.empty(nl.value, np.int64); Lx = np.empty(nl.value)
+            Up = np.empty(n + 1, np.int64); Ui = np.empty(nu.value, np.int64); Ux = np.empty(nu.value)
+            p = np.empty(n, np.int64); q = np.empty(n, np.int64); Rs = np.empty(n)
+            _check(L.smlu_get_factors(self._h, C.ptr(Lp), C.ptr(Li), C.ptr(Lx), C.ptr(Up), C.ptr(Ui),
+                                      C.ptr(Ux), C.ptr(p), C.ptr(q), C.ptr(Rs)), self._h)
+            self._factors = dict(L=sp.csc_matrix((Lx, Li, Lp), shape=(n, n)),
+                                 U=sp.csc_matrix((Ux, Ui, Up), shape=(n, n)), p=p, q=q, Rs=Rs)
+        return self._factors
+
+    @property
+    def L(self):
+        return self._download()["L"]
+
+    @property
+    def U(self):
+        return self._download()["U"]
+
+    @property
+    def p(self):
+        return self._download()["p"]
+
+    @property
+    def q(self):
+        return self._download()["q"]
+
+    @property
+    def Rs(self):
+        return self._download()["Rs"]
+
+    def stat(self, key):
+        return C.lib().smlu_stat(self._h, key.encode())
+
+    # ---- device-resident entry points (values / vectors already in HBM) ----
+    def refactor_device(self, d_values):
+        """lu! with values already on the device (torch tensor or raw pointer int)."""
+        ptr = d_values.data_ptr() if hasattr(d_values, "data_ptr") else int(d_values)
+        rc = _check(C.lib().smlu_refactor_device(self._h, ctypes.c_void_p(ptr)), self._h)
+        self._factors = None
+        if rc == C.SMLU_SINGULAR:
+            raise SingularException(C.lib().smlu_last_error_col(self._h))
+        return rc
+
+    def solve_device(self, d_x, d_b):
+        px = d_x.data_ptr() if hasattr(d_x, "data_ptr") else int(d_x)
+        pb = d_b.data_ptr() if hasattr(d_b, "data_ptr") else int(d_b)
+        return _check(C.lib().smlu_solve_device(self._h, ctypes.c_void_p(pb), ctypes.c_void_p(px)),
+                      self._h)
+
+    def close(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            C.lib().smlu_destroy(h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __repr__(self):
+        return f"ParallelSparseLU(n={self.n}, nnz(L+U)={self.stat('nnzLU'):.0f})"
+
+
+def lu_(F: ParallelSparseLU, A):
+    """lu!(F, A) — src/SharedMemSparseLU.jl:245-279.  Same pattern: numeric refactor on the
+    GPU; different pattern: re-analysis (the reference's reallocate branch, :252-273)."""
+    A = _csc(A)
+    if A.shape != (F.m, F.n):
+        raise DimensionMismatch(f"A has size {A.shape}, F has size {(F.m, F.n)}")
+    vals = np.ascontiguousarray(A.data, dtype=np.float64)
+    L = C.lib()
+    same = (A.nnz == F._rowval.size and np.array_equal(A.indptr, F._colptr)
+            and np.array_equal(A.indices, F._rowval))
+    if same:
+        rc = L.smlu_refactor(F._h, C.ptr(vals))
+    else:
+        F._colptr = np.ascontiguousarray(A.indptr, dtype=np.int64)
+        F._rowval = np.ascontiguousarray(A.indices, dtype=np.int64)
+        rc = L.smlu_refactor_csc(F._h, F.n, C.ptr(F._colptr), C.ptr(F._rowval), C.ptr(vals))
+    F._factors = None
+    _check(rc, F._h)
+    if rc == C.SMLU_SINGULAR:
+        raise SingularException(L.smlu_last_error_col(F._h))
+    return None
+
+
+def ldiv_(x, F: ParallelSparseLU, b):
+    """ldiv!(x, F, b) — src/SharedMemSparseLU.jl:286-342.  ``x is b`` is allowed."""
+    if F.m != F.n:
+        raise DimensionMismatch(f"`F` is not square: F.m={F.m}, F.n={F.n}")
+    if len(x) != F.n:
+        raise DimensionMismatch(f"`x` does not have same size as F: length(x)={len(x)}, F.n={F.n}")
+    if len(b) != F.n:
+        raise DimensionMismatch(f"`b` does not have same size as F: length(b)={len(b)}, F.n={F.n}")
+    bb = np.ascontiguousarray(b, dtype=np.float64)
+    xx = x if (isinstance(x, np.ndarray) and x.dtype == np.float64 and x.flags.c_contiguous) \
+        else np.empty(F.n)
+    _check(C.lib().smlu_solve(F._h, C.ptr(bb), C.ptr(xx)), F._h)
+    if xx is not x:
+        x[:] = xx
+    return x
+
+
+def _tri(F, x, which):
+    if len(x) != F.n:
+        raise DimensionMismatch(f"`x` does not have same size as F: length(x)={len(x)}, F.n={F.n}")
+    xx = x if (isinstance(x, np.ndarray) and x.dtype == np.float64 and x.flags.c_contiguous) \
+        else np.ascontiguousarray(x, dtype=np.float64)
+    fn = C.lib().smlu_lsolve if which == "L" else C.lib().smlu_rsolve
+    _check(fn(F._h, C.ptr(xx)), F._h)
+    if xx is not x:
+        x[:] = xx
+    return None
+
+
+def lsolve_(F: ParallelSparseLU, x):
+    """lsolve!(F, x) — src/SharedMemSparseLU.jl:349-367: in place ``L \\ x``."""
+    return _tri(F, x, "L")
+
+
+def rsolve_(F: ParallelSparseLU, x):
+    """rsolve!(F, x) — src/SharedMemSparseLU.jl:374-392: in place ``U \\ x``."""
+    return _tri(F, x, "U")
+
+
+def cleanup_ParallelSparseLU_(F: ParallelSparseLU):
+    """cleanup_ParallelSparseLU!(F) — exported but undefined in the reference (:31); here it
+    releases the device memory, stream and host plan of F."""
+    F.close()
+
+
+def allocate_shared(T, *dims):
+    """allocate_shared — exported but undefined in the reference (:31).  There are no MPI
+    shared-memory windows on the GPU path; this returns a zeroed host array of the shape."""
+    return np.zeros(dims, dtype=T)

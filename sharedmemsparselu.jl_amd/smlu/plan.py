@@ -1,0 +1,68 @@
+"""Host-only access to the symbolic plan (no GPU needed): ordering, supernodes, levels and the
+structural pattern of L.  Used by the CPU test-suite and by bench.py for algorithmic byte and
+flop counts."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import scipy.sparse as sp
+
+from . import _lib as C
+
+
+class Plan:
+    def __init__(self, A, ordering="auto", grid=None, relax=True, leaf_size=None):
+        A = sp.csc_matrix(A, dtype=np.float64)
+        A.sort_indices()
+        A.sum_duplicates()
+        n = A.shape[0]
+        order = {"auto": C.ORDER_AUTO, "natural": C.ORDER_NATURAL, "nd": C.ORDER_GRAPH_ND,
+                 "geometric": C.ORDER_GEOMETRIC_ND}[ordering]
+        kw = dict(index_base=0, ordering=order, relax=1 if relax else 0)
+        if grid is not None:
+            kw["grid"] = grid
+            if ordering == "auto":
+                kw["ordering"] = C.ORDER_GEOMETRIC_ND
+        if leaf_size is not None:
+            kw["leaf_size"] = int(leaf_size)
+        o = C.default_opts(**kw)
+        self.n = n
+        cp = np.ascontiguousarray(A.indptr, dtype=np.int64)
+        ri = np.ascontiguousarray(A.indices, dtype=np.int64)
+        h = ctypes.c_void_p()
+        rc = C.lib().smlu_plan_create(n, C.ptr(cp), C.ptr(ri), ctypes.byref(o), ctypes.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"smlu_plan_create failed ({rc}): {C.last_error(None)}")
+        self._h = h
+
+    def stat(self, key):
+        return C.lib().smlu_plan_stat(self._h, key.encode())
+
+    def q(self):
+        q = np.empty(self.n, np.int64)
+        C.lib().smlu_plan_pattern(self._h, C.ptr(q), None, None)
+        return q
+
+    def L_pattern(self):
+        n = self.n
+        Lp = np.empty(n + 1, np.int64)
+        C.lib().smlu_plan_pattern(self._h, None, C.ptr(Lp), None)
+        Li = np.empty(Lp[-1], np.int64)
+        C.lib().smlu_plan_pattern(self._h, None, C.ptr(Lp), C.ptr(Li))
+        return sp.csc_matrix((np.ones(Li.size), Li, Lp), shape=(n, n))
+
+    def supernodes(self):
+        ns = int(self.stat("nsuper"))
+        first = np.empty(ns + 1, np.int64)
+        parent = np.empty(ns, np.int64)
+        level = np.empty(ns, np.int64)
+        C.lib().smlu_plan_supernodes(self._h, C.ptr(first), C.ptr(parent), C.ptr(level))
+        return first, parent, level
+
+    def __del__(self):
+        try:
+            if self._h:
+                C.lib().smlu_plan_destroy(self._h)
+        except Exception:
+            pass

@@ -1,0 +1,140 @@
+"""GPU parity tests: libsmlu.so (HIP, gfx950) against the CPU oracle (oracle/) and against
+independent solvers, at the reference's tolerances (test/runtests.jl:25-26)."""
+import numpy as np
+import pytest
+import scipy.linalg as sla
+import scipy.sparse as sp
+import scipy.sparse.linalg as spla
+
+import oracle as O
+import smlu
+from smlu import matrices as mats
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1.0e-12
+DENSE_TOL = 1.0e-10
+
+
+def isapprox(x, y, rtol, atol):
+    """Julia's isapprox for vectors: norm(x-y) <= max(atol, rtol*max(norm(x), norm(y)))."""
+    return np.linalg.norm(x - y) <= max(atol, rtol * max(np.linalg.norm(x), np.linalg.norm(y)))
+
+
+def factor_parity(A, F, rtol=1e-12):
+    """Exported factors vs the oracle's fixed-pivot LU with the GPU's own (p, q)."""
+    p, q, Rs = F.p, F.q, F.Rs
+    Ro = O.rowscale(A)
+    assert np.array_equal(Rs, Ro), "row scaling must be bitwise identical"
+    ref = O.OracleLU(A, p, q, Ro)
+    assert ref.status == 0
+    L, U = F.L, F.U
+    for G, R in ((L, ref.L), (U, ref.U)):
+        G = sp.csc_matrix(G); R = sp.csc_matrix(R)
+        # pattern: oracle's structural fill must be contained; extras hold exact zeros
+        Gp = G.copy(); Gp.data[:] = 1
+        Rp = R.copy(); Rp.data[:] = 1
+        missing = (Rp - Gp.multiply(Rp))
+        assert missing.count_nonzero() == 0, "GPU pattern misses structural entries"
+        extra = G - G.multiply(Rp)
+        assert extra.count_nonzero() == 0, "entries outside the structural pattern must be 0"
+        D = (G - R)
+        scale = max(abs(R).max(), 1.0)
+        assert abs(D).max() <= rtol * scale, f"factor mismatch {abs(D).max()} (scale {scale})"
+    # UMFPACK contract L*U == (Rs.*A)[p,q]
+    B = (sp.diags(Rs) @ A).tocsr()[p][:, q]
+    E = L @ U - B
+    assert abs(E).max() <= 1e-10 * max(abs(B).max(), 1.0)
+    return ref
+
+
+@pytest.mark.parametrize("N", [4, 10, 23])
+def test_poisson2d_factors_identical_pattern(gpu, N):
+    A = mats.poisson2d(N)
+    F = smlu.ParallelSparseLU(A)
+    factor_parity(A, F)
+    # diagonally dominant M-matrix: pivot order = column order (no swaps)
+    assert np.array_equal(F.p, F.q)
+    Lpat = smlu.Plan(A).L_pattern()
+    G = F.L.copy(); G.data[:] = 1
+    assert abs(G - Lpat).count_nonzero() == 0
+
+
+@pytest.mark.parametrize("N,grid", [(6, True), (9, False), (13, True)])
+def test_poisson3d_factors(gpu, N, grid):
+    A = mats.poisson3d(N)
+    F = smlu.ParallelSparseLU(A, grid=(N, N, N) if grid else None)
+    factor_parity(A, F)
+    assert np.array_equal(F.p, F.q)
+    b = np.random.default_rng(1).random(A.shape[0])
+    x = np.empty_like(b)
+    smlu.ldiv_(x, F, b)
+    assert isapprox(x, spla.spsolve(A, b), TOL, TOL)
+
+
+@pytest.mark.parametrize("nel", [1, 2, 3, 7, 20, 57, 200])
+def test_fe_matrix_ldiv(gpu, nel):
+    rng = np.random.default_rng(47 + nel)
+    A = O.test_matrix(rng, nel, 5)
+    n = A.shape[0]
+    F = smlu.ParallelSparseLU(A)
+    factor_parity(A, F, rtol=1e-10)
+    b = rng.random(n)
+    x = np.empty(n)
+    smlu.ldiv_(x, F, b)
+    assert isapprox(x, spla.spsolve(A, b), TOL, TOL)
+
+
+@pytest.mark.parametrize("n", [1, 2, 5, 17, 64, 130, 200, 333])
+def test_dense_ldiv_and_refactor(gpu, n):
+    rng = np.random.default_rng(n)
+    A = sp.csc_matrix(rng.random((n, n)))
+    F = smlu.ParallelSparseLU(A)
+    b = rng.random(n)
+    x = np.empty(n)
+    smlu.ldiv_(x, F, b)
+    assert isapprox(x, np.linalg.solve(A.toarray(), b), DENSE_TOL, DENSE_TOL)
+    A2 = sp.csc_matrix(rng.random((n, n)))
+    smlu.lu_(F, A2)
+    b = rng.random(n)
+    smlu.ldiv_(x, F, b)
+    assert isapprox(x, np.linalg.solve(A2.toarray(), b), DENSE_TOL, DENSE_TOL)
+
+
+def test_lsolve_rsolve(gpu):
+    rng = np.random.default_rng(3)
+    A = O.test_matrix(rng, 30, 5)
+    F = smlu.ParallelSparseLU(A)
+    n = A.shape[0]
+    b = rng.random(n)
+    x = b.copy()
+    smlu.lsolve_(F, x)
+    assert isapprox(x, spla.spsolve_triangular(F.L.tocsr(), b, lower=True), TOL, TOL)
+    x = b.copy()
+    smlu.rsolve_(F, x)
+    assert isapprox(x, spla.spsolve_triangular(F.U.tocsr(), b, lower=False), DENSE_TOL, DENSE_TOL)
+
+
+def test_random_dominant_c1(gpu):
+    A = mats.random_dominant(1000, 0.01, 47)
+    F = smlu.ParallelSparseLU(A)
+    factor_parity(A, F, rtol=1e-11)
+    b = np.random.default_rng(2).random(1000)
+    x = np.empty(1000)
+    smlu.ldiv_(x, F, b)
+    assert isapprox(x, spla.spsolve(A, b), TOL, TOL)
+
+
+def test_blocked_tile_mode_dominant(gpu):
+    # ns > 512 -> diagonal-tile pivoting path (mode 2) on a dense dominant matrix
+    n = 700
+    rng = np.random.default_rng(5)
+    D = rng.random((n, n))
+    D += np.diag(D.sum(axis=1) + 1)
+    A = sp.csc_matrix(D)
+    F = smlu.ParallelSparseLU(A)
+    b = rng.random(n)
+    x = np.empty(n)
+    smlu.ldiv_(x, F, b)
+    assert isapprox(x, np.linalg.solve(D, b), DENSE_TOL, DENSE_TOL)
+    factor_parity(A, F, rtol=1e-11)
