@@ -776,12 +776,12 @@ hipError_t launch_front_lds(hipStream_t st, int cnt, int Mmax, const int32_t* li
   k_front_lds<<<cnt, 256, lds, st>>>(list, sn, store, scratch, rowperm, info, growth, diag_tol, piv_tol);
   return hipGetLastError();
 }
-hipError_t launch_panel(hipStream_t st, int cnt, int Rmax, int Wmax, int step, const int32_t* list,
+hipError_t launch_panel(hipStream_t st, int cnt, int lds_doubles, int step, const int32_t* list,
                         const SNode* sn, double* store, double* scratch, int32_t* rowperm,
                         int32_t* swaps, int64_t swap_stride, int32_t* info, double* growth,
                         double diag_tol) {
   if (cnt <= 0) return hipSuccess;
-  size_t lds = (size_t)(Rmax | 1) * (size_t)Wmax * sizeof(double);
+  size_t lds = (size_t)lds_doubles * sizeof(double);
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute((const void*)k_panel, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);

@@ -14,6 +14,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <map>
@@ -34,7 +35,7 @@ hipError_t launch_extend_add(hipStream_t, int64_t, const int2*, const SNode*, co
                              double*);
 hipError_t launch_front_lds(hipStream_t, int, int, const int32_t*, const SNode*, double*, double*,
                             int32_t*, int32_t*, double*, double, double);
-hipError_t launch_panel(hipStream_t, int, int, int, int, const int32_t*, const SNode*, double*, double*,
+hipError_t launch_panel(hipStream_t, int, int, int, const int32_t*, const SNode*, double*, double*,
                         int32_t*, int32_t*, int64_t, int32_t*, double*, double);
 hipError_t launch_laswp_trsm_u(hipStream_t, int64_t, const FrontTile*, int, int, const SNode*, double*,
                                double*, const int32_t*, int64_t);
@@ -326,18 +327,19 @@ static int build_schedule(smlu_handle* h) {
       L.kind = K_PANEL;
       L.step = (int)t;
       L.off = (int64_t)ilist.size();
-      int64_t Rmax = 1, Wmax = 1;
+      int64_t ldsmax = 1, Rmax = 1;
       for (auto s : act) {
         const SNode& r = h->hsn[s];
         int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
         int64_t R = r.mode == 1 ? r.ns - kb : w;
+        ldsmax = std::max(ldsmax, (R | 1) * w);
         Rmax = std::max(Rmax, R);
-        Wmax = std::max(Wmax, w);
         ilist.push_back((int32_t)s);
       }
+      if (ldsmax * 8 > 148 * 1024 || Rmax > 512) return fail(h, SMLU_ERR_ARG, "internal: panel LDS budget");
       L.cnt = (int64_t)act.size();
-      L.aux = Rmax;
-      L.aux2 = Wmax;
+      L.aux = ldsmax;
+      L.aux2 = Rmax;
       h->fac.push_back(L);
       // laswp + trsm_u
       L = Launch();
@@ -558,7 +560,7 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
       return launch_front_lds(st, (int)L.cnt, (int)L.aux, h->ilist.p + L.off, h->sn.p, h->store.p,
                               h->scratch.p, h->rowperm.p, h->info.p, h->growth.p, diag_tol, piv_tol);
     case K_PANEL:
-      return launch_panel(st, (int)L.cnt, (int)L.aux, (int)L.aux2, L.step, h->ilist.p + L.off, h->sn.p,
+      return launch_panel(st, (int)L.cnt, (int)L.aux, L.step, h->ilist.p + L.off, h->sn.p,
                           h->store.p, h->scratch.p, h->rowperm.p, h->swaps.p, kSwapStride, h->info.p,
                           h->growth.p, diag_tol);
     case K_TRSMU:
@@ -591,10 +593,19 @@ static int run_factor(smlu_handle* h) {
   // A given (p, q) order means "no pivoting on top": only a zero diagonal moves.
   double diag_tol = P.given_order ? 0.0 : h->opts.diag_pivot_tol;
   double piv_tol = h->opts.pivot_tol;
+  static const bool dbg = std::getenv("SMLU_DEBUG_SYNC") != nullptr;
   for (const Launch& L : h->fac) {
     hipEvent_t stop;
     HIPCHK(tm.begin(L.kind, &stop));
-    HIPCHK(run_launch(h, L, diag_tol, piv_tol));
+    hipError_t e = run_launch(h, L, diag_tol, piv_tol);
+    if (e == hipSuccess && dbg) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+      char buf[256];
+      std::snprintf(buf, sizeof buf, "HIP error '%s' in launch kind=%d step=%d off=%lld cnt=%lld nwg=%lld aux=%lld aux2=%lld",
+                    hipGetErrorString(e), L.kind, L.step, (long long)L.off, (long long)L.cnt,
+                    (long long)L.nwg, (long long)L.aux, (long long)L.aux2);
+      return fail(h, SMLU_ERR_HIP, buf);
+    }
     HIPCHK(tm.end(stop));
   }
   HIPCHK(hipMemcpyAsync(h->hinfo, h->info.p, sizeof(int32_t) * P.nsup, hipMemcpyDeviceToHost, st));
