@@ -51,6 +51,36 @@ def cpu_baseline(N_cpu, ordering, grid_hint):
             "seconds": dt, "gflops": 2 * P.stat("upd") / dt / 1e9}
 
 
+def max_over_ranks(x, device=None):
+    """Max of a float over all ranks (identity when torch.distributed is not initialised)."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device or "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed_region(step, steps, warmup, sync, device=None):
+    """Contract of the driver: W untimed warmup steps, then EXACTLY `steps` steps bracketed by
+    a barrier + device sync on both sides; returns the MAX wall time over ranks."""
+    import torch.distributed as dist
+    dist_on = dist.is_available() and dist.is_initialized()
+    for r in range(warmup):
+        step(r)
+    if dist_on:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for r in range(steps):
+        step(warmup + r)
+    sync()
+    if dist_on:
+        dist.barrier()
+    return max_over_ranks(time.perf_counter() - t0, device)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -102,29 +132,19 @@ def main():
         vals.append(v)
     torch.cuda.synchronize()
 
-    for r in range(args.warmup):
-        F.refactor_device(vals[r])
-        log(f"rank {rank}: warmup {r} refactor {F.stat('refactor_ms_last'):.1f} ms")
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ms_gemm = ms_total = 0.0
     kinds = ["gemm", "panel", "trsm", "small", "assemble", "memset"]
     kind_ms = {k: 0.0 for k in kinds}
-    t0 = time.perf_counter()
-    for r in range(args.steps):
-        F.refactor_device(vals[args.warmup + r])
-        for k in kinds:
-            kind_ms[k] += F.stat("ms_" + k)
-        log(f"rank {rank}: step {r} refactor {F.stat('refactor_ms_last'):.1f} ms")
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+
+    def step(r):
+        F.refactor_device(vals[r])
+        if r >= args.warmup:
+            for k in kinds:
+                kind_ms[k] += F.stat("ms_" + k)
+        log(f"rank {rank}: {'warmup' if r < args.warmup else 'step'} {r} refactor "
+            f"{F.stat('refactor_ms_last'):.1f} ms")
+
+    dt = timed_region(step, args.steps, args.warmup, torch.cuda.synchronize,
+                      dev if world > 1 else None)
     # one solve (reported, not the metric)
     b = torch.rand(n, dtype=torch.float64, device=dev)
     x = torch.empty_like(b)

@@ -1,0 +1,107 @@
+"""CPU tests of the host symbolic analysis (no GPU): the plan's L pattern is exactly the
+structural fill of (Rs.*A)[q,q] computed independently by the oracle, for structurally
+symmetric inputs; a superset for unsymmetric ones; supernode/level invariants hold."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import oracle as O
+import smlu
+from smlu import matrices as mats
+
+
+def pattern(M):
+    M = sp.csc_matrix(M, copy=True)
+    M.data[:] = 1.0
+    return M
+
+
+def fill_pattern(A, q):
+    F = O.OracleLU(A, q, q)
+    return pattern(F.L), pattern(F.U)
+
+
+CASES = [
+    ("poisson2d_10", lambda: mats.poisson2d(10), {}),
+    ("poisson2d_16_geo", lambda: mats.poisson2d(16), {"grid": (16, 16)}),
+    ("poisson3d_6_geo", lambda: mats.poisson3d(6), {"grid": (6, 6, 6)}),
+    ("poisson3d_9", lambda: mats.poisson3d(9), {}),
+    ("poisson3d_8_natural", lambda: mats.poisson3d(8), {"ordering": "natural"}),
+    ("poisson3d_8_norelax", lambda: mats.poisson3d(8), {"relax": False}),
+    ("fe_20", lambda: O.test_matrix(np.random.default_rng(1), 20, 5), {}),
+    ("fe_1", lambda: O.test_matrix(np.random.default_rng(1), 1, 5), {}),
+    ("dense_30", lambda: sp.csc_matrix(np.random.default_rng(2).random((30, 30))), {}),
+    ("dense_1", lambda: sp.csc_matrix(np.ones((1, 1))), {}),
+    ("diag_7", lambda: sp.identity(7, format="csc"), {}),
+    ("sym_random", lambda: sp.csc_matrix((lambda R: R + R.T + sp.identity(150))(
+        sp.random(150, 150, density=0.02, random_state=3))), {}),
+]
+
+
+@pytest.mark.parametrize("name,make,kw", CASES, ids=[c[0] for c in CASES])
+def test_plan_pattern_equals_structural_fill(name, make, kw):
+    A = sp.csc_matrix(make())
+    P = smlu.Plan(A, **kw)
+    q = P.q()
+    assert np.array_equal(np.sort(q), np.arange(A.shape[0]))
+    Lp = P.L_pattern()
+    Lo, Uo = fill_pattern(A, q)
+    assert abs(Lp - Lo).count_nonzero() == 0
+    assert abs(Lp.T - Uo).count_nonzero() == 0
+    assert P.stat("nnzL") == Lo.nnz
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_plan_pattern_superset_unsymmetric(seed):
+    n = 120
+    A = sp.csc_matrix(sp.random(n, n, density=0.03, random_state=seed) + sp.identity(n))
+    P = smlu.Plan(A)
+    q = P.q()
+    Lp = P.L_pattern()
+    Lo, Uo = fill_pattern(A, q)
+    assert (Lo - Lo.multiply(Lp)).count_nonzero() == 0       # oracle fill contained
+    assert (Uo - Uo.multiply(Lp.T)).count_nonzero() == 0
+
+
+def test_supernode_and_level_invariants():
+    A = mats.poisson3d(12)
+    P = smlu.Plan(A)
+    first, parent, level = P.supernodes()
+    ns = len(parent)
+    assert first[0] == 0 and first[-1] == A.shape[0] and np.all(np.diff(first) > 0)
+    for s in range(ns):
+        if parent[s] >= 0:
+            assert parent[s] > s
+            assert level[parent[s]] > level[s]
+    assert P.stat("nlevels") == level.max() + 1
+
+
+def test_graph_nd_beats_natural_fill():
+    A = mats.poisson3d(16)
+    nd = smlu.Plan(A).stat("nnzL")
+    nat = smlu.Plan(A, ordering="natural").stat("nnzL")
+    geo = smlu.Plan(A, grid=(16, 16, 16)).stat("nnzL")
+    assert nd < nat and geo < nat
+
+
+def test_geometric_needs_matching_grid():
+    with pytest.raises(RuntimeError):
+        smlu.Plan(mats.poisson2d(8), ordering="geometric", grid=(7, 8))
+
+
+def test_plan_rejects_bad_pattern():
+    A = sp.csc_matrix(np.eye(3))
+    A.indices = np.array([0, 5, 2], dtype=A.indices.dtype)   # row out of range
+    with pytest.raises(RuntimeError):
+        smlu.Plan(A)
+
+
+def test_flop_and_update_counts_match_oracle():
+    A = mats.poisson2d(12)
+    P = smlu.Plan(A, relax=False)
+    q = P.q()
+    Lo, Uo = fill_pattern(A, q)
+    # upd = sum_k |L_k| * |U_k| over strictly off-diagonal counts
+    lk = np.diff(Lo.indptr) - 1
+    uk = np.diff(sp.csr_matrix(Uo).indptr) - 1
+    assert P.stat("upd") == float(np.sum(lk * uk))
