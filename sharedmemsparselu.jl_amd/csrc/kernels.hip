@@ -599,6 +599,98 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
 }
 
 // ------------------------------------------------------------------------------------
+// Dense update C -= A*B, large tiles: 128x128 output tile per 256-thread workgroup, 8x8
+// accumulators per thread (128 VGPRs), K staged through double-buffered LDS in slices of 16
+// with the next slice prefetched into registers.  Each thread owns rows {2tx,2tx+1}+32i and
+// columns {2ty,2ty+1}+32j so every fragment read is one conflict-free ds_read_b128.
+// Per k: 8 ds_read_b128 feed 64 v_fma_f64 (0.25 doubles of LDS per FMA).
+// ------------------------------------------------------------------------------------
+#define HBM_ 128
+#define HBK_ 16
+#define HLDB_ (HBM_ + 2)
+#ifndef KK_UNROLL
+#define KK_UNROLL 2
+#endif
+__global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__ tasks, int ntask) {
+  __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
+  __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
+  const int64_t b = blockIdx.x;
+  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+  const int64_t tl = b - t.tile0;
+  const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
+  const int m0 = tm * HBM_, n0 = tn * HBM_;
+  const int tid = threadIdx.x;
+  const int tx = tid & 15, ty = tid >> 4;
+  double acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0.0;
+  // global->register mapping: A: row = tid & 127, k = (tid >> 7) + 2r ; B: k = tid & 15, col = (tid >> 4) + 16r
+  const int ar = tid & 127, ak = tid >> 7;
+  const int bk = tid & 15, bc = tid >> 4;
+  const int K = t.k;
+  const int arow = m0 + ar;
+  const bool arow_ok = arow < t.m;
+  const double* Ap = t.A + arow;
+  double ra[8], rb[8];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int kk = k0 + ak + 2 * r;
+      ra[r] = (arow_ok && kk < K) ? Ap[(int64_t)kk * t.lda] : 0.0;
+      const int col = n0 + bc + 16 * r;
+      rb[r] = (col < t.n && k0 + bk < K) ? t.B[(int64_t)col * t.ldb + k0 + bk] : 0.0;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      As[buf][ak + 2 * r][ar] = ra[r];
+      Bs[buf][bk][bc + 16 * r] = rb[r];
+    }
+  };
+  const int nk = (K + HBK_ - 1) / HBK_;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * HBK_);
+#pragma unroll KK_UNROLL
+    for (int kk = 0; kk < HBK_; ++kk) {
+      double a[8], bb[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double2 v = *reinterpret_cast<const double2*>(&As[cur][kk][2 * tx + 32 * i]);
+        a[2 * i] = v.x;
+        a[2 * i + 1] = v.y;
+        const double2 w = *reinterpret_cast<const double2*>(&Bs[cur][kk][2 * ty + 32 * i]);
+        bb[2 * i] = w.x;
+        bb[2 * i + 1] = w.y;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = fma(a[i], bb[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = n0 + 2 * ty + 32 * (j >> 1) + (j & 1);
+    if (col >= t.n) continue;
+    double* Cc = t.C + (int64_t)col * t.ldc;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int row = m0 + 2 * tx + 32 * (i >> 1) + (i & 1);
+      if (row < t.m) Cc[row] = Cc[row] - acc[i][j];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Solves.  Front vectors v_s (M doubles) live in vbuf[voff[s]].
 // Forward (L): gather own rows + children's update vectors, apply the front's row
 // permutation, unit-lower solve of the diagonal block in 64-column blocks (one wave does
@@ -707,6 +799,116 @@ __global__ __launch_bounds__(256) void k_bwd_front(const int32_t* __restrict__ l
   for (int64_t i = tid; i < ns; i += 256) xo[i] = v[i];
 }
 
+// ------------------------------------------------------------------------------------
+// Solves for large fronts (ns > 256): the diagonal block sweep is split over workgroups.
+// k_fwd_gather: front vector = own rows + children's update vectors, row permutation.
+// k_fwd_block (step t, jb = 64t): every workgroup re-solves the 64x64 unit-lower diagonal
+//   block from v (read-only in this launch), applies it to its 256-row chunk below; chunk 0
+//   publishes the solved block into x.  k_bwd_u12: x_s -= U12 x[R_s] by row chunks.
+// k_bwd_block: same as k_fwd_block for U11 from the bottom block up.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fwd_gather(const int32_t* __restrict__ list,
+                                                    const SNode* __restrict__ sn,
+                                                    const int32_t* __restrict__ chlist,
+                                                    const int32_t* __restrict__ relmap,
+                                                    const int32_t* __restrict__ rowperm,
+                                                    double* __restrict__ x, double* __restrict__ vbuf) {
+  const SNode s = sn[list[blockIdx.x]];
+  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
+  double* v = vbuf + s.voff;
+  double* xo = x + s.first;
+  const int tid = threadIdx.x;
+  for (int64_t i = tid; i < M; i += 256) v[i] = i < ns ? xo[i] : 0.0;
+  __syncthreads();
+  for (int c = s.chbeg; c < s.chend; ++c) {
+    const SNode ch = sn[chlist[c]];
+    const double* u = vbuf + ch.voff + ch.ns;
+    const int32_t* rm = relmap + ch.rowptr;
+    for (int64_t i = tid; i < ch.nu; i += 256) v[rm[i]] += u[i];
+    __syncthreads();
+  }
+  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[rowperm[s.first + i]];
+  __syncthreads();
+  for (int64_t i = tid; i < ns; i += 256) v[i] = xo[i];
+}
+
+template <bool UPPER>
+__global__ __launch_bounds__(256) void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step,
+                                                   const SNode* __restrict__ sn,
+                                                   const double* __restrict__ store,
+                                                   double* __restrict__ x, double* __restrict__ vbuf) {
+  __shared__ double xs[64];
+  const int64_t b = blockIdx.x;
+  const int fi = find_front_tile(ft, nft, b);
+  const SNode s = sn[ft[fi].s];
+  const int64_t chunk = b - ft[fi].wg0;
+  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
+  const int64_t nblk = (ns + 63) / 64;
+  const int64_t jb = UPPER ? (nblk - 1 - step) * 64 : (int64_t)step * 64;
+  const int bw = (int)min<int64_t>(64, ns - jb);
+  double* v = vbuf + s.voff;
+  const double* Lp = store + s.Loff;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (wv == 0) {
+    double xi = lane < bw ? v[jb + lane] : 0.0;
+    if (!UPPER) {
+      for (int j = 0; j < bw; ++j) {
+        double xj = __shfl(xi, j, 64);
+        if (lane > j && lane < bw) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
+      }
+    } else {
+      for (int j = bw - 1; j >= 0; --j) {
+        if (lane == j) xi = xi / Lp[(jb + j) * M + jb + j];
+        double xj = __shfl(xi, j, 64);
+        if (lane < j) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
+      }
+    }
+    if (lane < bw) {
+      xs[lane] = xi;
+      if (chunk == 0) x[s.first + jb + lane] = xi;
+    }
+  }
+  __syncthreads();
+  // rows updated by this chunk: forward -> [jb+bw, M), backward -> [0, jb)
+  const int64_t r0 = UPPER ? chunk * 256 : jb + bw + chunk * 256;
+  const int64_t r1 = UPPER ? jb : M;
+  const int64_t i = r0 + tid;
+  if (i < r1 && i < r0 + 256) {
+    double acc = 0.0;
+    for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
+    v[i] -= acc;
+  }
+}
+
+// x_s[i] (in v) = x[first+i] - sum_j U12[i,j] * x[R_j], 256 rows per workgroup
+__global__ __launch_bounds__(256) void k_bwd_u12(const FrontTile* __restrict__ ft, int nft,
+                                                 const SNode* __restrict__ sn,
+                                                 const int32_t* __restrict__ rows,
+                                                 const double* __restrict__ store,
+                                                 const double* __restrict__ x,
+                                                 double* __restrict__ vbuf) {
+  __shared__ double xr[256];
+  const int64_t b = blockIdx.x;
+  const int fi = find_front_tile(ft, nft, b);
+  const SNode s = sn[ft[fi].s];
+  const int64_t chunk = b - ft[fi].wg0;
+  const int64_t ns = s.ns, nu = s.nu;
+  const int32_t* R = rows + s.rowptr;
+  const double* U12 = store + s.Uoff;
+  const int tid = threadIdx.x;
+  const int64_t i = chunk * 256 + tid;
+  double acc = 0.0;
+  for (int64_t j0 = 0; j0 < nu; j0 += 256) {
+    __syncthreads();
+    if (j0 + tid < nu) xr[tid] = x[R[j0 + tid]];
+    __syncthreads();
+    const int cnt = (int)min<int64_t>(256, nu - j0);
+    if (i < ns)
+      for (int j = 0; j < cnt; ++j) acc = fma(U12[(j0 + j) * ns + i], xr[j], acc);
+  }
+  if (i < ns) vbuf[s.voff + i] = x[s.first + i] - acc;
+}
+
 // wrk[i] = Rs[p0[i]] * b[p0[i]]
 __global__ void k_perm_in(int64_t n, const int64_t* __restrict__ p0, const double* __restrict__ Rs,
                           const double* __restrict__ b, double* __restrict__ wrk) {
@@ -809,9 +1011,10 @@ hipError_t launch_trsm_l(hipStream_t st, int64_t nwg, int W, const FrontTile* ft
     k_trsm_l<64><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, scratch, info, growth, piv_tol);
   return hipGetLastError();
 }
-hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask) {
+hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask, int tile) {
   if (ntiles <= 0) return hipSuccess;
-  k_gemm<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
+  if (tile == 128) k_gemm128<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
+  else k_gemm<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
   return hipGetLastError();
 }
 hipError_t launch_fwd(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
@@ -825,6 +1028,26 @@ hipError_t launch_bwd(hipStream_t st, int cnt, const int32_t* list, const SNode*
                       const int32_t* rows, const double* store, double* x, double* vbuf) {
   if (cnt <= 0) return hipSuccess;
   k_bwd_front<<<cnt, 256, 0, st>>>(list, sn, rows, store, x, vbuf);
+  return hipGetLastError();
+}
+hipError_t launch_fwd_gather(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
+                             const int32_t* chlist, const int32_t* relmap, const int32_t* rowperm,
+                             double* x, double* vbuf) {
+  if (cnt <= 0) return hipSuccess;
+  k_fwd_gather<<<cnt, 256, 0, st>>>(list, sn, chlist, relmap, rowperm, x, vbuf);
+  return hipGetLastError();
+}
+hipError_t launch_tri_block(hipStream_t st, bool upper, int64_t nwg, const FrontTile* ft, int nft,
+                            int step, const SNode* sn, const double* store, double* x, double* vbuf) {
+  if (nwg <= 0) return hipSuccess;
+  if (upper) k_tri_block<true><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, x, vbuf);
+  else k_tri_block<false><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, x, vbuf);
+  return hipGetLastError();
+}
+hipError_t launch_bwd_u12(hipStream_t st, int64_t nwg, const FrontTile* ft, int nft, const SNode* sn,
+                          const int32_t* rows, const double* store, const double* x, double* vbuf) {
+  if (nwg <= 0) return hipSuccess;
+  k_bwd_u12<<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sn, rows, store, x, vbuf);
   return hipGetLastError();
 }
 hipError_t launch_perm_in(hipStream_t st, int64_t n, const int64_t* p0, const double* Rs,

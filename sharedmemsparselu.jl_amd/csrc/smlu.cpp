@@ -41,7 +41,13 @@ hipError_t launch_laswp_trsm_u(hipStream_t, int64_t, const FrontTile*, int, int,
                                double*, const int32_t*, int64_t);
 hipError_t launch_trsm_l(hipStream_t, int64_t, int, const FrontTile*, int, int, const SNode*, double*,
                          double*, int32_t*, double*, double);
-hipError_t launch_gemm(hipStream_t, int64_t, const GemmTask*, int);
+hipError_t launch_gemm(hipStream_t, int64_t, const GemmTask*, int, int);
+hipError_t launch_fwd_gather(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
+                             const int32_t*, double*, double*);
+hipError_t launch_tri_block(hipStream_t, bool, int64_t, const FrontTile*, int, int, const SNode*,
+                            const double*, double*, double*);
+hipError_t launch_bwd_u12(hipStream_t, int64_t, const FrontTile*, int, const SNode*, const int32_t*,
+                          const double*, const double*, double*);
 hipError_t launch_fwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                       const int32_t*, const double*, double*, double*);
 hipError_t launch_bwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*,
@@ -65,10 +71,12 @@ thread_local std::string g_last_error;
 
 enum Kind : int {
   K_MEMSET_STORE, K_MEMSET_SCRATCH, K_SCATTER, K_EXTADD, K_FRONT_LDS, K_PANEL, K_TRSMU, K_TRSML,
-  K_GEMM, K_FWD, K_BWD, K_NKIND
+  K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_NKIND
 };
 const char* kKindName[K_NKIND] = {"memset", "memset", "assemble", "assemble", "small", "panel",
-                                  "trsm", "trsm", "gemm", "solve", "solve"};
+                                  "trsm", "trsm", "gemm", "solve", "solve", "solve", "solve",
+                                  "solve", "solve"};
+constexpr int kSolveBigNs = 256;  // fronts with more pivots use the multi-workgroup solve
 
 struct Launch {
   int kind = 0;
@@ -247,6 +255,31 @@ static int build_schedule(smlu_handle* h) {
   h->gemm_flops = 0;
   h->dense_flops = P.flops;
   int64_t max_list = 1;
+  // GEMM launches: 128x128 tiles when the launch has enough of them to fill the GPU,
+  // otherwise 64x64 tiles (same per-element arithmetic, bitwise-identical results).
+  auto add_gemm_launch = [&](std::vector<GemmTask>& cand, double fl, int step) {
+    if (cand.empty()) return;
+    int64_t t128 = 0;
+    for (auto& g : cand) t128 += (int64_t)((g.m + 127) / 128) * ((g.n + 127) / 128);
+    int tile = t128 >= 512 ? 128 : 64;
+    Launch L;
+    L.kind = K_GEMM;
+    L.step = step;
+    L.off = (int64_t)gt.size();
+    L.aux = tile;
+    int64_t tiles = 0;
+    for (auto& g : cand) {
+      g.tiles_m = (g.m + tile - 1) / tile;
+      g.tile0 = tiles;
+      tiles += (int64_t)g.tiles_m * ((g.n + tile - 1) / tile);
+      gt.push_back(g);
+    }
+    L.cnt = (int64_t)cand.size();
+    L.nwg = tiles;
+    L.flops = fl;
+    h->fac.push_back(L);
+    h->gemm_flops += fl;
+  };
   for (int l = 0; l < P.nlevels; ++l) {
     Launch L;
     // zero this level's fronts
@@ -376,54 +409,42 @@ static int build_schedule(smlu_handle* h) {
       L.aux = W;
       if (wg > 0) h->fac.push_back(L);
       // trailing update of the pivot part (R1: L panel, R2: U12)
-      L = Launch();
-      L.kind = K_GEMM;
-      L.step = (int)t;
-      L.off = (int64_t)gt.size();
-      int64_t tiles = 0;
-      for (auto s : act) {
-        const SNode& r = h->hsn[s];
-        int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
-        int64_t m1 = M - kb - w, n1 = r.ns - kb - w;
-        if (m1 > 0 && n1 > 0) {
-          GemmTask g{};
-          g.A = store + r.Loff + kb * M + kb + w;
-          g.B = store + r.Loff + (kb + w) * M + kb;
-          g.C = store + r.Loff + (kb + w) * M + kb + w;
-          g.m = (int)m1; g.n = (int)n1; g.k = (int)w;
-          g.lda = (int)M; g.ldb = (int)M; g.ldc = (int)M;
-          g.tiles_m = (int)((m1 + 63) / 64);
-          g.tile0 = tiles;
-          tiles += g.tiles_m * ((n1 + 63) / 64);
-          gt.push_back(g);
-          L.flops += 2.0 * m1 * n1 * w;
+      {
+        std::vector<GemmTask> cand;
+        double fl = 0;
+        for (auto s : act) {
+          const SNode& r = h->hsn[s];
+          int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
+          int64_t m1 = M - kb - w, n1 = r.ns - kb - w;
+          if (m1 > 0 && n1 > 0) {
+            GemmTask g{};
+            g.A = store + r.Loff + kb * M + kb + w;
+            g.B = store + r.Loff + (kb + w) * M + kb;
+            g.C = store + r.Loff + (kb + w) * M + kb + w;
+            g.m = (int)m1; g.n = (int)n1; g.k = (int)w;
+            g.lda = (int)M; g.ldb = (int)M; g.ldc = (int)M;
+            cand.push_back(g);
+            fl += 2.0 * m1 * n1 * w;
+          }
+          int64_t m2 = r.ns - kb - w, n2 = r.nu;
+          if (m2 > 0 && n2 > 0) {
+            GemmTask g{};
+            g.A = store + r.Loff + kb * M + kb + w;
+            g.B = store + r.Uoff + kb;
+            g.C = store + r.Uoff + kb + w;
+            g.m = (int)m2; g.n = (int)n2; g.k = (int)w;
+            g.lda = (int)M; g.ldb = r.ns; g.ldc = r.ns;
+            cand.push_back(g);
+            fl += 2.0 * m2 * n2 * w;
+          }
         }
-        int64_t m2 = r.ns - kb - w, n2 = r.nu;
-        if (m2 > 0 && n2 > 0) {
-          GemmTask g{};
-          g.A = store + r.Loff + kb * M + kb + w;
-          g.B = store + r.Uoff + kb;
-          g.C = store + r.Uoff + kb + w;
-          g.m = (int)m2; g.n = (int)n2; g.k = (int)w;
-          g.lda = (int)M; g.ldb = r.ns; g.ldc = r.ns;
-          g.tiles_m = (int)((m2 + 63) / 64);
-          g.tile0 = tiles;
-          tiles += g.tiles_m * ((n2 + 63) / 64);
-          gt.push_back(g);
-          L.flops += 2.0 * m2 * n2 * w;
-        }
+        add_gemm_launch(cand, fl, (int)t);
       }
-      L.cnt = (int64_t)gt.size() - L.off;
-      L.nwg = tiles;
-      if (tiles > 0) { h->fac.push_back(L); h->gemm_flops += L.flops; }
     }
     // F22 -= L21 * U12 for the blocked fronts of this level
     {
-      L = Launch();
-      L.kind = K_GEMM;
-      L.step = -1;
-      L.off = (int64_t)gt.size();
-      int64_t tiles = 0;
+      std::vector<GemmTask> cand;
+      double fl = 0;
       for (auto s : big) {
         const SNode& r = h->hsn[s];
         if (r.nu == 0) continue;
@@ -434,31 +455,98 @@ static int build_schedule(smlu_handle* h) {
         g.C = scratch + r.Foff;
         g.m = r.nu; g.n = r.nu; g.k = r.ns;
         g.lda = (int)M; g.ldb = r.ns; g.ldc = r.nu;
-        g.tiles_m = (r.nu + 63) / 64;
-        g.tile0 = tiles;
-        tiles += (int64_t)g.tiles_m * ((r.nu + 63) / 64);
-        gt.push_back(g);
-        L.flops += 2.0 * r.nu * (double)r.nu * r.ns;
+        cand.push_back(g);
+        fl += 2.0 * r.nu * (double)r.nu * r.ns;
       }
-      L.cnt = (int64_t)gt.size() - L.off;
-      L.nwg = tiles;
-      if (tiles > 0) { h->fac.push_back(L); h->gemm_flops += L.flops; }
+      add_gemm_launch(cand, fl, -1);
     }
   }
-  // solves: one launch per level, all fronts
+  // solves: per level, small fronts by one workgroup each; large fronts (ns > kSolveBigNs)
+  // gather + one launch per 64-column block with 256-row chunks per workgroup
   h->fwd.clear();
   h->bwd.clear();
+  std::vector<std::vector<Launch>> bwd_levels;
   for (int l = 0; l < P.nlevels; ++l) {
-    Launch L;
-    L.kind = K_FWD;
-    L.off = (int64_t)ilist.size();
-    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) ilist.push_back(P.lev_sup[k]);
-    L.cnt = P.lev_ptr[l + 1] - P.lev_ptr[l];
-    h->fwd.push_back(L);
-    L.kind = K_BWD;
-    h->bwd.push_back(L);
+    std::vector<int64_t> small, bigs;
+    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+      int64_t s = P.lev_sup[k];
+      (h->hsn[s].ns > kSolveBigNs ? bigs : small).push_back(s);
+    }
+    std::vector<Launch> bl;
+    if (!small.empty()) {
+      Launch L;
+      L.kind = K_FWD;
+      L.off = (int64_t)ilist.size();
+      for (auto s : small) ilist.push_back((int32_t)s);
+      L.cnt = (int64_t)small.size();
+      h->fwd.push_back(L);
+      L.kind = K_BWD;
+      bl.push_back(L);
+    }
+    if (!bigs.empty()) {
+      Launch L;
+      L.kind = K_FWDG;
+      L.off = (int64_t)ilist.size();
+      for (auto s : bigs) ilist.push_back((int32_t)s);
+      L.cnt = (int64_t)bigs.size();
+      h->fwd.push_back(L);
+      int64_t nb = 0;
+      for (auto s : bigs) nb = std::max<int64_t>(nb, (h->hsn[s].ns + 63) / 64);
+      // backward: U12 product first
+      Launch U;
+      U.kind = K_BWDU;
+      U.off = (int64_t)ft.size();
+      int64_t wg = 0;
+      for (auto s : bigs) {
+        ft.push_back(FrontTile{(int32_t)s, 0, wg});
+        wg += (h->hsn[s].ns + 255) / 256;
+      }
+      U.cnt = (int64_t)bigs.size();
+      U.nwg = wg;
+      std::vector<Launch> bsteps;
+      for (int64_t t = 0; t < nb; ++t) {
+        Launch F, B;
+        F.kind = K_TRIF;
+        B.kind = K_TRIB;
+        F.step = B.step = (int)t;
+        F.off = (int64_t)ft.size();
+        int64_t wf = 0, cnt = 0;
+        for (auto s : bigs) {
+          const SNode& r = h->hsn[s];
+          int64_t nbs = (r.ns + 63) / 64;
+          if (t >= nbs) continue;
+          int64_t jb = t * 64, bw = std::min<int64_t>(64, r.ns - jb), M = (int64_t)r.ns + r.nu;
+          ft.push_back(FrontTile{(int32_t)s, 0, wf});
+          wf += std::max<int64_t>(1, (M - jb - bw + 255) / 256);
+          ++cnt;
+        }
+        F.cnt = cnt;
+        F.nwg = wf;
+        h->fwd.push_back(F);
+        B.off = (int64_t)ft.size();
+        int64_t wb = 0;
+        cnt = 0;
+        for (auto s : bigs) {
+          const SNode& r = h->hsn[s];
+          int64_t nbs = (r.ns + 63) / 64;
+          if (t >= nbs) continue;
+          int64_t jb = (nbs - 1 - t) * 64;
+          ft.push_back(FrontTile{(int32_t)s, 0, wb});
+          wb += std::max<int64_t>(1, (jb + 255) / 256);
+          ++cnt;
+        }
+        B.cnt = cnt;
+        B.nwg = wb;
+        bsteps.push_back(B);
+      }
+      bl.push_back(U);
+      for (auto& b : bsteps) bl.push_back(b);
+    }
+    bwd_levels.push_back(bl);
   }
-  std::reverse(h->bwd.begin(), h->bwd.end());
+  for (int l = P.nlevels - 1; l >= 0; --l)
+    for (auto& L : bwd_levels[l]) h->bwd.push_back(L);
+
   h->nlaunch = (int64_t)h->fac.size();
   // upload
   HIPCHK(h->sn.upload(h->hsn.data(), h->hsn.size(), st));
@@ -570,7 +658,7 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
       return launch_trsm_l(st, L.nwg, (int)L.aux, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p,
                            h->store.p, h->scratch.p, h->info.p, h->growth.p, piv_tol);
     case K_GEMM:
-      return launch_gemm(st, L.nwg, h->gtasks.p + L.off, (int)L.cnt);
+      return launch_gemm(st, L.nwg, h->gtasks.p + L.off, (int)L.cnt, (int)L.aux);
   }
   return hipErrorInvalidValue;
 }
@@ -631,6 +719,30 @@ static int run_factor(smlu_handle* h) {
   return rc;
 }
 
+static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w) {
+  hipStream_t st = h->stream;
+  switch (L.kind) {
+    case K_FWD:
+      return launch_fwd(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->chlist.p, h->relmap.p,
+                        h->rowperm.p, h->store.p, w, h->vbuf.p);
+    case K_BWD:
+      return launch_bwd(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->rows.p, h->store.p, w, h->vbuf.p);
+    case K_FWDG:
+      return launch_fwd_gather(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->chlist.p, h->relmap.p,
+                               h->rowperm.p, w, h->vbuf.p);
+    case K_TRIF:
+      return launch_tri_block(st, false, L.nwg, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p,
+                              h->store.p, w, h->vbuf.p);
+    case K_TRIB:
+      return launch_tri_block(st, true, L.nwg, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p,
+                              h->store.p, w, h->vbuf.p);
+    case K_BWDU:
+      return launch_bwd_u12(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->sn.p, h->rows.p, h->store.p, w,
+                            h->vbuf.p);
+  }
+  return hipErrorInvalidValue;
+}
+
 static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode) {
   // mode 0: ldiv (b -> x); 1: lsolve in place on dx (final order); 2: rsolve in place
   Plan& P = h->plan;
@@ -644,12 +756,9 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode)
   if (mode == 1) HIPCHK(launch_unswap(st, P.n, h->posfirst.p, h->rowperm.p, dx, w));
   if (mode == 2) HIPCHK(hipMemcpyAsync(w, dx, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st));
   if (mode != 2)
-    for (const Launch& L : h->fwd)
-      HIPCHK(launch_fwd(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->chlist.p, h->relmap.p,
-                        h->rowperm.p, h->store.p, w, h->vbuf.p));
+    for (const Launch& L : h->fwd) HIPCHK(run_solve_launch(h, L, w));
   if (mode != 1)
-    for (const Launch& L : h->bwd)
-      HIPCHK(launch_bwd(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->rows.p, h->store.p, w, h->vbuf.p));
+    for (const Launch& L : h->bwd) HIPCHK(run_solve_launch(h, L, w));
   if (mode == 0) HIPCHK(launch_perm_out(st, P.n, h->q.p, w, dx));
   else HIPCHK(hipMemcpyAsync(dx, w, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st));
   HIPCHK(tm.end(stop));
