@@ -33,6 +33,17 @@ __device__ __forceinline__ double wave_max_idx(double v, int& idx) {
   return v;
 }
 
+// 1/x with one Newton step on the hardware estimate (v_rcp_f64): ~3 dependent fp64 ops instead
+// of the ~10 of an IEEE division (a dependent fp64 op costs ~32 cycles on gfx950).  Used on the
+// sequential pivot and triangular-solve chains; results stay within a few ulp of division.
+__device__ __forceinline__ double recip(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  const double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  const double e2 = fma(-x, r, 1.0);
+  return fma(r, e2, r);
+}
+
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
@@ -228,8 +239,8 @@ __global__ __launch_bounds__(256) void k_front_lds(const int32_t* __restrict__ l
       }
       __syncthreads();
     }
-    const double pv = lds[k * ld + k];
-    for (int i = k + 1 + tid; i < M; i += 256) lds[k * ld + i] = lds[k * ld + i] / pv;
+    const double pinv = recip(lds[k * ld + k]);
+    for (int i = k + 1 + tid; i < M; i += 256) lds[k * ld + i] = lds[k * ld + i] * pinv;
     __syncthreads();
     for (int j = k + 1 + wv; j < M; j += 4) {
       const double u = lds[j * ld + k];
@@ -253,7 +264,7 @@ __global__ __launch_bounds__(256) void k_front_lds(const int32_t* __restrict__ l
 // (R x w) is factored in LDS; rows are permuted in place and the composed permutation is
 // recorded for the row swaps of the other columns (k_laswp_trsm_u).
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_panel(const int32_t* __restrict__ list, int step,
+__global__ __launch_bounds__(256) void k_panel(const int32_t* __restrict__ list, int step, int slot0,
                                                const SNode* __restrict__ sn,
                                                double* __restrict__ store,
                                                double* __restrict__ scratch,
@@ -337,7 +348,7 @@ __global__ __launch_bounds__(256) void k_panel(const int32_t* __restrict__ list,
   for (int i = tid; i < R; i += 256) old[i] = rp[i];
   __syncthreads();
   for (int i = tid; i < R; i += 256) rp[i] = old[s_lp[i]];
-  int32_t* sw = swaps + (int64_t)blockIdx.x * swap_stride;
+  int32_t* sw = swaps + (int64_t)(slot0 + blockIdx.x) * swap_stride;
   if (tid == 0) {
     int cnt = 0;
     for (int i = 0; i < R; ++i)
@@ -348,6 +359,372 @@ __global__ __launch_bounds__(256) void k_panel(const int32_t* __restrict__ list,
       }
     sw[0] = cnt;
     if (s_flag) publish_info(info + sid, s_flag, s_err);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Panel factorization, one wavefront per front (no block barriers): the R x w candidate block
+// lives in LDS (column-major, ld = R|1); lane l owns rows l, l+64, ...  Per column: wave
+// argmax (shuffles), diagonal-preference choice, in-LDS row swap (lanes over columns), pivot
+// scaling and the rank-1 update of the lane's own rows (the pivot row is an LDS broadcast).
+// ------------------------------------------------------------------------------------
+template <int RPL>
+__global__ __launch_bounds__(64) void k_panel1(const int32_t* __restrict__ list, int step, int slot0,
+                                               const SNode* __restrict__ sn,
+                                               double* __restrict__ store,
+                                               double* __restrict__ scratch,
+                                               int32_t* __restrict__ rowperm,
+                                               int32_t* __restrict__ swaps,
+                                               int64_t swap_stride, int32_t* __restrict__ info,
+                                               double* __restrict__ growth, double diag_tol) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ int s_lp[512];
+  const int sid = list[blockIdx.x];
+  const SNode s = sn[sid];
+  FrontPtrs f = front_ptrs(s, store, scratch);
+  const int64_t M = f.M;
+  const int ns = (int)f.ns;
+  const int kb = step * s.nb;
+  const int w = min(s.nb, ns - kb);
+  const int R = (s.mode == 1) ? ns - kb : w;
+  const int ld = R | 1;
+  const int lane = threadIdx.x;
+  double* P = f.L + (int64_t)kb * M + kb;
+  for (int j = 0; j < w; ++j)
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+      const int i = lane + 64 * r;
+      if (i < R) lds[j * ld + i] = P[(int64_t)j * M + i];
+    }
+  for (int i = lane; i < R; i += 64) s_lp[i] = i;
+  int flag = 0, err = -1;
+  double gmax = 0.0;
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  for (int k = 0; k < w; ++k) {
+    double am = -1.0;
+    int ai = k;
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+      const int i = lane + 64 * r;
+      if (i >= k && i < R) {
+        const double v = fabs(lds[k * ld + i]);
+        if (v > am) { am = v; ai = i; }
+      }
+    }
+    am = wave_max_idx(am, ai);
+    const double akk = lds[k * ld + k];
+    const int piv = choose_pivot(akk, am, ai, k, diag_tol);
+    if (am <= 0.0) {
+      flag |= 1;
+      if (err < 0) err = kb + k;
+    }
+    if (piv != k) {
+      __builtin_amdgcn_wave_barrier();
+      for (int j = lane; j < w; j += 64) {
+        const double t = lds[j * ld + k];
+        lds[j * ld + k] = lds[j * ld + piv];
+        lds[j * ld + piv] = t;
+      }
+      if (lane == 0) {
+        const int t = s_lp[k];
+        s_lp[k] = s_lp[piv];
+        s_lp[piv] = t;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    const double pv = lds[k * ld + k];
+    if (am > 0.0) gmax = fmax(gmax, am / fabs(pv));
+    double l[RPL];
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+      const int i = lane + 64 * r;
+      l[r] = 0.0;
+      if (i > k && i < R) {
+        l[r] = lds[k * ld + i] / pv;
+        lds[k * ld + i] = l[r];
+      }
+    }
+    // rank-1 update of the lane's rows; columns unrolled by 4 for independent LDS loads
+    int j = k + 1;
+    for (; j + 4 <= w; j += 4) {
+      double u[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) u[q] = lds[(j + q) * ld + k];
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        const int i = lane + 64 * r;
+        if (i > k && i < R) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) lds[(j + q) * ld + i] = fma(-l[r], u[q], lds[(j + q) * ld + i]);
+        }
+      }
+    }
+    for (; j < w; ++j) {
+      const double u = lds[j * ld + k];
+#pragma unroll
+      for (int r = 0; r < RPL; ++r) {
+        const int i = lane + 64 * r;
+        if (i > k && i < R) lds[j * ld + i] = fma(-l[r], u, lds[j * ld + i]);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  for (int j = 0; j < w; ++j)
+#pragma unroll
+    for (int r = 0; r < RPL; ++r) {
+      const int i = lane + 64 * r;
+      if (i < R) P[(int64_t)j * M + i] = lds[j * ld + i];
+    }
+  // compose the row permutation of positions [kb, kb+R) and publish the moved rows
+  int32_t* rp = rowperm + s.first + kb;
+  int* old = reinterpret_cast<int*>(lds);
+  __builtin_amdgcn_wave_barrier();
+  for (int i = lane; i < R; i += 64) old[i] = rp[i];
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  for (int i = lane; i < R; i += 64) rp[i] = old[s_lp[i]];
+  int32_t* sw = swaps + (int64_t)(slot0 + blockIdx.x) * swap_stride;
+  int cnt = 0;
+  for (int base = 0; base < R; base += 64) {
+    const int i = base + lane;
+    const bool mv = i < R && s_lp[i] != i;
+    const unsigned long long m = __ballot(mv);
+    if (mv) {
+      const int pos = cnt + __popcll(m & ((1ull << lane) - 1ull));
+      sw[1 + 2 * pos] = i;
+      sw[2 + 2 * pos] = s_lp[i];
+    }
+    cnt += __popcll(m);
+  }
+  if (lane == 0) sw[0] = cnt;
+  gmax = wave_max(gmax);
+  if (lane == 0) {
+    if (gmax > 0.0) atomic_max_pos(&growth[0], gmax);
+    if (flag) publish_info(info + sid, flag, err);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Panel factorization with the candidate rows in REGISTERS: thread t owns candidate row t
+// (R <= 64*NW) as row[0..W).  No physical row swaps: pos[t] is the row's current position
+// (LAPACK transposition semantics, so at most 2w rows move); who[] maps positions to threads.
+// Per column k: the diagonal candidate (position k) is accepted when no other candidate
+// exceeds |a_kk|/diag_tol (one ballot per wave); only otherwise a full argmax runs.  The
+// pivot row is broadcast through LDS; each thread updates its own row in registers.
+// ------------------------------------------------------------------------------------
+template <int W, int NW>
+__global__ __launch_bounds__(64 * NW) void k_panel_reg(const int32_t* __restrict__ list, int step,
+                                                       int slot0, const SNode* __restrict__ sn,
+                                                       double* __restrict__ store,
+                                                       double* __restrict__ scratch,
+                                                       int32_t* __restrict__ rowperm,
+                                                       int32_t* __restrict__ swaps,
+                                                       int64_t swap_stride,
+                                                       int32_t* __restrict__ info,
+                                                       double* __restrict__ growth, double diag_tol) {
+  static_assert(W == 32 || W == 64, "panel width");
+  __shared__ __attribute__((aligned(16))) double s_prow[64];
+  __shared__ int s_who[64 * NW];
+  __shared__ int s_old[64 * NW];
+  __shared__ double s_val[NW];
+  __shared__ int s_idx[NW];
+  __shared__ int s_any[NW];
+  __shared__ int s_piv;
+  const int sid = list[blockIdx.x];
+  const SNode s = sn[sid];
+  FrontPtrs f = front_ptrs(s, store, scratch);
+  const int64_t M = f.M;
+  const int ns = (int)f.ns;
+  const int kb = step * s.nb;
+  const int w = min(s.nb, ns - kb);
+  const int R = (s.mode == 1) ? ns - kb : w;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const bool has = tid < R;
+  double* P = f.L + (int64_t)kb * M + kb;
+  double rA[32], rB[32];   // columns [0,32) and [32,64) of my candidate row
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    rA[j] = (has && j < w) ? P[(int64_t)j * M + tid] : 0.0;
+    rB[j] = (W == 64 && has && j + 32 < w) ? P[(int64_t)(j + 32) * M + tid] : 0.0;
+  }
+  int pos = tid;
+  s_who[tid] = tid;
+  int flag = 0, err = -1;
+  double lmax = 0.0;
+  __syncthreads();
+  // one elimination step at panel column kabs; `cur` holds that column at index kk, `rest`
+  // (when RESTB) is the whole second half that is updated too
+  // the pivot-candidate lane writes its row halves with 16-byte LDS stores (entries left of
+  // the current column are written too; nobody reads them in this step)
+  auto publish = [&](double (&cur)[32], double (&rest)[32], const int base, const bool restb) {
+    double2* d = reinterpret_cast<double2*>(s_prow + base);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) d[j] = make_double2(cur[2 * j], cur[2 * j + 1]);
+    if (restb) {
+      double2* d2 = reinterpret_cast<double2*>(s_prow + 32);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) d2[j] = make_double2(rest[2 * j], rest[2 * j + 1]);
+    }
+  };
+  auto column = [&](double (&cur)[32], double (&rest)[32], const int kk, const int kabs,
+                    const bool restb) {
+    const int q = s_who[kabs];
+    const bool cand = has && pos >= kabs;
+    // optimistic: the diagonal candidate publishes its whole row (the pivot row if accepted)
+    if (tid == q) publish(cur, rest, kabs - kk, restb);
+    __syncthreads();
+    const double akk = s_prow[kabs];
+    const bool beats = cand && pos != kabs && fabs(cur[kk]) * diag_tol > fabs(akk);
+    bool any = __ballot(beats) != 0ull;
+    if (NW > 1) {
+      if (lane == 0) s_any[wv] = any ? 1 : 0;
+      __syncthreads();
+      any = false;
+#pragma unroll
+      for (int v = 0; v < NW; ++v) any |= s_any[v] != 0;
+    }
+    int p = q;
+    if (any || akk == 0.0) {   // full argmax over the candidates (rare under dominance)
+      double am = cand ? fabs(cur[kk]) : -1.0;
+      int ai = cand ? pos : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(am, o, 64);
+        const int oi = __shfl_xor(ai, o, 64);
+        if (ov > am || (ov == am && oi < ai)) { am = ov; ai = oi; }
+      }
+      if (NW > 1) {
+        if (lane == 0) { s_val[wv] = am; s_idx[wv] = ai; }
+        __syncthreads();
+        am = s_val[0];
+        ai = s_idx[0];
+#pragma unroll
+        for (int v = 1; v < NW; ++v)
+          if (s_val[v] > am || (s_val[v] == am && s_idx[v] < ai)) { am = s_val[v]; ai = s_idx[v]; }
+      }
+      if (am <= 0.0) {
+        flag |= 1;
+        if (err < 0) err = kb + kabs;
+      } else {
+        p = s_who[ai];
+      }
+      if (p != q) {             // re-publish the chosen pivot row
+        __syncthreads();
+        if (tid == p) {
+          publish(cur, rest, kabs - kk, restb);
+          s_piv = pos;
+        }
+        __syncthreads();
+      }
+    }
+    const double pinv = recip(s_prow[kabs]);
+    if (cand && tid != p) {
+      const double l = cur[kk] * pinv;
+      cur[kk] = l;
+      lmax = fmax(lmax, fabs(l));
+      if (l != 0.0) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+          if (j > kk) cur[j] = fma(-l, s_prow[kabs - kk + j], cur[j]);
+        if (restb) {
+#pragma unroll
+          for (int j = 0; j < 32; ++j) rest[j] = fma(-l, s_prow[32 + j], rest[j]);
+        }
+      }
+    }
+    if (p != q) {               // transposition of positions kabs and ppos
+      const int ppos = s_piv;
+      if (tid == p) pos = kabs;
+      else if (tid == q) pos = ppos;
+      __syncthreads();
+      if (tid == 0) {
+        s_who[kabs] = p;
+        s_who[ppos] = q;
+      }
+    }
+    __syncthreads();
+  };
+#pragma unroll
+  for (int k = 0; k < 32; ++k)
+    if (k < w) column(rA, rB, k, k, W == 64 && w > 32);
+  if (W == 64) {
+#pragma unroll
+    for (int k = 0; k < 32; ++k)
+      if (k + 32 < w) column(rB, rA, k, k + 32, false);
+  }
+  if (has) {
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      if (j < w) P[(int64_t)j * M + pos] = rA[j];
+      if (W == 64 && j + 32 < w) P[(int64_t)(j + 32) * M + pos] = rB[j];
+    }
+  }
+  int32_t* rp = rowperm + s.first + kb;
+  if (has) s_old[tid] = rp[tid];
+  __syncthreads();
+  if (has) rp[pos] = s_old[tid];
+  int32_t* sw = swaps + (int64_t)(slot0 + blockIdx.x) * swap_stride;
+  const bool mv = has && pos != tid;
+  const unsigned long long m = __ballot(mv);
+  if (lane == 0) s_any[wv] = __popcll(m);
+  __syncthreads();
+  int base = 0;
+  for (int v = 0; v < wv; ++v) base += s_any[v];
+  if (mv) {
+    const int o = base + __popcll(m & ((1ull << lane) - 1ull));
+    sw[1 + 2 * o] = pos;
+    sw[2 + 2 * o] = tid;
+  }
+  if (tid == 0) {
+    int tot = 0;
+    for (int v = 0; v < NW; ++v) tot += s_any[v];
+    sw[0] = tot;
+  }
+  lmax = wave_max(lmax);
+  if (lane == 0) s_val[wv] = lmax;
+  __syncthreads();
+  if (tid == 0) {
+    double g = 0.0;
+    for (int v = 0; v < NW; ++v) g = fmax(g, s_val[v]);
+    if (g > 0.0) atomic_max_pos(&growth[0], g);
+    if (flag) publish_info(info + sid, flag, err);
+  }
+}
+
+// Row swaps of the panel at kb applied to every column outside the panel (all fronts of the
+// step, grid-stride; a front without swaps costs one load).  Runs before the TRSM kernels.
+__global__ __launch_bounds__(256) void k_laswp(const FrontTile* __restrict__ ft, int nft,
+                                               const SNode* __restrict__ sn,
+                                               double* __restrict__ store,
+                                               double* __restrict__ scratch,
+                                               const int32_t* __restrict__ swaps, int64_t swap_stride) {
+  __shared__ double buf[64 * 65];   // [column][moved row]
+  for (int fi = blockIdx.x; fi < nft; fi += gridDim.x) {
+    const int32_t* sw = swaps + (int64_t)fi * swap_stride;
+    const int nsw = sw[0];
+    if (nsw == 0) continue;   // uniform per workgroup
+    const SNode s = sn[ft[fi].s];
+    FrontPtrs f = front_ptrs(s, store, scratch);
+    const int64_t M = f.M;
+    const int kb = ft[fi].pad;
+    const int w = min(s.nb, (int)f.ns - kb);
+    const int cnt = min(64, nsw);
+    for (int64_t c0 = 0; c0 < M - w; c0 += 64) {
+      const int ncol = (int)min<int64_t>(64, M - w - c0);
+      for (int idx = threadIdx.x; idx < cnt * ncol; idx += 256) {
+        const int p = idx % cnt, cj = idx / cnt;
+        const int64_t c = c0 + cj, col = c < kb ? c : c + w;
+        buf[cj * 65 + p] = *fel(f, kb + sw[2 + 2 * p], col);
+      }
+      __syncthreads();
+      for (int idx = threadIdx.x; idx < cnt * ncol; idx += 256) {
+        const int p = idx % cnt, cj = idx / cnt;
+        const int64_t c = c0 + cj, col = c < kb ? c : c + w;
+        *fel(f, kb + sw[1 + 2 * p], col) = buf[cj * 65 + p];
+      }
+      __syncthreads();
+    }
   }
 }
 
@@ -367,14 +744,24 @@ __device__ __forceinline__ int find_front_tile(const FrontTile* __restrict__ ft,
   return lo;
 }
 
-__global__ __launch_bounds__(256) void k_laswp_trsm_u(const FrontTile* __restrict__ ft, int nft,
-                                                      int step, const SNode* __restrict__ sn,
-                                                      double* __restrict__ store,
-                                                      double* __restrict__ scratch,
-                                                      const int32_t* __restrict__ swaps,
-                                                      int64_t swap_stride) {
-  __shared__ double sL[64 * 65];      // L_kk, unit lower (w <= 64), ld 65
-  __shared__ double sX[64 * 65];      // 64 columns x w rows, ld 65 ; reused as swap buffer
+// Two-level blocking: inner panels (nb = 32/64 columns) are grouped in outer blocks of OB = 256
+// columns [ostart, oend).  mode 0 (inner step, panel at kb): apply the panel's row swaps to
+// every column outside the panel; TRSM only the columns inside the outer block [kb+w, oend).
+// mode 1 (outer phase, sub-panel at kb): TRSM rows [kb, kb+w) on the columns right of the
+// outer block [oend, M); no swaps (already applied).  kb comes from FrontTile.pad.
+template <int W>
+__global__ __launch_bounds__(256) void k_trsm_u(const FrontTile* __restrict__ ft, int nft, int OB,
+                                                int mode, const SNode* __restrict__ sn,
+                                                double* __restrict__ store,
+                                                double* __restrict__ scratch,
+                                                const int32_t* __restrict__ swaps,
+                                                int64_t swap_stride) {
+  // outer phase (mode 1): U rows [kb, kb+w) of the columns [oend, M), kb = FrontTile.pad;
+  // one thread per column, the column in registers, L_kk broadcast from LDS
+  (void)mode;
+  (void)swaps;
+  (void)swap_stride;
+  __shared__ double sT[W * W];
   const int64_t b = blockIdx.x;
   const int fi = find_front_tile(ft, nft, b);
   const SNode s = sn[ft[fi].s];
@@ -382,66 +769,34 @@ __global__ __launch_bounds__(256) void k_laswp_trsm_u(const FrontTile* __restric
   FrontPtrs f = front_ptrs(s, store, scratch);
   const int64_t M = f.M;
   const int ns = (int)f.ns;
-  const int kb = step * s.nb;
+  const int kb = ft[fi].pad;
   const int w = min(s.nb, ns - kb);
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int32_t* sw = swaps + (int64_t)fi * swap_stride;
-  const int nsw = sw[0];
-  const int64_t c0 = tile * 64;
-  const int64_t nout = M - w;
-  const int ncol = (int)min<int64_t>(64, nout - c0);
-  if (ncol <= 0) return;
-  // --- row permutation on these columns (rows are relative to kb) ---
-  if (nsw > 0) {
-    // process swap list in chunks of 64 moved rows
-    for (int base = 0; base < nsw; base += 64) {
-      int cnt = min(64, nsw - base);
-      for (int idx = tid; idx < cnt * ncol; idx += 256) {
-        int pi = idx % cnt, cj = idx / cnt;
-        int64_t c = c0 + cj;
-        int64_t col = c < kb ? c : c + w;
-        sX[cj * 65 + pi] = *fel(f, kb + sw[2 + 2 * (base + pi)], col);
-      }
-      __syncthreads();
-      for (int idx = tid; idx < cnt * ncol; idx += 256) {
-        int pi = idx % cnt, cj = idx / cnt;
-        int64_t c = c0 + cj;
-        int64_t col = c < kb ? c : c + w;
-        *fel(f, kb + sw[1 + 2 * (base + pi)], col) = sX[cj * 65 + pi];
-      }
-      __syncthreads();
-      // a later chunk may read rows written by an earlier chunk only if they alias; swap
-      // lists are permutations so sources of chunk 2 may be destinations of chunk 1 -> the
-      // whole list is handled in one chunk when nsw <= 64 (always true for nb <= 32 full
-      // mode and nb <= 64 tile mode, since moved rows <= 2*nb and tile mode moves <= w).
-    }
-  }
-  // --- TRSM on right-hand columns only ---
-  if (c0 + ncol <= kb) return;  // tile entirely left of the panel
+  const int64_t ostart = (int64_t)(kb / OB) * OB;
+  const int64_t oend = min<int64_t>(ns, ostart + OB);
+  const int tid = threadIdx.x;
   const double* Lkk = f.L + (int64_t)kb * M + kb;
-  for (int j = wv; j < w; j += 4)
-    for (int i = lane; i < w; i += 64) sL[j * 65 + i] = Lkk[(int64_t)j * M + i];
-  for (int cj = wv; cj < ncol; cj += 4) {
-    int64_t c = c0 + cj;
-    if (c < kb) continue;
-    int64_t col = c + w;
-    for (int i = lane; i < w; i += 64) sX[cj * 65 + i] = *fel(f, kb + i, col);
+  for (int idx = tid; idx < W * W; idx += 256) {
+    const int i = idx % W, j = idx / W;
+    sT[idx] = (i < w && j < w) ? Lkk[(int64_t)j * M + i] : 0.0;
   }
   __syncthreads();
-  if (tid < ncol && c0 + tid >= kb) {
-    double* x = sX + tid * 65;
-    for (int j = 0; j < w; ++j) {
+  const int64_t col = oend + tile * 256 + tid;
+  if (col >= M) return;
+  double* cp = fel(f, kb, col);
+  double x[W];
+#pragma unroll
+  for (int j = 0; j < W; ++j) x[j] = j < w ? cp[j] : 0.0;
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    if (j < w) {
       const double xj = x[j];
-      for (int i = j + 1; i < w; ++i) x[i] = fma(-sL[j * 65 + i], xj, x[i]);
+#pragma unroll
+      for (int i = j + 1; i < W; ++i) x[i] = fma(-sT[j * W + i], xj, x[i]);
     }
   }
-  __syncthreads();
-  for (int cj = wv; cj < ncol; cj += 4) {
-    int64_t c = c0 + cj;
-    if (c < kb) continue;
-    int64_t col = c + w;
-    for (int i = lane; i < w; i += 64) *fel(f, kb + i, col) = sX[cj * 65 + i];
-  }
+#pragma unroll
+  for (int j = 0; j < W; ++j)
+    if (j < w) cp[j] = x[j];
 }
 
 // ------------------------------------------------------------------------------------
@@ -501,6 +856,117 @@ __global__ __launch_bounds__(256) void k_trsm_l(const FrontTile* __restrict__ ft
   __syncthreads();
   if (tid == 0) {
     double g = fmax(fmax(s_red[0], s_red[1]), fmax(s_red[2], s_red[3]));
+    if (g > 0.0) atomic_max_pos(&growth[0], g);
+    if (g > 1.0 / piv_tol) atomicOr(&info[sid], 2);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// One launch per inner step for both triangular solves of the panel (row swaps already
+// applied by k_laswp):
+//   role U (workgroups [0, nU)): U[kb:kb+w, c] = L_kk^{-1} A[kb:kb+w, c] for the columns
+//     c in [kb+w, oend) of the outer block, one thread per column, the column in registers,
+//     L_kk broadcast from LDS;
+//   role L (workgroups [nU, nU+nL)): rows below the candidate block, L = A U_kk^{-1}, one
+//     thread per row in registers, U_kk broadcast from LDS; growth max for the threshold test.
+// ------------------------------------------------------------------------------------
+template <int W>
+__global__ __launch_bounds__(256) void k_step_trsm(const FrontTile* __restrict__ ftU, int nftU, int64_t nU,
+                                                   const FrontTile* __restrict__ ftL, int nftL,
+                                                   int step, int OB, const SNode* __restrict__ sn,
+                                                   double* __restrict__ store,
+                                                   double* __restrict__ scratch,
+                                                   int32_t* __restrict__ info,
+                                                   double* __restrict__ growth, double piv_tol) {
+  __shared__ double sT[W * W];   // L_kk (role U) or U_kk (role L), [col][row]
+  __shared__ double s_rd[W];     // 1 / diag(U_kk) (role L)
+  __shared__ double s_red[4];
+  const int64_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (b < nU) {
+    const int fi = find_front_tile(ftU, nftU, b);
+    const SNode s = sn[ftU[fi].s];
+    const int64_t tile = b - ftU[fi].wg0;
+    FrontPtrs f = front_ptrs(s, store, scratch);
+    const int64_t M = f.M;
+    const int ns = (int)f.ns;
+    const int kb = ftU[fi].pad;
+    const int w = min(s.nb, ns - kb);
+    const int64_t ostart = (int64_t)(kb / OB) * OB;
+    const int64_t oend = min<int64_t>(ns, ostart + OB);
+    const double* Lkk = f.L + (int64_t)kb * M + kb;
+    for (int idx = tid; idx < W * W; idx += 256) {
+      const int i = idx % W, j = idx / W;
+      sT[idx] = (i < w && j < w) ? Lkk[(int64_t)j * M + i] : 0.0;
+    }
+    __syncthreads();
+    const int64_t col = kb + w + tile * 256 + tid;
+    if (col < oend) {
+      double* cp = fel(f, kb, col);   // rows [kb, kb+w) of this column are contiguous
+      double x[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) x[j] = j < w ? cp[j] : 0.0;
+      // the runtime guard splits the unrolled solve into per-step blocks; without it the
+      // scheduler hoists all 2016 LDS reads into one block and spills
+#pragma unroll
+      for (int j = 0; j < W; ++j) {
+        if (j < w) {
+          const double xj = x[j];
+#pragma unroll
+          for (int i = j + 1; i < W; ++i) x[i] = fma(-sT[j * W + i], xj, x[i]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < W; ++j)
+        if (j < w) cp[j] = x[j];
+    }
+    return;
+  }
+  // role L
+  const int64_t bl = b - nU;
+  const int fi = find_front_tile(ftL, nftL, bl);
+  const int sid = ftL[fi].s;
+  const SNode s = sn[sid];
+  const int64_t tile = bl - ftL[fi].wg0;
+  FrontPtrs f = front_ptrs(s, store, scratch);
+  const int64_t M = f.M;
+  const int ns = (int)f.ns;
+  const int kb = step * s.nb;
+  const int w = min(s.nb, ns - kb);
+  const int R = (s.mode == 1) ? ns - kb : w;
+  const int64_t r0 = kb + R;
+  double* P = f.L + (int64_t)kb * M;
+  for (int idx = tid; idx < W * W; idx += 256) {
+    const int i = idx % W, j = idx / W;
+    sT[idx] = (i < w && j < w) ? P[(int64_t)j * M + kb + i] : 0.0;
+  }
+  __syncthreads();
+  if (tid < W) s_rd[tid] = tid < w ? recip(sT[tid * W + tid]) : 0.0;
+  __syncthreads();
+  const int64_t row = r0 + tile * 256 + tid;
+  double gmax = 0.0;
+  if (row < M) {
+    double x[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) x[j] = (j < w) ? P[(int64_t)j * M + row] : 0.0;
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      if (j < w) {
+        x[j] = x[j] * s_rd[j];
+        gmax = fmax(gmax, fabs(x[j]));
+#pragma unroll
+        for (int k = j + 1; k < W; ++k) x[k] = fma(-x[j], sT[k * W + j], x[k]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < W; ++j)
+      if (j < w) P[(int64_t)j * M + row] = x[j];
+  }
+  gmax = wave_max(gmax);
+  if ((tid & 63) == 0) s_red[tid >> 6] = gmax;
+  __syncthreads();
+  if (tid == 0) {
+    const double g = fmax(fmax(s_red[0], s_red[1]), fmax(s_red[2], s_red[3]));
     if (g > 0.0) atomic_max_pos(&growth[0], g);
     if (g > 1.0 / piv_tol) atomicOr(&info[sid], 2);
   }
@@ -691,6 +1157,94 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__
 }
 
 // ------------------------------------------------------------------------------------
+// Optional fp64 MFMA variant of the same 128x128 tile (opts.use_mfma; default off: the north
+// star asks for no MFMA).  v_mfma_f64_16x16x4_f64; each wave owns a 64x64 quadrant = 4x4
+// blocks.  The product is formed as C^T = B^T A^T so that the accumulator's lane index runs
+// along C's rows (column-major C stays coalesced): lane l of block (bi,bj) holds
+// C[row = 16 bi + (l & 15)][col = 16 bj + (l >> 4) + 4 r], r = 0..3.
+// ------------------------------------------------------------------------------------
+typedef double v4d __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restrict__ tasks, int ntask) {
+  __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
+  __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
+  const int64_t b = blockIdx.x;
+  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+  const int64_t tl = b - t.tile0;
+  const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
+  const int m0 = tm * HBM_, n0 = tn * HBM_;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = (wv & 1) * 64, wc = (wv >> 1) * 64;   // wave quadrant (rows, cols)
+  v4d acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (v4d){0.0, 0.0, 0.0, 0.0};
+  const int ar = tid & 127, ak = tid >> 7;
+  const int bk = tid & 15, bc = tid >> 4;
+  const int K = t.k;
+  const int arow = m0 + ar;
+  const bool arow_ok = arow < t.m;
+  const double* Ap = t.A + arow;
+  double ra[8], rb[8];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int kk = k0 + ak + 2 * r;
+      ra[r] = (arow_ok && kk < K) ? Ap[(int64_t)kk * t.lda] : 0.0;
+      const int col = n0 + bc + 16 * r;
+      rb[r] = (col < t.n && k0 + bk < K) ? t.B[(int64_t)col * t.ldb + k0 + bk] : 0.0;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      As[buf][ak + 2 * r][ar] = ra[r];
+      Bs[buf][bk][bc + 16 * r] = rb[r];
+    }
+  };
+  const int nk = (K + HBK_ - 1) / HBK_;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  const int li = lane & 15, lk = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * HBK_);
+#pragma unroll
+    for (int kq = 0; kq < HBK_ / 4; ++kq) {
+      const int k = kq * 4 + lk;
+      double fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = As[cur][k][wr + 16 * i + li];   // A[row][k]
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = Bs[cur][k][wc + 16 * j + li];   // B[k][col]
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = m0 + wr + 16 * i + li;
+    if (row >= t.m) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = n0 + wc + 16 * j + lk + 4 * r;
+        if (col < t.n) {
+          double* c = t.C + (int64_t)col * t.ldc + row;
+          *c = *c - acc[i][j][r];
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Solves.  Front vectors v_s (M doubles) live in vbuf[voff[s]].
 // Forward (L): gather own rows + children's update vectors, apply the front's row
 // permutation, unit-lower solve of the diagonal block in 64-column blocks (one wave does
@@ -779,7 +1333,7 @@ __global__ __launch_bounds__(256) void k_bwd_front(const int32_t* __restrict__ l
     if (wv == 0) {
       double xi = lane < bw ? v[jb + lane] : 0.0;
       for (int j = bw - 1; j >= 0; --j) {
-        if (lane == j) xi = xi / Lp[(jb + j) * M + jb + j];
+        if (lane == j) xi = xi * recip(Lp[(jb + j) * M + jb + j]);
         double xj = __shfl(xi, j, 64);
         if (lane < j) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
       }
@@ -858,7 +1412,7 @@ __global__ __launch_bounds__(256) void k_tri_block(const FrontTile* __restrict__
       }
     } else {
       for (int j = bw - 1; j >= 0; --j) {
-        if (lane == j) xi = xi / Lp[(jb + j) * M + jb + j];
+        if (lane == j) xi = xi * recip(Lp[(jb + j) * M + jb + j]);
         double xj = __shfl(xi, j, 64);
         if (lane < j) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
       }
@@ -940,6 +1494,21 @@ __global__ void k_unswap(int64_t n, const int64_t* __restrict__ pos_first,
 // ------------------------------------------------------------------------------------
 static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
+// Dynamic LDS above 64 KiB must be enabled per kernel before launch (and before any capture).
+hipError_t init_kernel_attributes() {
+  hipError_t e = hipFuncSetAttribute((const void*)k_front_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)k_panel, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+  if (e != hipSuccess) return e;
+  const void* ks[4] = {(const void*)k_panel1<1>, (const void*)k_panel1<2>, (const void*)k_panel1<4>,
+                       (const void*)k_panel1<8>};
+  for (auto k : ks) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 hipError_t launch_rowscale(hipStream_t st, int64_t n, const int64_t* rowptr, const int32_t* ent,
                            const double* a, double* Rs) {
   if (n <= 0) return hipSuccess;
@@ -969,36 +1538,59 @@ hipError_t launch_front_lds(hipStream_t st, int cnt, int Mmax, const int32_t* li
                             double* growth, double diag_tol, double piv_tol) {
   if (cnt <= 0) return hipSuccess;
   size_t lds = (size_t)Mmax * (size_t)(Mmax | 1) * sizeof(double);
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_front_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
   k_front_lds<<<cnt, 256, lds, st>>>(list, sn, store, scratch, rowperm, info, growth, diag_tol, piv_tol);
   return hipGetLastError();
 }
-hipError_t launch_panel(hipStream_t st, int cnt, int lds_doubles, int step, const int32_t* list,
+hipError_t launch_panel(hipStream_t st, int cnt, int lds_doubles, int step, int slot0, const int32_t* list,
                         const SNode* sn, double* store, double* scratch, int32_t* rowperm,
                         int32_t* swaps, int64_t swap_stride, int32_t* info, double* growth,
                         double diag_tol) {
   if (cnt <= 0) return hipSuccess;
   size_t lds = (size_t)lds_doubles * sizeof(double);
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_panel, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  k_panel<<<cnt, 256, lds, st>>>(list, step, sn, store, scratch, rowperm, swaps, swap_stride, info,
+  k_panel<<<cnt, 256, lds, st>>>(list, step, slot0, sn, store, scratch, rowperm, swaps, swap_stride, info,
                                  growth, diag_tol);
   return hipGetLastError();
 }
-hipError_t launch_laswp_trsm_u(hipStream_t st, int64_t nwg, const FrontTile* ft, int nft, int step,
-                               const SNode* sn, double* store, double* scratch,
-                               const int32_t* swaps, int64_t swap_stride) {
+hipError_t launch_panel1(hipStream_t st, int cnt, int lds_doubles, int rmax, int wmax, int step,
+                         int slot0, const int32_t* list,
+                         const SNode* sn, double* store, double* scratch, int32_t* rowperm,
+                         int32_t* swaps, int64_t swap_stride, int32_t* info, double* growth,
+                         double diag_tol) {
+  if (cnt <= 0) return hipSuccess;
+  size_t lds = (size_t)lds_doubles * sizeof(double);
+#define PANEL1_ARGS list, step, slot0, sn, store, scratch, rowperm, swaps, swap_stride, info, growth, diag_tol
+  (void)lds;
+  if (wmax > 32) k_panel_reg<64, 1><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
+  else if (rmax <= 64) k_panel_reg<32, 1><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
+  else if (rmax <= 128) k_panel_reg<32, 2><<<cnt, 128, 0, st>>>(PANEL1_ARGS);
+  else if (rmax <= 256) k_panel_reg<32, 4><<<cnt, 256, 0, st>>>(PANEL1_ARGS);
+  else k_panel_reg<32, 8><<<cnt, 512, 0, st>>>(PANEL1_ARGS);
+#undef PANEL1_ARGS
+  return hipGetLastError();
+}
+hipError_t launch_laswp(hipStream_t st, const FrontTile* ft, int nft, const SNode* sn, double* store,
+                        double* scratch, const int32_t* swaps, int64_t swap_stride) {
+  if (nft <= 0) return hipSuccess;
+  k_laswp<<<(unsigned)min(nft, 1024), 256, 0, st>>>(ft, nft, sn, store, scratch, swaps, swap_stride);
+  return hipGetLastError();
+}
+hipError_t launch_step_trsm(hipStream_t st, int W, const FrontTile* ftU, int nftU, int64_t nU,
+                            const FrontTile* ftL, int nftL, int64_t nL, int step, int OB, const SNode* sn,
+                            double* store, double* scratch, int32_t* info, double* growth, double piv_tol) {
+  if (nU + nL <= 0) return hipSuccess;
+  if (W <= 32)
+    k_step_trsm<32><<<(unsigned)(nU + nL), 256, 0, st>>>(ftU, nftU, nU, ftL, nftL, step, OB, sn, store,
+                                                         scratch, info, growth, piv_tol);
+  else
+    k_step_trsm<64><<<(unsigned)(nU + nL), 256, 0, st>>>(ftU, nftU, nU, ftL, nftL, step, OB, sn, store,
+                                                         scratch, info, growth, piv_tol);
+  return hipGetLastError();
+}
+hipError_t launch_trsm_u(hipStream_t st, int64_t nwg, const FrontTile* ft, int nft, int OB, int mode,
+                         const SNode* sn, double* store, double* scratch, const int32_t* swaps,
+                         int64_t swap_stride) {
   if (nwg <= 0) return hipSuccess;
-  k_laswp_trsm_u<<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, scratch, swaps, swap_stride);
+  k_trsm_u<64><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, OB, mode, sn, store, scratch, swaps, swap_stride);
   return hipGetLastError();
 }
 hipError_t launch_trsm_l(hipStream_t st, int64_t nwg, int W, const FrontTile* ft, int nft, int step,
@@ -1013,7 +1605,8 @@ hipError_t launch_trsm_l(hipStream_t st, int64_t nwg, int W, const FrontTile* ft
 }
 hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask, int tile) {
   if (ntiles <= 0) return hipSuccess;
-  if (tile == 128) k_gemm128<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
+  if (tile == 129) k_gemm128_mfma<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
+  else if (tile == 128) k_gemm128<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
   else k_gemm<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
   return hipGetLastError();
 }

@@ -35,10 +35,17 @@ hipError_t launch_extend_add(hipStream_t, int64_t, const int2*, const SNode*, co
                              double*);
 hipError_t launch_front_lds(hipStream_t, int, int, const int32_t*, const SNode*, double*, double*,
                             int32_t*, int32_t*, double*, double, double);
-hipError_t launch_panel(hipStream_t, int, int, int, const int32_t*, const SNode*, double*, double*,
+hipError_t init_kernel_attributes();
+hipError_t launch_panel(hipStream_t, int, int, int, int, const int32_t*, const SNode*, double*, double*,
                         int32_t*, int32_t*, int64_t, int32_t*, double*, double);
-hipError_t launch_laswp_trsm_u(hipStream_t, int64_t, const FrontTile*, int, int, const SNode*, double*,
-                               double*, const int32_t*, int64_t);
+hipError_t launch_panel1(hipStream_t, int, int, int, int, int, int, const int32_t*, const SNode*, double*, double*,
+                         int32_t*, int32_t*, int64_t, int32_t*, double*, double);
+hipError_t launch_step_trsm(hipStream_t, int, const FrontTile*, int, int64_t, const FrontTile*, int, int64_t,
+                            int, int, const SNode*, double*, double*, int32_t*, double*, double);
+hipError_t launch_laswp(hipStream_t, const FrontTile*, int, const SNode*, double*, double*, const int32_t*,
+                        int64_t);
+hipError_t launch_trsm_u(hipStream_t, int64_t, const FrontTile*, int, int, int, const SNode*, double*,
+                         double*, const int32_t*, int64_t);
 hipError_t launch_trsm_l(hipStream_t, int64_t, int, const FrontTile*, int, int, const SNode*, double*,
                          double*, int32_t*, double*, double);
 hipError_t launch_gemm(hipStream_t, int64_t, const GemmTask*, int, int);
@@ -66,22 +73,24 @@ constexpr int kFullPivNs = 512;  // blocked fronts up to this many pivots search
 constexpr int kNbFull = 32;
 constexpr int kNbTile = 64;
 constexpr int kSwapStride = 1 + 2 * 64;
+constexpr int kOB = 256;        // outer block of the two-level blocked front factorization
 
 thread_local std::string g_last_error;
 
 enum Kind : int {
   K_MEMSET_STORE, K_MEMSET_SCRATCH, K_SCATTER, K_EXTADD, K_FRONT_LDS, K_PANEL, K_TRSMU, K_TRSML,
-  K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_NKIND
+  K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_GEMM22, K_LASWP, K_STEPTRSM, K_NKIND
 };
 const char* kKindName[K_NKIND] = {"memset", "memset", "assemble", "assemble", "small", "panel",
                                   "trsm", "trsm", "gemm", "solve", "solve", "solve", "solve",
-                                  "solve", "solve"};
+                                  "solve", "solve", "gemm22", "trsm", "trsm"};
 constexpr int kSolveBigNs = 256;  // fronts with more pivots use the multi-workgroup solve
 
 struct Launch {
   int kind = 0;
   int step = 0;
   int64_t off = 0, cnt = 0, nwg = 0, aux = 0, aux2 = 0;
+  int64_t off2 = 0, cnt2 = 0, nwg2 = 0;   // second work list (merged launches)
   double flops = 0;
 };
 
@@ -132,7 +141,7 @@ struct smlu_handle {
   // schedule
   std::vector<Launch> fac, fwd, bwd;
   std::vector<SNode> hsn;
-  double gemm_flops = 0, dense_flops = 0;
+  double gemm_flops = 0, gemm22_flops = 0, dense_flops = 0;
   int64_t nlaunch = 0;
   // stats
   double refactor_ms = 0, solve_ms = 0, growth_max = 0;
@@ -141,9 +150,14 @@ struct smlu_handle {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   std::vector<int> ev_kind;
   int32_t* hinfo = nullptr;  // pinned
+  hipGraphExec_t fac_exec = nullptr, sol_exec = nullptr;
+  int fac_exec_profile = -1;
+  size_t fac_graph_events = 0;
+  bool graph_failed = false;
   ~smlu_handle() { release_all(); }
   void release_buffers() {
     if (stream) (void)hipSetDevice(device);
+    release_graphs();
     DBuf<double>* d[] = {&A, &Rs, &store, &scratch, &wrk, &wrk2, &vbuf, &growth};
     for (auto* b : d) b->free();
     DBuf<int64_t>* l[] = {&Arowptr, &Adest, &p0, &q, &posfirst};
@@ -155,7 +169,14 @@ struct smlu_handle {
     ftiles.free();
     gtasks.free();
   }
+  void release_graphs() {
+    if (fac_exec) (void)hipGraphExecDestroy(fac_exec);
+    if (sol_exec) (void)hipGraphExecDestroy(sol_exec);
+    fac_exec = sol_exec = nullptr;
+    fac_exec_profile = -1;
+  }
   void release_all() {
+    release_graphs();
     release_buffers();
     for (auto& e : ev_pool) {
       (void)hipEventDestroy(e.first);
@@ -253,6 +274,7 @@ static int build_schedule(smlu_handle* h) {
   double* scratch = h->scratch.p;
   h->fac.clear();
   h->gemm_flops = 0;
+  h->gemm22_flops = 0;
   h->dense_flops = P.flops;
   int64_t max_list = 1;
   // GEMM launches: 128x128 tiles when the launch has enough of them to fill the GPU,
@@ -262,16 +284,18 @@ static int build_schedule(smlu_handle* h) {
     int64_t t128 = 0;
     for (auto& g : cand) t128 += (int64_t)((g.m + 127) / 128) * ((g.n + 127) / 128);
     int tile = t128 >= 512 ? 128 : 64;
+    if (tile == 128 && h->opts.use_mfma) tile = 129;   // fp64 MFMA variant of the 128 tile
     Launch L;
-    L.kind = K_GEMM;
+    L.kind = step < 0 ? K_GEMM22 : K_GEMM;
     L.step = step;
     L.off = (int64_t)gt.size();
     L.aux = tile;
     int64_t tiles = 0;
+    const int ts = tile == 129 ? 128 : tile;
     for (auto& g : cand) {
-      g.tiles_m = (g.m + tile - 1) / tile;
+      g.tiles_m = (g.m + ts - 1) / ts;
       g.tile0 = tiles;
-      tiles += (int64_t)g.tiles_m * ((g.n + tile - 1) / tile);
+      tiles += (int64_t)g.tiles_m * ((g.n + ts - 1) / ts);
       gt.push_back(g);
     }
     L.cnt = (int64_t)cand.size();
@@ -279,6 +303,7 @@ static int build_schedule(smlu_handle* h) {
     L.flops = fl;
     h->fac.push_back(L);
     h->gemm_flops += fl;
+    if (step < 0) h->gemm22_flops += fl;
   };
   for (int l = 0; l < P.nlevels; ++l) {
     Launch L;
@@ -320,22 +345,26 @@ static int build_schedule(smlu_handle* h) {
       L.cnt = (int64_t)xt.size() - L.off;
       if (L.cnt > 0) h->fac.push_back(L);
     }
-    // small fronts
+    // small fronts, launched per size class so that small fronts get small LDS (occupancy)
     {
-      L = Launch();
-      L.kind = K_FRONT_LDS;
-      L.off = (int64_t)ilist.size();
-      int64_t Mmax = 0;
-      for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
-        int64_t s = P.lev_sup[k];
-        if (h->hsn[s].mode != 0) continue;
-        ilist.push_back((int32_t)s);
-        Mmax = std::max(Mmax, P.M(s));
+      const int64_t cls[4] = {32, 64, 96, kSmallM};
+      for (int c = 0; c < 4; ++c) {
+        L = Launch();
+        L.kind = K_FRONT_LDS;
+        L.off = (int64_t)ilist.size();
+        int64_t Mmax = 0;
+        for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+          int64_t s = P.lev_sup[k];
+          if (h->hsn[s].mode != 0) continue;
+          int64_t M = P.M(s);
+          if (M > cls[c] || (c > 0 && M <= cls[c - 1])) continue;
+          ilist.push_back((int32_t)s);
+          Mmax = std::max(Mmax, M);
+        }
+        L.cnt = (int64_t)ilist.size() - L.off;
+        L.aux = Mmax;
+        if (L.cnt > 0) h->fac.push_back(L);
       }
-      L.cnt = (int64_t)ilist.size() - L.off;
-      L.aux = Mmax;
-      if (L.cnt > 0) h->fac.push_back(L);
-      max_list = std::max(max_list, L.cnt);
     }
     // blocked fronts
     std::vector<int64_t> big;
@@ -355,67 +384,88 @@ static int build_schedule(smlu_handle* h) {
       }
       if (act.empty()) continue;
       max_list = std::max<int64_t>(max_list, (int64_t)act.size());
-      // panel
-      L = Launch();
-      L.kind = K_PANEL;
-      L.step = (int)t;
-      L.off = (int64_t)ilist.size();
-      int64_t ldsmax = 1, Rmax = 1;
-      for (auto s : act) {
+      // panel, split into LDS classes (act sorted by LDS need; swap slots = position in act)
+      // panel launch classes by register-kernel shape: (W=64, 1 wave), (W=32, 1/2/4/8 waves)
+      auto pclass = [&](int64_t s) {
         const SNode& r = h->hsn[s];
         int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
         int64_t R = r.mode == 1 ? r.ns - kb : w;
-        ldsmax = std::max(ldsmax, (R | 1) * w);
-        Rmax = std::max(Rmax, R);
-        ilist.push_back((int32_t)s);
+        if (r.nb > 32) return 0;
+        return R <= 64 ? 1 : R <= 128 ? 2 : R <= 256 ? 3 : 4;
+      };
+      std::stable_sort(act.begin(), act.end(), [&](int64_t a, int64_t b) { return pclass(a) < pclass(b); });
+      {
+        size_t pos = 0;
+        for (int c = 0; c < 5 && pos < act.size(); ++c) {
+          L = Launch();
+          L.kind = K_PANEL;
+          L.step = (int)t;
+          L.off = (int64_t)ilist.size();
+          L.aux2 = (int64_t)pos;  // first swap slot
+          int64_t rmax = 1, wmax = 1;
+          while (pos < act.size() && pclass(act[pos]) == c) {
+            const SNode& r = h->hsn[act[pos]];
+            int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
+            rmax = std::max(rmax, r.mode == 1 ? r.ns - kb : w);
+            wmax = std::max<int64_t>(wmax, r.nb);
+            ilist.push_back((int32_t)act[pos]);
+            ++pos;
+          }
+          L.cnt = (int64_t)ilist.size() - L.off;
+          L.aux = 0;
+          L.nwg = rmax | (wmax << 16);
+          if (L.cnt > 0) h->fac.push_back(L);
+        }
+        if (pos != act.size()) return fail(h, SMLU_ERR_ARG, "internal: panel classes");
       }
-      if (ldsmax * 8 > 148 * 1024 || Rmax > 512) return fail(h, SMLU_ERR_ARG, "internal: panel LDS budget");
+      // row swaps on every other column (cheap no-op without pivoting), then the U row block
+      // inside the outer block
+      L = Launch();
+      L.kind = K_LASWP;
+      L.step = (int)t;
+      L.off = (int64_t)ft.size();
+      for (auto s : act) ft.push_back(FrontTile{(int32_t)s, (int32_t)(t * h->hsn[s].nb), 0});
       L.cnt = (int64_t)act.size();
-      L.aux = ldsmax;
-      L.aux2 = Rmax;
       h->fac.push_back(L);
-      // laswp + trsm_u
-      L = Launch();
-      L.kind = K_TRSMU;
-      L.step = (int)t;
-      L.off = (int64_t)ft.size();
-      int64_t wg = 0;
-      for (auto s : act) {
-        const SNode& r = h->hsn[s];
-        int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
-        ft.push_back(FrontTile{(int32_t)s, 0, wg});
-        wg += (M - w + 63) / 64;
+      {
+        Launch T;
+        T.kind = K_STEPTRSM;
+        T.step = (int)t;
+        T.off = (int64_t)ft.size();
+        int64_t wgU = 0, W = 32;
+        for (auto s : act) {
+          const SNode& r = h->hsn[s];
+          int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
+          int64_t ostart = (kb / kOB) * kOB, oend = std::min<int64_t>(r.ns, ostart + kOB);
+          ft.push_back(FrontTile{(int32_t)s, (int32_t)kb, wgU});
+          wgU += (oend - kb - w + 255) / 256;
+          W = std::max<int64_t>(W, w);
+        }
+        T.cnt = (int64_t)act.size();
+        T.nwg = wgU;
+        T.off2 = (int64_t)ft.size();
+        int64_t wgL = 0;
+        for (auto s : act) {
+          const SNode& r = h->hsn[s];
+          int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
+          int64_t R = r.mode == 1 ? r.ns - kb : w;
+          ft.push_back(FrontTile{(int32_t)s, (int32_t)kb, wgL});
+          wgL += (M - kb - R + 255) / 256;
+        }
+        T.cnt2 = (int64_t)act.size();
+        T.nwg2 = wgL;
+        T.aux = W;
+        if (wgU + wgL > 0) h->fac.push_back(T);
       }
-      L.cnt = (int64_t)act.size();
-      L.nwg = wg;
-      if (wg > 0) h->fac.push_back(L);
-      // trsm_l
-      L = Launch();
-      L.kind = K_TRSML;
-      L.step = (int)t;
-      L.off = (int64_t)ft.size();
-      wg = 0;
-      int64_t W = 32;
-      for (auto s : act) {
-        const SNode& r = h->hsn[s];
-        int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
-        int64_t R = r.mode == 1 ? r.ns - kb : w;
-        ft.push_back(FrontTile{(int32_t)s, 0, wg});
-        wg += (M - kb - R + 255) / 256;
-        W = std::max<int64_t>(W, w);
-      }
-      L.cnt = (int64_t)act.size();
-      L.nwg = wg;
-      L.aux = W;
-      if (wg > 0) h->fac.push_back(L);
-      // trailing update of the pivot part (R1: L panel, R2: U12)
+      // inner trailing update: rows [kb+w, M) x columns [kb+w, oend) of the outer block
       {
         std::vector<GemmTask> cand;
         double fl = 0;
         for (auto s : act) {
           const SNode& r = h->hsn[s];
           int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
-          int64_t m1 = M - kb - w, n1 = r.ns - kb - w;
+          int64_t ostart = (kb / kOB) * kOB, oend = std::min<int64_t>(r.ns, ostart + kOB);
+          int64_t m1 = M - kb - w, n1 = oend - kb - w;
           if (m1 > 0 && n1 > 0) {
             GemmTask g{};
             g.A = store + r.Loff + kb * M + kb + w;
@@ -426,16 +476,103 @@ static int build_schedule(smlu_handle* h) {
             cand.push_back(g);
             fl += 2.0 * m1 * n1 * w;
           }
-          int64_t m2 = r.ns - kb - w, n2 = r.nu;
-          if (m2 > 0 && n2 > 0) {
+        }
+        add_gemm_launch(cand, fl, (int)t);
+      }
+      // outer phase for the fronts whose outer block ends with this panel
+      {
+        std::vector<int64_t> fin;
+        int64_t nsubmax = 0;
+        for (auto s : act) {
+          const SNode& r = h->hsn[s];
+          int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
+          int64_t ostart = (kb / kOB) * kOB, oend = std::min<int64_t>(r.ns, ostart + kOB);
+          if (kb + w != oend) continue;
+          int64_t M = (int64_t)r.ns + r.nu;
+          if (oend == M) continue;   // nothing right of the block
+          fin.push_back(s);
+          nsubmax = std::max<int64_t>(nsubmax, (oend - ostart + r.nb - 1) / r.nb);
+        }
+        for (int64_t u = 0; u < nsubmax; ++u) {
+          // (a) U row block of sub-panel u: TRSM on columns [oend, M)
+          L = Launch();
+          L.kind = K_TRSMU;
+          L.step = (int)t;
+          L.aux = 1;   // outer mode
+          L.off = (int64_t)ft.size();
+          int64_t wg = 0, cnt = 0;
+          std::vector<GemmTask> cand;
+          double fl = 0;
+          for (auto s : fin) {
+            const SNode& r = h->hsn[s];
+            int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb;
+            int64_t ostart = (kb / kOB) * kOB, oend = std::min<int64_t>(r.ns, ostart + kOB);
+            int64_t kbu = ostart + u * r.nb;
+            if (kbu >= oend) continue;
+            int64_t wu = std::min<int64_t>(r.nb, oend - kbu);
+            ft.push_back(FrontTile{(int32_t)s, (int32_t)kbu, wg});
+            wg += (M - oend + 255) / 256;
+            ++cnt;
+            // (b) rows below the sub-panel inside the block: [kbu+wu, oend) x [oend, M)
+            int64_t m = oend - kbu - wu;
+            if (m > 0) {
+              int64_t n1 = r.ns - oend;       // L-panel columns
+              if (n1 > 0) {
+                GemmTask g{};
+                g.A = store + r.Loff + kbu * M + kbu + wu;
+                g.B = store + r.Loff + oend * M + kbu;
+                g.C = store + r.Loff + oend * M + kbu + wu;
+                g.m = (int)m; g.n = (int)n1; g.k = (int)wu;
+                g.lda = (int)M; g.ldb = (int)M; g.ldc = (int)M;
+                cand.push_back(g);
+                fl += 2.0 * m * n1 * wu;
+              }
+              if (r.nu > 0) {                 // U12 columns
+                GemmTask g{};
+                g.A = store + r.Loff + kbu * M + kbu + wu;
+                g.B = store + r.Uoff + kbu;
+                g.C = store + r.Uoff + kbu + wu;
+                g.m = (int)m; g.n = r.nu; g.k = (int)wu;
+                g.lda = (int)M; g.ldb = r.ns; g.ldc = r.ns;
+                cand.push_back(g);
+                fl += 2.0 * m * (double)r.nu * wu;
+              }
+            }
+          }
+          L.cnt = cnt;
+          L.nwg = wg;
+          if (wg > 0) h->fac.push_back(L);
+          add_gemm_launch(cand, fl, (int)t);
+        }
+        // (c) outer trailing update with k = oend - ostart (<= 256)
+        std::vector<GemmTask> cand;
+        double fl = 0;
+        for (auto s : fin) {
+          const SNode& r = h->hsn[s];
+          int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb;
+          int64_t ostart = (kb / kOB) * kOB, oend = std::min<int64_t>(r.ns, ostart + kOB);
+          int64_t kk = oend - ostart;
+          int64_t m1 = M - oend, n1 = r.ns - oend;
+          if (m1 > 0 && n1 > 0) {       // rows [oend, M) x L-panel columns [oend, ns)
             GemmTask g{};
-            g.A = store + r.Loff + kb * M + kb + w;
-            g.B = store + r.Uoff + kb;
-            g.C = store + r.Uoff + kb + w;
-            g.m = (int)m2; g.n = (int)n2; g.k = (int)w;
+            g.A = store + r.Loff + ostart * M + oend;
+            g.B = store + r.Loff + oend * M + ostart;
+            g.C = store + r.Loff + oend * M + oend;
+            g.m = (int)m1; g.n = (int)n1; g.k = (int)kk;
+            g.lda = (int)M; g.ldb = (int)M; g.ldc = (int)M;
+            cand.push_back(g);
+            fl += 2.0 * m1 * n1 * kk;
+          }
+          int64_t m2 = r.ns - oend;
+          if (m2 > 0 && r.nu > 0) {     // rows [oend, ns) x U12 columns
+            GemmTask g{};
+            g.A = store + r.Loff + ostart * M + oend;
+            g.B = store + r.Uoff + ostart;
+            g.C = store + r.Uoff + oend;
+            g.m = (int)m2; g.n = r.nu; g.k = (int)kk;
             g.lda = (int)M; g.ldb = r.ns; g.ldc = r.ns;
             cand.push_back(g);
-            fl += 2.0 * m2 * n2 * w;
+            fl += 2.0 * m2 * (double)r.nu * kk;
           }
         }
         add_gemm_launch(cand, fl, (int)t);
@@ -593,6 +730,7 @@ static int setup_device(smlu_handle* h) {
     HIPCHK(h->rowperm0.upload(id.data(), id.size(), st));
   }
   HIPCHK(h->info.alloc((size_t)std::max<int64_t>(P.nsup, 1)));
+  HIPCHK(init_kernel_attributes());
   if (h->hinfo) HIPCHK(hipHostFree(h->hinfo));
   h->hinfo = nullptr;
   HIPCHK(hipHostMalloc((void**)&h->hinfo, sizeof(int32_t) * std::max<int64_t>(P.nsup, 1), 0));
@@ -647,29 +785,35 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
     case K_FRONT_LDS:
       return launch_front_lds(st, (int)L.cnt, (int)L.aux, h->ilist.p + L.off, h->sn.p, h->store.p,
                               h->scratch.p, h->rowperm.p, h->info.p, h->growth.p, diag_tol, piv_tol);
+    case K_STEPTRSM:
+      return launch_step_trsm(st, (int)L.aux, h->ftiles.p + L.off, (int)L.cnt, L.nwg, h->ftiles.p + L.off2,
+                              (int)L.cnt2, L.nwg2, L.step, kOB, h->sn.p, h->store.p, h->scratch.p, h->info.p,
+                              h->growth.p, piv_tol);
+    case K_LASWP:
+      return launch_laswp(st, h->ftiles.p + L.off, (int)L.cnt, h->sn.p, h->store.p, h->scratch.p, h->swaps.p,
+                          kSwapStride);
     case K_PANEL:
-      return launch_panel(st, (int)L.cnt, (int)L.aux, L.step, h->ilist.p + L.off, h->sn.p,
+      return launch_panel1(st, (int)L.cnt, (int)L.aux, (int)(L.nwg & 0xffff), (int)(L.nwg >> 16), L.step,
+                           (int)L.aux2, h->ilist.p + L.off, h->sn.p,
                           h->store.p, h->scratch.p, h->rowperm.p, h->swaps.p, kSwapStride, h->info.p,
                           h->growth.p, diag_tol);
     case K_TRSMU:
-      return launch_laswp_trsm_u(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p, h->store.p,
-                                 h->scratch.p, h->swaps.p, kSwapStride);
+      return launch_trsm_u(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, kOB, (int)L.aux, h->sn.p,
+                           h->store.p, h->scratch.p, h->swaps.p, kSwapStride);
     case K_TRSML:
       return launch_trsm_l(st, L.nwg, (int)L.aux, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p,
                            h->store.p, h->scratch.p, h->info.p, h->growth.p, piv_tol);
     case K_GEMM:
+    case K_GEMM22:
       return launch_gemm(st, L.nwg, h->gtasks.p + L.off, (int)L.cnt, (int)L.aux);
   }
   return hipErrorInvalidValue;
 }
 
-static int run_factor(smlu_handle* h) {
+// All device work of one numeric refactorization, in stream order (captured into a graph).
+static int enqueue_factor(smlu_handle* h, Timer& tm, bool dbg) {
   Plan& P = h->plan;
   hipStream_t st = h->stream;
-  HIPCHK(hipSetDevice(h->device));
-  auto t0 = std::chrono::steady_clock::now();
-  for (auto& v : h->kind_ms) v = 0;
-  Timer tm(h);
   HIPCHK(hipMemsetAsync(h->info.p, 0, sizeof(int32_t) * std::max<int64_t>(P.nsup, 1), st));
   HIPCHK(hipMemsetAsync(h->growth.p, 0, sizeof(double), st));
   // identity (local) row permutation; fronts overwrite their part
@@ -681,7 +825,6 @@ static int run_factor(smlu_handle* h) {
   // A given (p, q) order means "no pivoting on top": only a zero diagonal moves.
   double diag_tol = P.given_order ? 0.0 : h->opts.diag_pivot_tol;
   double piv_tol = h->opts.pivot_tol;
-  static const bool dbg = std::getenv("SMLU_DEBUG_SYNC") != nullptr;
   for (const Launch& L : h->fac) {
     hipEvent_t stop;
     HIPCHK(tm.begin(L.kind, &stop));
@@ -695,6 +838,47 @@ static int run_factor(smlu_handle* h) {
       return fail(h, SMLU_ERR_HIP, buf);
     }
     HIPCHK(tm.end(stop));
+  }
+  return SMLU_OK;
+}
+
+static int run_factor(smlu_handle* h) {
+  Plan& P = h->plan;
+  hipStream_t st = h->stream;
+  HIPCHK(hipSetDevice(h->device));
+  auto t0 = std::chrono::steady_clock::now();
+  for (auto& v : h->kind_ms) v = 0;
+  Timer tm(h);
+  static const bool dbg = std::getenv("SMLU_DEBUG_SYNC") != nullptr;
+  static const bool nograph = std::getenv("SMLU_NO_GRAPH") != nullptr;
+  const int prof = h->opts.profile ? 1 : 0;
+  bool use_graph = !dbg && !nograph && !h->graph_failed && h->have_numeric;  // first run eager
+  if (use_graph && (!h->fac_exec || h->fac_exec_profile != prof)) {
+    if (h->fac_exec) (void)hipGraphExecDestroy(h->fac_exec);
+    h->fac_exec = nullptr;
+    hipGraph_t g = nullptr;
+    HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+    int rc = enqueue_factor(h, tm, false);
+    hipError_t ec = hipStreamEndCapture(st, &g);
+    if (rc == SMLU_OK && ec == hipSuccess && g) ec = hipGraphInstantiate(&h->fac_exec, g, nullptr, nullptr, 0);
+    if (g) (void)hipGraphDestroy(g);
+    if (rc != SMLU_OK || ec != hipSuccess || !h->fac_exec) {
+      (void)hipGetLastError();
+      h->graph_failed = true;   // fall back to eager launches
+      h->fac_exec = nullptr;
+      use_graph = false;
+      tm.used = 0;
+    } else {
+      h->fac_exec_profile = prof;
+      h->fac_graph_events = tm.used;
+    }
+  }
+  if (use_graph) {
+    tm.used = h->fac_graph_events;
+    HIPCHK(hipGraphLaunch(h->fac_exec, st));
+  } else {
+    int rc = enqueue_factor(h, tm, dbg);
+    if (rc != SMLU_OK) return rc;
   }
   HIPCHK(hipMemcpyAsync(h->hinfo, h->info.p, sizeof(int32_t) * P.nsup, hipMemcpyDeviceToHost, st));
   double g = 0;
@@ -827,6 +1011,7 @@ void smlu_default_opts(smlu_opts* o) {
   o->device = 0;
   o->profile = 0;
   o->leaf_size = 64;
+  o->use_mfma = std::getenv("SMLU_MFMA") ? 1 : 0;
 }
 
 int smlu_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
@@ -1119,6 +1304,7 @@ double smlu_stat(const smlu_handle* h, const char* key) {
   if (k == "growth_max") return h->growth_max;
   if (k == "weak") return (double)h->weak;
   if (k == "gemm_flops") return h->gemm_flops;
+  if (k == "gemm22_flops") return h->gemm22_flops;
   if (k.rfind("ms_", 0) == 0) {
     std::string name = k.substr(3);
     double t = 0;

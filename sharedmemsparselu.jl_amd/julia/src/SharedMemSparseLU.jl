@@ -12,10 +12,10 @@ const libsmlu = get(ENV, "SMLU_LIB", joinpath(@__DIR__, "..", "deps", "libsmlu.s
 mutable struct SmluOpts
     chunk_size::Int64; index_base::Int32; ordering::Int32; grid::NTuple{3,Int64}
     scale::Int32; relax::Int32; pivot_tol::Float64; diag_pivot_tol::Float64
-    device::Int32; profile::Int32; leaf_size::Int64
+    device::Int32; profile::Int32; leaf_size::Int64; use_mfma::Int32; reserved::Int32
 end
 function default_opts()
-    o = SmluOpts(0, 0, 0, (0, 0, 0), 0, 0, 0.0, 0.0, 0, 0, 0)
+    o = SmluOpts(0, 0, 0, (0, 0, 0), 0, 0, 0.0, 0.0, 0, 0, 0, 0, 0)
     ccall((:smlu_default_opts, libsmlu), Cvoid, (Ref{SmluOpts},), o)
     return o                                   # index_base = 1: Julia's 1-based CSC as is
 end

@@ -46,6 +46,8 @@ class SmluOpts(ctypes.Structure):
         ("device", i32),
         ("profile", i32),
         ("leaf_size", i64),
+        ("use_mfma", i32),
+        ("reserved", i32),
     ]
 
 

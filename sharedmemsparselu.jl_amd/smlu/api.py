@@ -64,7 +64,7 @@ class ParallelSparseLU:
 
     def __init__(self, A, chunk_size=None, *, ordering="auto", grid=None, device=0,
                  profile=False, p=None, q=None, Rs=None, pivot_tol=None, diag_pivot_tol=None,
-                 leaf_size=None, relax=True):
+                 leaf_size=None, relax=True, use_mfma=None):
         A = _csc(A)
         m, n = A.shape
         if m != n:
@@ -86,6 +86,8 @@ class ParallelSparseLU:
             kw["diag_pivot_tol"] = float(diag_pivot_tol)
         if leaf_size is not None:
             kw["leaf_size"] = int(leaf_size)
+        if use_mfma is not None:
+            kw["use_mfma"] = 1 if use_mfma else 0
         self._opts = C.default_opts(**kw)
         self.m, self.n = m, n
         self.chunk_size = chunk_size

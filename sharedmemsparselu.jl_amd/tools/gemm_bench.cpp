@@ -24,13 +24,14 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&A, hA.size() * 8)); CK(hipMalloc(&B, hB.size() * 8)); CK(hipMalloc(&C1, hC.size() * 8)); CK(hipMalloc(&C2, hC.size() * 8));
     CK(hipMemcpy(A, hA.data(), hA.size() * 8, hipMemcpyHostToDevice)); CK(hipMemcpy(B, hB.data(), hB.size() * 8, hipMemcpyHostToDevice));
     CK(hipMalloc(&dt, sizeof(GemmTask)));
-    double res[2] = {0, 0};
-    for (int variant = 0; variant < 2; ++variant) {
-      int tile = variant == 0 ? 64 : 128;
+    double res[3] = {0, 0, 0};
+    for (int variant = 0; variant < 3; ++variant) {
+      int tile = variant == 0 ? 64 : (variant == 1 ? 128 : 129);
       double* C = variant == 0 ? C1 : C2;
       GemmTask t{}; t.A = A; t.B = B; t.C = C; t.m = m; t.n = n; t.k = k; t.lda = lda; t.ldb = ldb; t.ldc = ldc;
-      t.tiles_m = (m + tile - 1) / tile; t.tile0 = 0;
-      int64_t tiles = (int64_t)t.tiles_m * ((n + tile - 1) / tile);
+      const int ts = tile == 129 ? 128 : tile;
+      t.tiles_m = (m + ts - 1) / ts; t.tile0 = 0;
+      int64_t tiles = (int64_t)t.tiles_m * ((n + ts - 1) / ts);
       CK(hipMemcpy(dt, &t, sizeof t, hipMemcpyHostToDevice));
       CK(hipMemcpy(C, hC.data(), hC.size() * 8, hipMemcpyHostToDevice));
       CK(launch_gemm(st, tiles, dt, 1, tile));   // one correctness pass
@@ -42,13 +43,14 @@ int main(int argc, char** argv) {
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       res[variant] = 2.0 * m * n * (double)k * reps / (ms * 1e-3) / 1e12;
     }
-    // compare after 1 + reps identical updates each: rerun exactly once from the same C for both
+    // compare 64-tile VALU (C1) against MFMA (C2) after one update from the same C
     for (int variant = 0; variant < 2; ++variant) {
-      int tile = variant == 0 ? 64 : 128;
+      int tile = variant == 0 ? 64 : 129;
       double* C = variant == 0 ? C1 : C2;
       GemmTask t{}; t.A = A; t.B = B; t.C = C; t.m = m; t.n = n; t.k = k; t.lda = lda; t.ldb = ldb; t.ldc = ldc;
-      t.tiles_m = (m + tile - 1) / tile; t.tile0 = 0;
-      int64_t tiles = (int64_t)t.tiles_m * ((n + tile - 1) / tile);
+      const int ts = tile == 129 ? 128 : tile;
+      t.tiles_m = (m + ts - 1) / ts; t.tile0 = 0;
+      int64_t tiles = (int64_t)t.tiles_m * ((n + ts - 1) / ts);
       CK(hipMemcpy(dt, &t, sizeof t, hipMemcpyHostToDevice));
       CK(hipMemcpy(C, hC.data(), hC.size() * 8, hipMemcpyHostToDevice));
       CK(launch_gemm(st, tiles, dt, 1, tile));
@@ -60,7 +62,7 @@ int main(int argc, char** argv) {
     for (int j = 0; j < n; ++j) for (int i = 0; i < m; ++i) { size_t o = (size_t)j * ldc + i; md = fmax(md, fabs(r1[o] - r2[o])); mx = fmax(mx, fabs(r1[o])); }
     bool pad_ok = true;  // rows >= m inside ld padding untouched
     for (int j = 0; j < n && pad_ok; ++j) for (int i = m; i < ldc; ++i) { size_t o = (size_t)j * ldc + i; if (r2[o] != hC[o]) pad_ok = false; }
-    printf("m=%6d n=%6d k=%6d  tile64 %6.2f TF  tile128 %6.2f TF  maxdiff %.2e (rel %.2e) pad_ok %d\n", m, n, k, res[0], res[1], md, md / mx, pad_ok);
+    printf("m=%6d n=%6d k=%6d  valu64 %6.2f TF  valu128 %6.2f TF  mfma128 %6.2f TF  maxdiff(valu,mfma) %.2e (rel %.2e) pad_ok %d\n", m, n, k, res[0], res[1], res[2], md, md / mx, pad_ok);
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C1)); CK(hipFree(C2)); CK(hipFree(dt));
   }
   return 0;
