@@ -132,7 +132,7 @@ def main():
         vals.append(v)
     torch.cuda.synchronize()
 
-    kinds = ["gemm", "gemm22", "panel", "trsm", "small", "assemble", "memset"]
+    kinds = ["gemm", "gemmu", "gemmo", "gemm22", "panel", "trsm", "small", "assemble", "memset"]
     kind_ms = {k: 0.0 for k in kinds}
 
     def step(r):
@@ -160,7 +160,7 @@ def main():
     if rank == 0:
         K = args.steps
         gemm_flops = F.stat("gemm_flops")
-        ms_gemm = (kind_ms["gemm"] + kind_ms["gemm22"]) / K
+        ms_gemm = (kind_ms["gemm"] + kind_ms["gemmu"] + kind_ms["gemmo"] + kind_ms["gemm22"]) / K
         upd = F.stat("upd")
         dense_flops = F.stat("dense_flops")
         achieved = gemm_flops / (ms_gemm * 1e-3) / 1e12 if ms_gemm > 0 else None
@@ -192,7 +192,7 @@ def main():
                          "note": "fp64 dense peak (vector == matrix on gfx950); achieved = gemm "
                                  "flops per refactor / summed k_gemm event time per refactor"},
             "kernel_ms_per_step": {k: v / K for k, v in kind_ms.items()},
-            "gemm_split": {"panel_tflops": (gemm_flops - F.stat("gemm22_flops")) / max(kind_ms["gemm"] / K, 1e-9) / 1e9,
+            "gemm_split": {"panel_tflops": (gemm_flops - F.stat("gemm22_flops")) / max((kind_ms["gemm"] + kind_ms["gemmu"] + kind_ms["gemmo"]) / K, 1e-9) / 1e9,
                            "f22_tflops": F.stat("gemm22_flops") / max(kind_ms["gemm22"] / K, 1e-9) / 1e9,
                            "panel_gflop": (gemm_flops - F.stat("gemm22_flops")) / 1e9,
                            "f22_gflop": F.stat("gemm22_flops") / 1e9},

@@ -42,4 +42,13 @@ struct FrontTile {
   int64_t wg0;
 };
 
+// Row swaps of one or more consecutive panels (sub-panels kb0 + u*nb, swap-list slots slot0 + u,
+// u < nsub) applied in order to the front columns [a, b) minus [c_lo, c_hi); 64 columns per
+// workgroup, workgroups numbered from wg0 within one launch (tasks sorted by wg0).
+struct SwapTask {
+  int32_t s, kb0, nsub, slot0;
+  int32_t a, b, c_lo, c_hi;
+  int64_t wg0;
+};
+
 }  // namespace smlu

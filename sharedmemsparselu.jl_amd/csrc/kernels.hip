@@ -6,15 +6,17 @@
 //   k_rowscale            UMFPACK SUM scaling behind lu(A) (src/SharedMemSparseLU.jl:74, Rs at :51)
 //   k_scatterA            gather A's values into fronts (the "active columns")
 //   k_extend_add          scatter of Schur-complement updates into ancestor fronts
-//   k_front_lds, k_panel, pivot search + pivot scaling + rank-1 Schur updates: the
-//   k_laswp_trsm_u,       numeric column-elimination loop of lu(A)/lu!(F,A) (:74, :247)
-//   k_trsm_l, k_gemm
-//   k_fwd_front           lsolve! (:349-367): trsv on the diagonal block + gemv below
-//   k_bwd_front           rsolve! (:374-392)
-//   k_perm_in/k_perm_out  ldiv!'s scale+permute / un-permute (:318-339)
+//   k_front_lds           whole small fronts in LDS: pivot search, pivot scaling, rank-1 updates
+//   k_panel_reg, k_laswp, the same column-elimination loop of lu(A)/lu!(F,A) (:74, :247) for
+//   k_step_trsm, k_trsm_u, large fronts, blocked: panel, row swaps, triangular solves and
+//   k_gemm*               Schur-complement (trailing) updates
+//   k_fwd_front, k_tri_block, k_fwd_gather   lsolve! (:349-367)
+//   k_bwd_front, k_bwd_u12                    rsolve! (:374-392)
+//   k_perm_in/k_perm_out/k_unswap             ldiv!'s scale+permute / un-permute (:318-339)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "device.hpp"
 
@@ -44,6 +46,15 @@ __device__ __forceinline__ double recip(double x) {
   return fma(r, e2, r);
 }
 
+// Global-address-space views of plain pointers: loads through them compile to global_load
+// (vmcnt only) instead of flat_load, which also counts against lgkmcnt and so makes every LDS
+// wait inside a loop wait for the global prefetch as well.
+typedef __attribute__((address_space(1))) double gdbl;
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gbl(T* p) {
+  return (__attribute__((address_space(1))) T*)p;
+}
+
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
@@ -63,9 +74,9 @@ __device__ __forceinline__ void publish_info(int32_t* info, int flag, int errcol
 }
 
 struct FrontPtrs {
-  double* L;
-  double* U;
-  double* F;
+  gdbl* L;
+  gdbl* U;
+  gdbl* F;
   int64_t M, ns, nu;
 };
 
@@ -74,13 +85,13 @@ __device__ __forceinline__ FrontPtrs front_ptrs(const SNode& s, double* store, d
   f.ns = s.ns;
   f.nu = s.nu;
   f.M = (int64_t)s.ns + s.nu;
-  f.L = store + s.Loff;
-  f.U = store + s.Uoff;
-  f.F = s.Foff >= 0 ? scratch + s.Foff : nullptr;
+  f.L = gbl(store + s.Loff);
+  f.U = gbl(store + s.Uoff);
+  f.F = s.Foff >= 0 ? gbl(scratch + s.Foff) : nullptr;
   return f;
 }
 
-__device__ __forceinline__ double* fel(const FrontPtrs& f, int64_t i, int64_t j) {
+__device__ __forceinline__ gdbl* fel(const FrontPtrs& f, int64_t i, int64_t j) {
   if (j < f.ns) return f.L + j * f.M + i;
   if (i < f.ns) return f.U + (j - f.ns) * f.ns + i;
   return f.F + (j - f.ns) * f.nu + (i - f.ns);
@@ -142,11 +153,11 @@ __global__ void k_extend_add(int64_t ntasks, const int2* __restrict__ tasks,
   const int32_t* rm = relmap + c.rowptr;
   const int64_t tj = rm[tk.y];
   if (tj < P.ns) {
-    double* col = P.L + tj * P.M;
+    gdbl* col = P.L + tj * P.M;
     for (int64_t i = lane; i < nuc; i += 64) col[rm[i]] += src[i];
   } else {
-    double* colU = P.U + (tj - P.ns) * P.ns;
-    double* colF = P.F + (tj - P.ns) * P.nu - P.ns;
+    gdbl* colU = P.U + (tj - P.ns) * P.ns;
+    gdbl* colF = P.F + (tj - P.ns) * P.nu - P.ns;
     for (int64_t i = lane; i < nuc; i += 64) {
       int64_t ti = rm[i];
       if (ti < P.ns) colU[ti] += src[i];
@@ -258,252 +269,7 @@ __global__ __launch_bounds__(256) void k_front_lds(const int32_t* __restrict__ l
   if (tid == 0 && s_flag) publish_info(info + sid, s_flag, s_err);
 }
 
-// ------------------------------------------------------------------------------------
-// Blocked path, step 1: panel factorization.  One workgroup per front.  Candidate rows:
-// [kb, ns) (mode 1, full) or [kb, kb+w) (mode 2, diagonal tile).  The candidate block
-// (R x w) is factored in LDS; rows are permuted in place and the composed permutation is
-// recorded for the row swaps of the other columns (k_laswp_trsm_u).
-// ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_panel(const int32_t* __restrict__ list, int step, int slot0,
-                                               const SNode* __restrict__ sn,
-                                               double* __restrict__ store,
-                                               double* __restrict__ scratch,
-                                               int32_t* __restrict__ rowperm,
-                                               int32_t* __restrict__ swaps,  // per front: [cnt, (dst,src)*]
-                                               int64_t swap_stride, int32_t* __restrict__ info,
-                                               double* __restrict__ growth, double diag_tol) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  __shared__ int s_lp[512];
-  __shared__ int s_piv;
-  __shared__ int s_flag;
-  __shared__ int s_err;
-  const int sid = list[blockIdx.x];
-  const SNode s = sn[sid];
-  FrontPtrs f = front_ptrs(s, store, scratch);
-  const int64_t M = f.M;
-  const int ns = (int)f.ns;
-  const int kb = step * s.nb;
-  const int w = min(s.nb, ns - kb);
-  const int R = (s.mode == 1) ? ns - kb : w;
-  const int ld = R | 1;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  double* P = f.L + (int64_t)kb * M + kb;  // panel origin, ld M
-  for (int j = wv; j < w; j += 4)
-    for (int i = lane; i < R; i += 64) lds[j * ld + i] = P[(int64_t)j * M + i];
-  for (int i = tid; i < R; i += 256) s_lp[i] = i;
-  if (tid == 0) { s_flag = 0; s_err = -1; }
-  __syncthreads();
-  for (int k = 0; k < w; ++k) {
-    if (wv == 0) {
-      double am = -1.0;
-      int ai = k;
-      for (int i = k + lane; i < R; i += 64) {
-        double v = fabs(lds[k * ld + i]);
-        if (v > am) { am = v; ai = i; }
-      }
-      am = wave_max_idx(am, ai);
-      if (lane == 0) {
-        int piv = choose_pivot(lds[k * ld + k], am, ai, k, diag_tol);
-        if (am <= 0.0) {
-          s_flag |= 1;
-          if (s_err < 0) s_err = kb + k;
-        } else {
-          atomic_max_pos(&growth[0], am / fabs(lds[k * ld + piv]));
-        }
-        s_piv = piv;
-      }
-    }
-    __syncthreads();
-    const int piv = s_piv;
-    if (piv != k) {
-      for (int j = tid; j < w; j += 256) {
-        double t = lds[j * ld + k];
-        lds[j * ld + k] = lds[j * ld + piv];
-        lds[j * ld + piv] = t;
-      }
-      if (tid == 0) {
-        int t = s_lp[k];
-        s_lp[k] = s_lp[piv];
-        s_lp[piv] = t;
-      }
-      __syncthreads();
-    }
-    const double pv = lds[k * ld + k];
-    for (int i = k + 1 + tid; i < R; i += 256) lds[k * ld + i] = lds[k * ld + i] / pv;
-    __syncthreads();
-    for (int j = k + 1 + wv; j < w; j += 4) {
-      const double u = lds[j * ld + k];
-      if (u != 0.0)
-        for (int i = k + 1 + lane; i < R; i += 64)
-          lds[j * ld + i] = fma(-lds[k * ld + i], u, lds[j * ld + i]);
-    }
-    __syncthreads();
-  }
-  for (int j = wv; j < w; j += 4)
-    for (int i = lane; i < R; i += 64) P[(int64_t)j * M + i] = lds[j * ld + i];
-  // compose the row permutation of positions [kb, kb+R) and publish the moved rows
-  int32_t* rp = rowperm + s.first + kb;
-  int* old = reinterpret_cast<int*>(lds);  // reuse LDS (panel already stored)
-  __syncthreads();
-  for (int i = tid; i < R; i += 256) old[i] = rp[i];
-  __syncthreads();
-  for (int i = tid; i < R; i += 256) rp[i] = old[s_lp[i]];
-  int32_t* sw = swaps + (int64_t)(slot0 + blockIdx.x) * swap_stride;
-  if (tid == 0) {
-    int cnt = 0;
-    for (int i = 0; i < R; ++i)
-      if (s_lp[i] != i) {
-        sw[1 + 2 * cnt] = i;
-        sw[2 + 2 * cnt] = s_lp[i];
-        ++cnt;
-      }
-    sw[0] = cnt;
-    if (s_flag) publish_info(info + sid, s_flag, s_err);
-  }
-}
 
-// ------------------------------------------------------------------------------------
-// Panel factorization, one wavefront per front (no block barriers): the R x w candidate block
-// lives in LDS (column-major, ld = R|1); lane l owns rows l, l+64, ...  Per column: wave
-// argmax (shuffles), diagonal-preference choice, in-LDS row swap (lanes over columns), pivot
-// scaling and the rank-1 update of the lane's own rows (the pivot row is an LDS broadcast).
-// ------------------------------------------------------------------------------------
-template <int RPL>
-__global__ __launch_bounds__(64) void k_panel1(const int32_t* __restrict__ list, int step, int slot0,
-                                               const SNode* __restrict__ sn,
-                                               double* __restrict__ store,
-                                               double* __restrict__ scratch,
-                                               int32_t* __restrict__ rowperm,
-                                               int32_t* __restrict__ swaps,
-                                               int64_t swap_stride, int32_t* __restrict__ info,
-                                               double* __restrict__ growth, double diag_tol) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  __shared__ int s_lp[512];
-  const int sid = list[blockIdx.x];
-  const SNode s = sn[sid];
-  FrontPtrs f = front_ptrs(s, store, scratch);
-  const int64_t M = f.M;
-  const int ns = (int)f.ns;
-  const int kb = step * s.nb;
-  const int w = min(s.nb, ns - kb);
-  const int R = (s.mode == 1) ? ns - kb : w;
-  const int ld = R | 1;
-  const int lane = threadIdx.x;
-  double* P = f.L + (int64_t)kb * M + kb;
-  for (int j = 0; j < w; ++j)
-#pragma unroll
-    for (int r = 0; r < RPL; ++r) {
-      const int i = lane + 64 * r;
-      if (i < R) lds[j * ld + i] = P[(int64_t)j * M + i];
-    }
-  for (int i = lane; i < R; i += 64) s_lp[i] = i;
-  int flag = 0, err = -1;
-  double gmax = 0.0;
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-  for (int k = 0; k < w; ++k) {
-    double am = -1.0;
-    int ai = k;
-#pragma unroll
-    for (int r = 0; r < RPL; ++r) {
-      const int i = lane + 64 * r;
-      if (i >= k && i < R) {
-        const double v = fabs(lds[k * ld + i]);
-        if (v > am) { am = v; ai = i; }
-      }
-    }
-    am = wave_max_idx(am, ai);
-    const double akk = lds[k * ld + k];
-    const int piv = choose_pivot(akk, am, ai, k, diag_tol);
-    if (am <= 0.0) {
-      flag |= 1;
-      if (err < 0) err = kb + k;
-    }
-    if (piv != k) {
-      __builtin_amdgcn_wave_barrier();
-      for (int j = lane; j < w; j += 64) {
-        const double t = lds[j * ld + k];
-        lds[j * ld + k] = lds[j * ld + piv];
-        lds[j * ld + piv] = t;
-      }
-      if (lane == 0) {
-        const int t = s_lp[k];
-        s_lp[k] = s_lp[piv];
-        s_lp[piv] = t;
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-    const double pv = lds[k * ld + k];
-    if (am > 0.0) gmax = fmax(gmax, am / fabs(pv));
-    double l[RPL];
-#pragma unroll
-    for (int r = 0; r < RPL; ++r) {
-      const int i = lane + 64 * r;
-      l[r] = 0.0;
-      if (i > k && i < R) {
-        l[r] = lds[k * ld + i] / pv;
-        lds[k * ld + i] = l[r];
-      }
-    }
-    // rank-1 update of the lane's rows; columns unrolled by 4 for independent LDS loads
-    int j = k + 1;
-    for (; j + 4 <= w; j += 4) {
-      double u[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) u[q] = lds[(j + q) * ld + k];
-#pragma unroll
-      for (int r = 0; r < RPL; ++r) {
-        const int i = lane + 64 * r;
-        if (i > k && i < R) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) lds[(j + q) * ld + i] = fma(-l[r], u[q], lds[(j + q) * ld + i]);
-        }
-      }
-    }
-    for (; j < w; ++j) {
-      const double u = lds[j * ld + k];
-#pragma unroll
-      for (int r = 0; r < RPL; ++r) {
-        const int i = lane + 64 * r;
-        if (i > k && i < R) lds[j * ld + i] = fma(-l[r], u, lds[j * ld + i]);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  for (int j = 0; j < w; ++j)
-#pragma unroll
-    for (int r = 0; r < RPL; ++r) {
-      const int i = lane + 64 * r;
-      if (i < R) P[(int64_t)j * M + i] = lds[j * ld + i];
-    }
-  // compose the row permutation of positions [kb, kb+R) and publish the moved rows
-  int32_t* rp = rowperm + s.first + kb;
-  int* old = reinterpret_cast<int*>(lds);
-  __builtin_amdgcn_wave_barrier();
-  for (int i = lane; i < R; i += 64) old[i] = rp[i];
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-  for (int i = lane; i < R; i += 64) rp[i] = old[s_lp[i]];
-  int32_t* sw = swaps + (int64_t)(slot0 + blockIdx.x) * swap_stride;
-  int cnt = 0;
-  for (int base = 0; base < R; base += 64) {
-    const int i = base + lane;
-    const bool mv = i < R && s_lp[i] != i;
-    const unsigned long long m = __ballot(mv);
-    if (mv) {
-      const int pos = cnt + __popcll(m & ((1ull << lane) - 1ull));
-      sw[1 + 2 * pos] = i;
-      sw[2 + 2 * pos] = s_lp[i];
-    }
-    cnt += __popcll(m);
-  }
-  if (lane == 0) sw[0] = cnt;
-  gmax = wave_max(gmax);
-  if (lane == 0) {
-    if (gmax > 0.0) atomic_max_pos(&growth[0], gmax);
-    if (flag) publish_info(info + sid, flag, err);
-  }
-}
 
 // ------------------------------------------------------------------------------------
 // Panel factorization with the candidate rows in REGISTERS: thread t owns candidate row t
@@ -515,7 +281,7 @@ __global__ __launch_bounds__(64) void k_panel1(const int32_t* __restrict__ list,
 // ------------------------------------------------------------------------------------
 template <int W, int NW>
 __global__ __launch_bounds__(64 * NW) void k_panel_reg(const int32_t* __restrict__ list, int step,
-                                                       int slot0, const SNode* __restrict__ sn,
+                                                       const SNode* __restrict__ sn,
                                                        double* __restrict__ store,
                                                        double* __restrict__ scratch,
                                                        int32_t* __restrict__ rowperm,
@@ -531,7 +297,7 @@ __global__ __launch_bounds__(64 * NW) void k_panel_reg(const int32_t* __restrict
   __shared__ int s_idx[NW];
   __shared__ int s_any[NW];
   __shared__ int s_piv;
-  const int sid = list[blockIdx.x];
+  const int sid = list[2 * blockIdx.x];       // (front, swap slot) pairs
   const SNode s = sn[sid];
   FrontPtrs f = front_ptrs(s, store, scratch);
   const int64_t M = f.M;
@@ -541,7 +307,7 @@ __global__ __launch_bounds__(64 * NW) void k_panel_reg(const int32_t* __restrict
   const int R = (s.mode == 1) ? ns - kb : w;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const bool has = tid < R;
-  double* P = f.L + (int64_t)kb * M + kb;
+  gdbl* P = f.L + (int64_t)kb * M + kb;
   double rA[32], rB[32];   // columns [0,32) and [32,64) of my candidate row
 #pragma unroll
   for (int j = 0; j < 32; ++j) {
@@ -624,12 +390,23 @@ __global__ __launch_bounds__(64 * NW) void k_panel_reg(const int32_t* __restrict
       cur[kk] = l;
       lmax = fmax(lmax, fabs(l));
       if (l != 0.0) {
+        // pivot-row reads batched ahead of their FMAs (one LDS latency per half-row)
+        double pr[32];
 #pragma unroll
         for (int j = 0; j < 32; ++j)
-          if (j > kk) cur[j] = fma(-l, s_prow[kabs - kk + j], cur[j]);
+          if (j > kk) pr[j] = s_prow[kabs - kk + j];
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+          if (j > kk) cur[j] = fma(-l, pr[j], cur[j]);
+        __builtin_amdgcn_sched_barrier(0);
         if (restb) {
 #pragma unroll
-          for (int j = 0; j < 32; ++j) rest[j] = fma(-l, s_prow[32 + j], rest[j]);
+          for (int j = 0; j < 32; ++j) pr[j] = s_prow[32 + j];
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int j = 0; j < 32; ++j) rest[j] = fma(-l, pr[j], rest[j]);
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
     }
@@ -664,7 +441,7 @@ __global__ __launch_bounds__(64 * NW) void k_panel_reg(const int32_t* __restrict
   if (has) s_old[tid] = rp[tid];
   __syncthreads();
   if (has) rp[pos] = s_old[tid];
-  int32_t* sw = swaps + (int64_t)(slot0 + blockIdx.x) * swap_stride;
+  int32_t* sw = swaps + (int64_t)list[2 * blockIdx.x + 1] * swap_stride;
   const bool mv = has && pos != tid;
   const unsigned long long m = __ballot(mv);
   if (lane == 0) s_any[wv] = __popcll(m);
@@ -692,39 +469,177 @@ __global__ __launch_bounds__(64 * NW) void k_panel_reg(const int32_t* __restrict
   }
 }
 
-// Row swaps of the panel at kb applied to every column outside the panel (all fronts of the
-// step, grid-stride; a front without swaps costs one load).  Runs before the TRSM kernels.
-__global__ __launch_bounds__(256) void k_laswp(const FrontTile* __restrict__ ft, int nft,
+// Single-wave variant of k_panel_reg (R <= 64 candidate rows): the same pivot choices and the
+// same arithmetic, with every broadcast done by v_readlane from the owning lane instead of
+// through LDS -- no LDS traffic and no barriers on the per-column chain.  who (position ->
+// thread) is kept one entry per lane.
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+template <int W>
+__global__ __launch_bounds__(64) void k_panel_wave(const int32_t* __restrict__ list, int step,
+                                                   const SNode* __restrict__ sn,
+                                                   double* __restrict__ store,
+                                                   double* __restrict__ scratch,
+                                                   int32_t* __restrict__ rowperm,
+                                                   int32_t* __restrict__ swaps,
+                                                   int64_t swap_stride,
+                                                   int32_t* __restrict__ info,
+                                                   double* __restrict__ growth, double diag_tol) {
+  static_assert(W == 32 || W == 64, "panel width");
+  const int sid = list[2 * blockIdx.x];
+  const SNode s = sn[sid];
+  FrontPtrs f = front_ptrs(s, store, scratch);
+  const int64_t M = f.M;
+  const int ns = (int)f.ns;
+  const int kb = step * s.nb;
+  const int w = min(s.nb, ns - kb);
+  const int R = (s.mode == 1) ? ns - kb : w;
+  const int lane = threadIdx.x;
+  const bool has = lane < R;
+  gdbl* P = f.L + (int64_t)kb * M + kb;
+  double rA[32], rB[32];
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    rA[j] = (has && j < w) ? P[(int64_t)j * M + lane] : 0.0;
+    rB[j] = (W == 64 && has && j + 32 < w) ? P[(int64_t)(j + 32) * M + lane] : 0.0;
+  }
+  int pos = lane, who = lane;
+  int flag = 0, err = -1;
+  double lmax = 0.0;
+  auto column = [&](double (&cur)[32], double (&rest)[32], const int kk, const int kabs,
+                    const bool restb) {
+    const int q = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(who, kabs));
+    const bool cand = has && pos >= kabs;
+    const double akk = readlane_f64(cur[kk], q);
+    const bool beats = cand && pos != kabs && fabs(cur[kk]) * diag_tol > fabs(akk);
+    int p = q;
+    if (__ballot(beats) != 0ull || akk == 0.0) {   // full argmax (rare under dominance)
+      double am = cand ? fabs(cur[kk]) : -1.0;
+      int ai = cand ? pos : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const double ov = __shfl_xor(am, o, 64);
+        const int oi = __shfl_xor(ai, o, 64);
+        if (ov > am || (ov == am && oi < ai)) { am = ov; ai = oi; }
+      }
+      if (am <= 0.0) {
+        flag |= 1;
+        if (err < 0) err = kb + kabs;
+      } else {
+        p = __builtin_amdgcn_readlane(who, __builtin_amdgcn_readfirstlane(ai));
+      }
+      p = __builtin_amdgcn_readfirstlane(p);
+    }
+    const double pinv = recip(readlane_f64(cur[kk], p));
+    if (cand && lane != p) {
+      const double l = cur[kk] * pinv;
+      cur[kk] = l;
+      lmax = fmax(lmax, fabs(l));
+      if (l != 0.0) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+          if (j > kk) cur[j] = fma(-l, readlane_f64(cur[j], p), cur[j]);
+        if (restb) {
+#pragma unroll
+          for (int j = 0; j < 32; ++j) rest[j] = fma(-l, readlane_f64(rest[j], p), rest[j]);
+        }
+      }
+    }
+    if (p != q) {               // transposition of positions kabs and ppos
+      const int ppos = __builtin_amdgcn_readlane(pos, p);
+      if (lane == p) pos = kabs;
+      else if (lane == q) pos = ppos;
+      if (lane == kabs) who = p;
+      else if (lane == ppos) who = q;
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < 32; ++k)
+    if (k < w) column(rA, rB, k, k, W == 64 && w > 32);
+  if (W == 64) {
+#pragma unroll
+    for (int k = 0; k < 32; ++k)
+      if (k + 32 < w) column(rB, rA, k, k + 32, false);
+  }
+  if (has) {
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      if (j < w) P[(int64_t)j * M + pos] = rA[j];
+      if (W == 64 && j + 32 < w) P[(int64_t)(j + 32) * M + pos] = rB[j];
+    }
+  }
+  int32_t* rp = rowperm + s.first + kb;
+  const int old = has ? rp[lane] : 0;
+  if (has) rp[pos] = old;
+  int32_t* sw = swaps + (int64_t)list[2 * blockIdx.x + 1] * swap_stride;
+  const bool mv = has && pos != lane;
+  const unsigned long long m = __ballot(mv);
+  if (mv) {
+    const int o = __popcll(m & ((1ull << lane) - 1ull));
+    sw[1 + 2 * o] = pos;
+    sw[2 + 2 * o] = lane;
+  }
+  if (lane == 0) sw[0] = __popcll(m);
+  lmax = wave_max(lmax);
+  if (lane == 0) {
+    if (lmax > 0.0) atomic_max_pos(&growth[0], lmax);
+    if (flag) publish_info(info + sid, flag, err);
+  }
+}
+
+// Row swaps (LAPACK laswp) of the panels of a SwapTask on its column set; one workgroup per 64
+// columns.  Within a workgroup the panels' swap lists are applied in order.  A list moves at
+// most 64 rows (mode 1 panels are 32 wide, mode 2 pivots inside the 64-row diagonal tile);
+// a panel without swaps costs one load.
+__device__ __forceinline__ int find_swap_task(const SwapTask* __restrict__ t, int cnt, int64_t b) {
+  int lo = 0, hi = cnt - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (t[mid].wg0 <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_laswp(const SwapTask* __restrict__ tasks, int ntask,
                                                const SNode* __restrict__ sn,
                                                double* __restrict__ store,
                                                double* __restrict__ scratch,
                                                const int32_t* __restrict__ swaps, int64_t swap_stride) {
   __shared__ double buf[64 * 65];   // [column][moved row]
-  for (int fi = blockIdx.x; fi < nft; fi += gridDim.x) {
-    const int32_t* sw = swaps + (int64_t)fi * swap_stride;
+  const SwapTask t = tasks[find_swap_task(tasks, ntask, blockIdx.x)];
+  const int64_t c0 = ((int64_t)blockIdx.x - t.wg0) * 64;
+  const int64_t ntot = (int64_t)(t.b - t.a) - (t.c_hi - t.c_lo);
+  const int ncol = (int)min<int64_t>(64, ntot - c0);
+  if (ncol <= 0) return;
+  const SNode s = sn[t.s];
+  FrontPtrs f = front_ptrs(s, store, scratch);
+  const int skip = t.c_hi - t.c_lo;
+  for (int u = 0; u < t.nsub; ++u) {
+    const int32_t* sw = swaps + (int64_t)(t.slot0 + u) * swap_stride;
     const int nsw = sw[0];
     if (nsw == 0) continue;   // uniform per workgroup
-    const SNode s = sn[ft[fi].s];
-    FrontPtrs f = front_ptrs(s, store, scratch);
-    const int64_t M = f.M;
-    const int kb = ft[fi].pad;
-    const int w = min(s.nb, (int)f.ns - kb);
+    const int kb = t.kb0 + u * s.nb;
     const int cnt = min(64, nsw);
-    for (int64_t c0 = 0; c0 < M - w; c0 += 64) {
-      const int ncol = (int)min<int64_t>(64, M - w - c0);
-      for (int idx = threadIdx.x; idx < cnt * ncol; idx += 256) {
-        const int p = idx % cnt, cj = idx / cnt;
-        const int64_t c = c0 + cj, col = c < kb ? c : c + w;
-        buf[cj * 65 + p] = *fel(f, kb + sw[2 + 2 * p], col);
-      }
-      __syncthreads();
-      for (int idx = threadIdx.x; idx < cnt * ncol; idx += 256) {
-        const int p = idx % cnt, cj = idx / cnt;
-        const int64_t c = c0 + cj, col = c < kb ? c : c + w;
-        *fel(f, kb + sw[1 + 2 * p], col) = buf[cj * 65 + p];
-      }
-      __syncthreads();
+    for (int idx = threadIdx.x; idx < cnt * ncol; idx += 256) {
+      const int p = idx % cnt, cj = idx / cnt;
+      int64_t col = t.a + c0 + cj;
+      if (col >= t.c_lo) col += skip;
+      buf[cj * 65 + p] = *fel(f, kb + sw[2 + 2 * p], col);
     }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < cnt * ncol; idx += 256) {
+      const int p = idx % cnt, cj = idx / cnt;
+      int64_t col = t.a + c0 + cj;
+      if (col >= t.c_lo) col += skip;
+      *fel(f, kb + sw[1 + 2 * p], col) = buf[cj * 65 + p];
+    }
+    __syncthreads();
   }
 }
 
@@ -742,6 +657,47 @@ __device__ __forceinline__ int find_front_tile(const FrontTile* __restrict__ ft,
     else hi = mid - 1;
   }
   return lo;
+}
+
+// Full-width (w == W) triangular solves for one column / row held in registers, with the
+// triangle broadcast from LDS.  Each elimination step first issues all of its LDS reads, then
+// its FMAs (sched_barrier keeps the scheduler from interleaving them), so the LDS latency is
+// paid once per step instead of once per pair of FMAs.  Same operations in the same order as
+// the guarded generic loops: results are bitwise identical.
+template <int W, int LD = W, int XN = W>
+__device__ __forceinline__ void lower_unit_solve_fast(double (&x)[XN], const double* __restrict__ sT) {
+#pragma unroll
+  for (int j = 0; j < W - 1; ++j) {
+    double lc[W];
+#pragma unroll
+    for (int i = j + 1; i < W; ++i) lc[i] = sT[j * LD + i];
+    __builtin_amdgcn_sched_barrier(0);
+    const double xj = x[j];
+#pragma unroll
+    for (int i = j + 1; i < W; ++i) x[i] = fma(-lc[i], xj, x[i]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// x <- x U^{-1} for a row vector x, U = sT (stored [col][row]), rd = 1/diag(U); returns max |x|
+template <int W>
+__device__ __forceinline__ double upper_right_solve_fast(double (&x)[W], const double* __restrict__ sT,
+                                                         const double* __restrict__ rd) {
+  double gmax = 0.0;
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    double uc[W];
+    const double r = rd[j];
+#pragma unroll
+    for (int k = j + 1; k < W; ++k) uc[k] = sT[k * W + j];
+    __builtin_amdgcn_sched_barrier(0);
+    x[j] = x[j] * r;
+    gmax = fmax(gmax, fabs(x[j]));
+#pragma unroll
+    for (int k = j + 1; k < W; ++k) x[k] = fma(-x[j], uc[k], x[k]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  return gmax;
 }
 
 // Two-level blocking: inner panels (nb = 32/64 columns) are grouped in outer blocks of OB = 256
@@ -774,7 +730,7 @@ __global__ __launch_bounds__(256) void k_trsm_u(const FrontTile* __restrict__ ft
   const int64_t ostart = (int64_t)(kb / OB) * OB;
   const int64_t oend = min<int64_t>(ns, ostart + OB);
   const int tid = threadIdx.x;
-  const double* Lkk = f.L + (int64_t)kb * M + kb;
+  const gdbl* Lkk = f.L + (int64_t)kb * M + kb;
   for (int idx = tid; idx < W * W; idx += 256) {
     const int i = idx % W, j = idx / W;
     sT[idx] = (i < w && j < w) ? Lkk[(int64_t)j * M + i] : 0.0;
@@ -782,8 +738,24 @@ __global__ __launch_bounds__(256) void k_trsm_u(const FrontTile* __restrict__ ft
   __syncthreads();
   const int64_t col = oend + tile * 256 + tid;
   if (col >= M) return;
-  double* cp = fel(f, kb, col);
+  gdbl* cp = fel(f, kb, col);
   double x[W];
+  if (w == W && (mode & 2)) {
+#pragma unroll
+    for (int j = 0; j < W; ++j) x[j] = cp[j];
+    lower_unit_solve_fast<W>(x, sT);
+#pragma unroll
+    for (int j = 0; j < W; ++j) cp[j] = x[j];
+    return;
+  }
+  if (W == 64 && w == 32 && (mode & 2)) {   // 32-wide panels (mode 1 fronts)
+#pragma unroll
+    for (int j = 0; j < 32; ++j) x[j] = cp[j];
+    lower_unit_solve_fast<32, W>(x, sT);
+#pragma unroll
+    for (int j = 0; j < 32; ++j) cp[j] = x[j];
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < W; ++j) x[j] = j < w ? cp[j] : 0.0;
 #pragma unroll
@@ -799,67 +771,6 @@ __global__ __launch_bounds__(256) void k_trsm_u(const FrontTile* __restrict__ ft
     if (j < w) cp[j] = x[j];
 }
 
-// ------------------------------------------------------------------------------------
-// Blocked path, step 3: rows below the candidate block, L = A * U_kk^{-1}.  One thread per
-// row holds its w panel entries in registers; U_kk is broadcast from LDS.  Tracks the
-// growth max |l| for the threshold check of mode 2.
-// ------------------------------------------------------------------------------------
-template <int W>
-__global__ __launch_bounds__(256) void k_trsm_l(const FrontTile* __restrict__ ft, int nft, int step,
-                                                const SNode* __restrict__ sn,
-                                                double* __restrict__ store,
-                                                double* __restrict__ scratch,
-                                                int32_t* __restrict__ info,
-                                                double* __restrict__ growth, double piv_tol) {
-  __shared__ double sU[W * W];
-  __shared__ double s_red[4];
-  const int64_t b = blockIdx.x;
-  const int fi = find_front_tile(ft, nft, b);
-  const int sid = ft[fi].s;
-  const SNode s = sn[sid];
-  const int64_t tile = b - ft[fi].wg0;
-  FrontPtrs f = front_ptrs(s, store, scratch);
-  const int64_t M = f.M;
-  const int ns = (int)f.ns;
-  const int kb = step * s.nb;
-  const int w = min(s.nb, ns - kb);
-  const int R = (s.mode == 1) ? ns - kb : w;
-  const int64_t r0 = kb + R;  // first row handled here
-  const int tid = threadIdx.x;
-  double* P = f.L + (int64_t)kb * M;  // column kb of the L panel
-  for (int idx = tid; idx < W * W; idx += 256) {
-    int i = idx % W, j = idx / W;
-    sU[idx] = (i < w && j < w) ? P[(int64_t)j * M + kb + i] : 0.0;
-  }
-  __syncthreads();
-  const int64_t row = r0 + tile * 256 + tid;
-  double gmax = 0.0;
-  if (row < M) {
-    double x[W];
-#pragma unroll
-    for (int j = 0; j < W; ++j) x[j] = (j < w) ? P[(int64_t)j * M + row] : 0.0;
-#pragma unroll
-    for (int j = 0; j < W; ++j) {
-      if (j < w) {
-        x[j] = x[j] / sU[j * W + j];
-        gmax = fmax(gmax, fabs(x[j]));
-#pragma unroll
-        for (int k = j + 1; k < W; ++k) x[k] = fma(-x[j], sU[k * W + j], x[k]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < W; ++j)
-      if (j < w) P[(int64_t)j * M + row] = x[j];
-  }
-  gmax = wave_max(gmax);
-  if ((tid & 63) == 0) s_red[tid >> 6] = gmax;
-  __syncthreads();
-  if (tid == 0) {
-    double g = fmax(fmax(s_red[0], s_red[1]), fmax(s_red[2], s_red[3]));
-    if (g > 0.0) atomic_max_pos(&growth[0], g);
-    if (g > 1.0 / piv_tol) atomicOr(&info[sid], 2);
-  }
-}
 
 // ------------------------------------------------------------------------------------
 // One launch per inner step for both triangular solves of the panel (row swaps already
@@ -877,7 +788,8 @@ __global__ __launch_bounds__(256) void k_step_trsm(const FrontTile* __restrict__
                                                    double* __restrict__ store,
                                                    double* __restrict__ scratch,
                                                    int32_t* __restrict__ info,
-                                                   double* __restrict__ growth, double piv_tol) {
+                                                   double* __restrict__ growth, double piv_tol,
+                                                   int fast) {
   __shared__ double sT[W * W];   // L_kk (role U) or U_kk (role L), [col][row]
   __shared__ double s_rd[W];     // 1 / diag(U_kk) (role L)
   __shared__ double s_red[4];
@@ -894,15 +806,23 @@ __global__ __launch_bounds__(256) void k_step_trsm(const FrontTile* __restrict__
     const int w = min(s.nb, ns - kb);
     const int64_t ostart = (int64_t)(kb / OB) * OB;
     const int64_t oend = min<int64_t>(ns, ostart + OB);
-    const double* Lkk = f.L + (int64_t)kb * M + kb;
+    const gdbl* Lkk = f.L + (int64_t)kb * M + kb;
     for (int idx = tid; idx < W * W; idx += 256) {
       const int i = idx % W, j = idx / W;
       sT[idx] = (i < w && j < w) ? Lkk[(int64_t)j * M + i] : 0.0;
     }
     __syncthreads();
     const int64_t col = kb + w + tile * 256 + tid;
-    if (col < oend) {
-      double* cp = fel(f, kb, col);   // rows [kb, kb+w) of this column are contiguous
+    if (col < oend && w == W && fast) {
+      gdbl* cp = fel(f, kb, col);
+      double x[W];
+#pragma unroll
+      for (int j = 0; j < W; ++j) x[j] = cp[j];
+      lower_unit_solve_fast<W>(x, sT);
+#pragma unroll
+      for (int j = 0; j < W; ++j) cp[j] = x[j];
+    } else if (col < oend) {
+      gdbl* cp = fel(f, kb, col);   // rows [kb, kb+w) of this column are contiguous
       double x[W];
 #pragma unroll
       for (int j = 0; j < W; ++j) x[j] = j < w ? cp[j] : 0.0;
@@ -935,7 +855,7 @@ __global__ __launch_bounds__(256) void k_step_trsm(const FrontTile* __restrict__
   const int w = min(s.nb, ns - kb);
   const int R = (s.mode == 1) ? ns - kb : w;
   const int64_t r0 = kb + R;
-  double* P = f.L + (int64_t)kb * M;
+  gdbl* P = f.L + (int64_t)kb * M;
   for (int idx = tid; idx < W * W; idx += 256) {
     const int i = idx % W, j = idx / W;
     sT[idx] = (i < w && j < w) ? P[(int64_t)j * M + kb + i] : 0.0;
@@ -945,7 +865,14 @@ __global__ __launch_bounds__(256) void k_step_trsm(const FrontTile* __restrict__
   __syncthreads();
   const int64_t row = r0 + tile * 256 + tid;
   double gmax = 0.0;
-  if (row < M) {
+  if (row < M && w == W && fast) {
+    double x[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) x[j] = P[(int64_t)j * M + row];
+    gmax = upper_right_solve_fast<W>(x, sT, s_rd);
+#pragma unroll
+    for (int j = 0; j < W; ++j) P[(int64_t)j * M + row] = x[j];
+  } else if (row < M) {
     double x[W];
 #pragma unroll
     for (int j = 0; j < W; ++j) x[j] = (j < w) ? P[(int64_t)j * M + row] : 0.0;
@@ -994,6 +921,9 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
   __shared__ double Bs[2][GBK][GBN + 2];
   const int64_t b = blockIdx.x;
   const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+  const gdbl* gA = gbl(t.A);
+  const gdbl* gB = gbl(t.B);
+  gdbl* gC = gbl(t.C);
   const int64_t tl = b - t.tile0;
   const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
   const int m0 = tm * GBM, n0 = tn * GBN;
@@ -1015,9 +945,9 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
     for (int r = 0; r < 4; ++r) {
       int kk = ak + 4 * r;
       int row = m0 + ar;
-      ra[r] = (row < t.m && k0 + kk < K) ? t.A[(int64_t)(k0 + kk) * t.lda + row] : 0.0;
+      ra[r] = (row < t.m && k0 + kk < K) ? gA[(int64_t)(k0 + kk) * t.lda + row] : 0.0;
       int col = n0 + bc + 16 * r;
-      rb[r] = (col < t.n && k0 + bk < K) ? t.B[(int64_t)col * t.ldb + k0 + bk] : 0.0;
+      rb[r] = (col < t.n && k0 + bk < K) ? gB[(int64_t)col * t.ldb + k0 + bk] : 0.0;
     }
   };
   auto sstore = [&](int buf) {
@@ -1057,7 +987,7 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
     for (int i = 0; i < 4; ++i) {
       int row = m0 + tx + 16 * i;
       if (row < t.m) {
-        double* c = t.C + (int64_t)col * t.ldc + row;
+        gdbl* c = gC + (int64_t)col * t.ldc + row;
         *c = *c - acc[i][j];
       }
     }
@@ -1082,6 +1012,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__
   __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
   const int64_t b = blockIdx.x;
   const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+  const gdbl* gA = gbl(t.A);
+  const gdbl* gB = gbl(t.B);
+  gdbl* gC = gbl(t.C);
   const int64_t tl = b - t.tile0;
   const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
   const int m0 = tm * HBM_, n0 = tn * HBM_;
@@ -1098,7 +1031,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__
   const int K = t.k;
   const int arow = m0 + ar;
   const bool arow_ok = arow < t.m;
-  const double* Ap = t.A + arow;
+  const gdbl* Ap = gA + arow;
   double ra[8], rb[8];
   auto gload = [&](int k0) {
 #pragma unroll
@@ -1106,7 +1039,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__
       const int kk = k0 + ak + 2 * r;
       ra[r] = (arow_ok && kk < K) ? Ap[(int64_t)kk * t.lda] : 0.0;
       const int col = n0 + bc + 16 * r;
-      rb[r] = (col < t.n && k0 + bk < K) ? t.B[(int64_t)col * t.ldb + k0 + bk] : 0.0;
+      rb[r] = (col < t.n && k0 + bk < K) ? gB[(int64_t)col * t.ldb + k0 + bk] : 0.0;
     }
   };
   auto sstore = [&](int buf) {
@@ -1147,7 +1080,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__
   for (int j = 0; j < 8; ++j) {
     const int col = n0 + 2 * ty + 32 * (j >> 1) + (j & 1);
     if (col >= t.n) continue;
-    double* Cc = t.C + (int64_t)col * t.ldc;
+    gdbl* Cc = gC + (int64_t)col * t.ldc;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int row = m0 + 2 * tx + 32 * (i >> 1) + (i & 1);
@@ -1169,6 +1102,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
   __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
   const int64_t b = blockIdx.x;
   const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+  const gdbl* gA = gbl(t.A);
+  const gdbl* gB = gbl(t.B);
+  gdbl* gC = gbl(t.C);
   const int64_t tl = b - t.tile0;
   const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
   const int m0 = tm * HBM_, n0 = tn * HBM_;
@@ -1184,7 +1120,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
   const int K = t.k;
   const int arow = m0 + ar;
   const bool arow_ok = arow < t.m;
-  const double* Ap = t.A + arow;
+  const gdbl* Ap = gA + arow;
   double ra[8], rb[8];
   auto gload = [&](int k0) {
 #pragma unroll
@@ -1192,7 +1128,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
       const int kk = k0 + ak + 2 * r;
       ra[r] = (arow_ok && kk < K) ? Ap[(int64_t)kk * t.lda] : 0.0;
       const int col = n0 + bc + 16 * r;
-      rb[r] = (col < t.n && k0 + bk < K) ? t.B[(int64_t)col * t.ldb + k0 + bk] : 0.0;
+      rb[r] = (col < t.n && k0 + bk < K) ? gB[(int64_t)col * t.ldb + k0 + bk] : 0.0;
     }
   };
   auto sstore = [&](int buf) {
@@ -1237,7 +1173,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
       for (int r = 0; r < 4; ++r) {
         const int col = n0 + wc + 16 * j + lk + 4 * r;
         if (col < t.n) {
-          double* c = t.C + (int64_t)col * t.ldc + row;
+          gdbl* c = gC + (int64_t)col * t.ldc + row;
           *c = *c - acc[i][j][r];
         }
       }
@@ -1498,15 +1434,7 @@ static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / 
 hipError_t init_kernel_attributes() {
   hipError_t e = hipFuncSetAttribute((const void*)k_front_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
   if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)k_panel, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-  if (e != hipSuccess) return e;
-  const void* ks[4] = {(const void*)k_panel1<1>, (const void*)k_panel1<2>, (const void*)k_panel1<4>,
-                       (const void*)k_panel1<8>};
-  for (auto k : ks) {
-    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
+  return e;
 }
 
 hipError_t launch_rowscale(hipStream_t st, int64_t n, const int64_t* rowptr, const int32_t* ent,
@@ -1541,26 +1469,19 @@ hipError_t launch_front_lds(hipStream_t st, int cnt, int Mmax, const int32_t* li
   k_front_lds<<<cnt, 256, lds, st>>>(list, sn, store, scratch, rowperm, info, growth, diag_tol, piv_tol);
   return hipGetLastError();
 }
-hipError_t launch_panel(hipStream_t st, int cnt, int lds_doubles, int step, int slot0, const int32_t* list,
-                        const SNode* sn, double* store, double* scratch, int32_t* rowperm,
-                        int32_t* swaps, int64_t swap_stride, int32_t* info, double* growth,
-                        double diag_tol) {
-  if (cnt <= 0) return hipSuccess;
-  size_t lds = (size_t)lds_doubles * sizeof(double);
-  k_panel<<<cnt, 256, lds, st>>>(list, step, slot0, sn, store, scratch, rowperm, swaps, swap_stride, info,
-                                 growth, diag_tol);
-  return hipGetLastError();
-}
 hipError_t launch_panel1(hipStream_t st, int cnt, int lds_doubles, int rmax, int wmax, int step,
-                         int slot0, const int32_t* list,
+                         const int32_t* list,
                          const SNode* sn, double* store, double* scratch, int32_t* rowperm,
                          int32_t* swaps, int64_t swap_stride, int32_t* info, double* growth,
                          double diag_tol) {
   if (cnt <= 0) return hipSuccess;
   size_t lds = (size_t)lds_doubles * sizeof(double);
-#define PANEL1_ARGS list, step, slot0, sn, store, scratch, rowperm, swaps, swap_stride, info, growth, diag_tol
+#define PANEL1_ARGS list, step, sn, store, scratch, rowperm, swaps, swap_stride, info, growth, diag_tol
   (void)lds;
-  if (wmax > 32) k_panel_reg<64, 1><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
+  static const bool lds_panel = std::getenv("SMLU_LDS_PANEL") != nullptr;
+  if (wmax > 32 && !lds_panel) k_panel_wave<64><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
+  else if (wmax > 32) k_panel_reg<64, 1><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
+  else if (rmax <= 64 && !lds_panel) k_panel_wave<32><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
   else if (rmax <= 64) k_panel_reg<32, 1><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
   else if (rmax <= 128) k_panel_reg<32, 2><<<cnt, 128, 0, st>>>(PANEL1_ARGS);
   else if (rmax <= 256) k_panel_reg<32, 4><<<cnt, 256, 0, st>>>(PANEL1_ARGS);
@@ -1568,22 +1489,23 @@ hipError_t launch_panel1(hipStream_t st, int cnt, int lds_doubles, int rmax, int
 #undef PANEL1_ARGS
   return hipGetLastError();
 }
-hipError_t launch_laswp(hipStream_t st, const FrontTile* ft, int nft, const SNode* sn, double* store,
-                        double* scratch, const int32_t* swaps, int64_t swap_stride) {
-  if (nft <= 0) return hipSuccess;
-  k_laswp<<<(unsigned)min(nft, 1024), 256, 0, st>>>(ft, nft, sn, store, scratch, swaps, swap_stride);
+hipError_t launch_laswp(hipStream_t st, int64_t nwg, const SwapTask* tasks, int ntask, const SNode* sn,
+                        double* store, double* scratch, const int32_t* swaps, int64_t swap_stride) {
+  if (nwg <= 0) return hipSuccess;
+  k_laswp<<<(unsigned)nwg, 256, 0, st>>>(tasks, ntask, sn, store, scratch, swaps, swap_stride);
   return hipGetLastError();
 }
 hipError_t launch_step_trsm(hipStream_t st, int W, const FrontTile* ftU, int nftU, int64_t nU,
                             const FrontTile* ftL, int nftL, int64_t nL, int step, int OB, const SNode* sn,
-                            double* store, double* scratch, int32_t* info, double* growth, double piv_tol) {
+                            double* store, double* scratch, int32_t* info, double* growth, double piv_tol,
+                            int fast) {
   if (nU + nL <= 0) return hipSuccess;
   if (W <= 32)
     k_step_trsm<32><<<(unsigned)(nU + nL), 256, 0, st>>>(ftU, nftU, nU, ftL, nftL, step, OB, sn, store,
-                                                         scratch, info, growth, piv_tol);
+                                                         scratch, info, growth, piv_tol, fast);
   else
     k_step_trsm<64><<<(unsigned)(nU + nL), 256, 0, st>>>(ftU, nftU, nU, ftL, nftL, step, OB, sn, store,
-                                                         scratch, info, growth, piv_tol);
+                                                         scratch, info, growth, piv_tol, fast);
   return hipGetLastError();
 }
 hipError_t launch_trsm_u(hipStream_t st, int64_t nwg, const FrontTile* ft, int nft, int OB, int mode,
@@ -1591,16 +1513,6 @@ hipError_t launch_trsm_u(hipStream_t st, int64_t nwg, const FrontTile* ft, int n
                          int64_t swap_stride) {
   if (nwg <= 0) return hipSuccess;
   k_trsm_u<64><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, OB, mode, sn, store, scratch, swaps, swap_stride);
-  return hipGetLastError();
-}
-hipError_t launch_trsm_l(hipStream_t st, int64_t nwg, int W, const FrontTile* ft, int nft, int step,
-                         const SNode* sn, double* store, double* scratch, int32_t* info,
-                         double* growth, double piv_tol) {
-  if (nwg <= 0) return hipSuccess;
-  if (W <= 32)
-    k_trsm_l<32><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, scratch, info, growth, piv_tol);
-  else
-    k_trsm_l<64><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, scratch, info, growth, piv_tol);
   return hipGetLastError();
 }
 hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask, int tile) {

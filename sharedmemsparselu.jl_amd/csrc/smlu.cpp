@@ -19,6 +19,7 @@
 #include <limits>
 #include <map>
 #include <memory>
+#include <unordered_map>
 #include <string>
 #include <vector>
 
@@ -36,18 +37,14 @@ hipError_t launch_extend_add(hipStream_t, int64_t, const int2*, const SNode*, co
 hipError_t launch_front_lds(hipStream_t, int, int, const int32_t*, const SNode*, double*, double*,
                             int32_t*, int32_t*, double*, double, double);
 hipError_t init_kernel_attributes();
-hipError_t launch_panel(hipStream_t, int, int, int, int, const int32_t*, const SNode*, double*, double*,
-                        int32_t*, int32_t*, int64_t, int32_t*, double*, double);
-hipError_t launch_panel1(hipStream_t, int, int, int, int, int, int, const int32_t*, const SNode*, double*, double*,
+hipError_t launch_panel1(hipStream_t, int, int, int, int, int, const int32_t*, const SNode*, double*, double*,
                          int32_t*, int32_t*, int64_t, int32_t*, double*, double);
 hipError_t launch_step_trsm(hipStream_t, int, const FrontTile*, int, int64_t, const FrontTile*, int, int64_t,
-                            int, int, const SNode*, double*, double*, int32_t*, double*, double);
-hipError_t launch_laswp(hipStream_t, const FrontTile*, int, const SNode*, double*, double*, const int32_t*,
+                            int, int, const SNode*, double*, double*, int32_t*, double*, double, int);
+hipError_t launch_laswp(hipStream_t, int64_t, const SwapTask*, int, const SNode*, double*, double*, const int32_t*,
                         int64_t);
 hipError_t launch_trsm_u(hipStream_t, int64_t, const FrontTile*, int, int, int, const SNode*, double*,
                          double*, const int32_t*, int64_t);
-hipError_t launch_trsm_l(hipStream_t, int64_t, int, const FrontTile*, int, int, const SNode*, double*,
-                         double*, int32_t*, double*, double);
 hipError_t launch_gemm(hipStream_t, int64_t, const GemmTask*, int, int);
 hipError_t launch_fwd_gather(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                              const int32_t*, double*, double*);
@@ -73,17 +70,18 @@ constexpr int kFullPivNs = 512;  // blocked fronts up to this many pivots search
 constexpr int kNbFull = 32;
 constexpr int kNbTile = 64;
 constexpr int kSwapStride = 1 + 2 * 64;
-constexpr int kOB = 256;        // outer block of the two-level blocked front factorization
+constexpr int kOBDefault = 256;   // outer block of the two-level blocked front factorization
 
 thread_local std::string g_last_error;
 
 enum Kind : int {
   K_MEMSET_STORE, K_MEMSET_SCRATCH, K_SCATTER, K_EXTADD, K_FRONT_LDS, K_PANEL, K_TRSMU, K_TRSML,
-  K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_GEMM22, K_LASWP, K_STEPTRSM, K_NKIND
+  K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_GEMM22, K_LASWP, K_STEPTRSM, K_GEMMU,
+  K_GEMMO, K_FORK, K_JOIN, K_NKIND
 };
 const char* kKindName[K_NKIND] = {"memset", "memset", "assemble", "assemble", "small", "panel",
                                   "trsm", "trsm", "gemm", "solve", "solve", "solve", "solve",
-                                  "solve", "solve", "gemm22", "trsm", "trsm"};
+                                  "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "sync", "sync"};
 constexpr int kSolveBigNs = 256;  // fronts with more pivots use the multi-workgroup solve
 
 struct Launch {
@@ -92,6 +90,7 @@ struct Launch {
   int64_t off = 0, cnt = 0, nwg = 0, aux = 0, aux2 = 0;
   int64_t off2 = 0, cnt2 = 0, nwg2 = 0;   // second work list (merged launches)
   double flops = 0;
+  int side = 0;                           // 1 = issued on the look-ahead stream
 };
 
 template <class T>
@@ -126,6 +125,8 @@ struct smlu_handle {
   Plan plan;
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;             // look-ahead stream (trailing updates beyond the next block)
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::string err;
   int64_t errcol = -1;
   bool have_numeric = false;
@@ -138,6 +139,7 @@ struct smlu_handle {
   DBuf<int2> xtasks;
   DBuf<FrontTile> ftiles;
   DBuf<GemmTask> gtasks;
+  DBuf<SwapTask> stasks;
   // schedule
   std::vector<Launch> fac, fwd, bwd;
   std::vector<SNode> hsn;
@@ -154,6 +156,10 @@ struct smlu_handle {
   int fac_exec_profile = -1;
   size_t fac_graph_events = 0;
   bool graph_failed = false;
+  bool lookahead = false;     // SMLU_LOOKAHEAD=1: trailing updates beyond the next block on a side stream
+  int ob = kOBDefault;        // outer block width (SMLU_OB overrides; multiple of 64)
+  int64_t t128_min = 128;     // 128x128 GEMM tiles when a launch has at least this many
+  int fast_trsm = 1;          // batched-LDS full-width triangular solves (SMLU_SLOW_TRSM=1: off)
   ~smlu_handle() { release_all(); }
   void release_buffers() {
     if (stream) (void)hipSetDevice(device);
@@ -168,6 +174,7 @@ struct smlu_handle {
     xtasks.free();
     ftiles.free();
     gtasks.free();
+    stasks.free();
   }
   void release_graphs() {
     if (fac_exec) (void)hipGraphExecDestroy(fac_exec);
@@ -186,6 +193,11 @@ struct smlu_handle {
     ev_kind.clear();
     if (hinfo) (void)hipHostFree(hinfo);
     hinfo = nullptr;
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_join) (void)hipEventDestroy(ev_join);
+    ev_fork = ev_join = nullptr;
+    if (side) (void)hipStreamDestroy(side);
+    side = nullptr;
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
   }
@@ -270,23 +282,30 @@ static int build_schedule(smlu_handle* h) {
   std::vector<int2> xt;
   std::vector<FrontTile> ft;
   std::vector<GemmTask> gt;
+  std::vector<SwapTask> st_tasks;
   double* store = h->store.p;
   double* scratch = h->scratch.p;
   h->fac.clear();
+  h->lookahead = std::getenv("SMLU_LOOKAHEAD") != nullptr;
+  h->fast_trsm = std::getenv("SMLU_SLOW_TRSM") ? 0 : 1;
+  if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
+  if (const char* e = std::getenv("SMLU_T128MIN")) h->t128_min = std::atoll(e);
   h->gemm_flops = 0;
   h->gemm22_flops = 0;
   h->dense_flops = P.flops;
   int64_t max_list = 1;
   // GEMM launches: 128x128 tiles when the launch has enough of them to fill the GPU,
   // otherwise 64x64 tiles (same per-element arithmetic, bitwise-identical results).
-  auto add_gemm_launch = [&](std::vector<GemmTask>& cand, double fl, int step) {
+  auto add_gemm_launch = [&](std::vector<GemmTask>& cand, double fl, int step, int kind = K_GEMM,
+                             int side = 0) {
     if (cand.empty()) return;
     int64_t t128 = 0;
     for (auto& g : cand) t128 += (int64_t)((g.m + 127) / 128) * ((g.n + 127) / 128);
-    int tile = t128 >= 512 ? 128 : 64;
+    int tile = t128 >= h->t128_min ? 128 : 64;
     if (tile == 128 && h->opts.use_mfma) tile = 129;   // fp64 MFMA variant of the 128 tile
     Launch L;
-    L.kind = step < 0 ? K_GEMM22 : K_GEMM;
+    L.kind = step < 0 ? K_GEMM22 : kind;
+    L.side = side;
     L.step = step;
     L.off = (int64_t)gt.size();
     L.aux = tile;
@@ -368,14 +387,27 @@ static int build_schedule(smlu_handle* h) {
     }
     // blocked fronts
     std::vector<int64_t> big;
+    std::unordered_map<int64_t, int64_t> bidx;   // front -> index in big (swap-list slots)
     int64_t maxsteps = 0;
     for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
       int64_t s = P.lev_sup[k];
       const SNode& r = h->hsn[s];
       if (r.mode == 0) continue;
+      bidx[s] = (int64_t)big.size();
       big.push_back(s);
       maxsteps = std::max<int64_t>(maxsteps, (r.ns + r.nb - 1) / r.nb);
     }
+    max_list = std::max<int64_t>(max_list, (int64_t)big.size() * (h->ob / 32));
+    // swap-list slot of sub-panel u of a front's current outer block
+    auto slot_of = [&](int64_t s, int64_t u) { return bidx[s] * (h->ob / 32) + u; };
+    bool side_busy = false;
+    auto join = [&]() {
+      if (!side_busy) return;
+      Launch J;
+      J.kind = K_JOIN;
+      h->fac.push_back(J);
+      side_busy = false;
+    };
     for (int64_t t = 0; t < maxsteps; ++t) {
       std::vector<int64_t> act;
       for (auto s : big) {
@@ -383,8 +415,6 @@ static int build_schedule(smlu_handle* h) {
         if (t * r.nb < r.ns) act.push_back(s);
       }
       if (act.empty()) continue;
-      max_list = std::max<int64_t>(max_list, (int64_t)act.size());
-      // panel, split into LDS classes (act sorted by LDS need; swap slots = position in act)
       // panel launch classes by register-kernel shape: (W=64, 1 wave), (W=32, 1/2/4/8 waves)
       auto pclass = [&](int64_t s) {
         const SNode& r = h->hsn[s];
@@ -401,32 +431,45 @@ static int build_schedule(smlu_handle* h) {
           L.kind = K_PANEL;
           L.step = (int)t;
           L.off = (int64_t)ilist.size();
-          L.aux2 = (int64_t)pos;  // first swap slot
-          int64_t rmax = 1, wmax = 1;
+          int64_t rmax = 1, wmax = 1, cnt = 0;
           while (pos < act.size() && pclass(act[pos]) == c) {
             const SNode& r = h->hsn[act[pos]];
             int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
             rmax = std::max(rmax, r.mode == 1 ? r.ns - kb : w);
             wmax = std::max<int64_t>(wmax, r.nb);
             ilist.push_back((int32_t)act[pos]);
+            ilist.push_back((int32_t)slot_of(act[pos], t % (h->ob / r.nb)));
             ++pos;
+            ++cnt;
           }
-          L.cnt = (int64_t)ilist.size() - L.off;
+          L.cnt = cnt;
           L.aux = 0;
           L.nwg = rmax | (wmax << 16);
           if (L.cnt > 0) h->fac.push_back(L);
         }
         if (pos != act.size()) return fail(h, SMLU_ERR_ARG, "internal: panel classes");
       }
-      // row swaps on every other column (cheap no-op without pivoting), then the U row block
-      // inside the outer block
-      L = Launch();
-      L.kind = K_LASWP;
-      L.step = (int)t;
-      L.off = (int64_t)ft.size();
-      for (auto s : act) ft.push_back(FrontTile{(int32_t)s, (int32_t)(t * h->hsn[s].nb), 0});
-      L.cnt = (int64_t)act.size();
-      h->fac.push_back(L);
+      // row swaps inside the outer block (the other columns get them at the end of the block)
+      {
+        L = Launch();
+        L.kind = K_LASWP;
+        L.step = (int)t;
+        L.off = (int64_t)st_tasks.size();
+        int64_t wg = 0;
+        for (auto s : act) {
+          const SNode& r = h->hsn[s];
+          int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
+          int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
+          int64_t ncol = oend - ostart - w;
+          if (ncol <= 0) continue;
+          st_tasks.push_back(SwapTask{(int32_t)s, (int32_t)kb, 1, (int32_t)slot_of(s, t % (h->ob / r.nb)),
+                                      (int32_t)ostart, (int32_t)oend, (int32_t)kb, (int32_t)(kb + w), wg});
+          wg += (ncol + 63) / 64;
+        }
+        L.cnt = (int64_t)st_tasks.size() - L.off;
+        L.nwg = wg;
+        if (wg > 0) h->fac.push_back(L);
+      }
       {
         Launch T;
         T.kind = K_STEPTRSM;
@@ -436,7 +479,7 @@ static int build_schedule(smlu_handle* h) {
         for (auto s : act) {
           const SNode& r = h->hsn[s];
           int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
-          int64_t ostart = (kb / kOB) * kOB, oend = std::min<int64_t>(r.ns, ostart + kOB);
+          int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
           ft.push_back(FrontTile{(int32_t)s, (int32_t)kb, wgU});
           wgU += (oend - kb - w + 255) / 256;
           W = std::max<int64_t>(W, w);
@@ -464,7 +507,7 @@ static int build_schedule(smlu_handle* h) {
         for (auto s : act) {
           const SNode& r = h->hsn[s];
           int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
-          int64_t ostart = (kb / kOB) * kOB, oend = std::min<int64_t>(r.ns, ostart + kOB);
+          int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
           int64_t m1 = M - kb - w, n1 = oend - kb - w;
           if (m1 > 0 && n1 > 0) {
             GemmTask g{};
@@ -479,105 +522,146 @@ static int build_schedule(smlu_handle* h) {
         }
         add_gemm_launch(cand, fl, (int)t);
       }
-      // outer phase for the fronts whose outer block ends with this panel
+      // end of an outer block [ostart, oend): deferred row swaps on the columns outside it, the
+      // U rows of the block right of it, and the trailing update with k = oend - ostart
+      std::vector<int64_t> fin_all;
+      for (auto s : act) {
+        const SNode& r = h->hsn[s];
+        int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
+        int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
+        if (kb + w == oend) fin_all.push_back(s);
+      }
+      if (fin_all.empty()) continue;
+      join();   // the previous block's look-ahead update has written these columns
       {
-        std::vector<int64_t> fin;
-        int64_t nsubmax = 0;
-        for (auto s : act) {
+        L = Launch();
+        L.kind = K_LASWP;
+        L.step = (int)t;
+        L.off = (int64_t)st_tasks.size();
+        int64_t wg = 0;
+        for (auto s : fin_all) {
           const SNode& r = h->hsn[s];
-          int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
-          int64_t ostart = (kb / kOB) * kOB, oend = std::min<int64_t>(r.ns, ostart + kOB);
-          if (kb + w != oend) continue;
-          int64_t M = (int64_t)r.ns + r.nu;
-          if (oend == M) continue;   // nothing right of the block
-          fin.push_back(s);
-          nsubmax = std::max<int64_t>(nsubmax, (oend - ostart + r.nb - 1) / r.nb);
+          int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb;
+          int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
+          int64_t ncol = M - (oend - ostart);
+          if (ncol <= 0) continue;
+          st_tasks.push_back(SwapTask{(int32_t)s, (int32_t)ostart, (int32_t)((oend - ostart + r.nb - 1) / r.nb),
+                                      (int32_t)slot_of(s, 0), 0, (int32_t)M, (int32_t)ostart, (int32_t)oend, wg});
+          wg += (ncol + 63) / 64;
         }
-        for (int64_t u = 0; u < nsubmax; ++u) {
-          // (a) U row block of sub-panel u: TRSM on columns [oend, M)
-          L = Launch();
-          L.kind = K_TRSMU;
-          L.step = (int)t;
-          L.aux = 1;   // outer mode
-          L.off = (int64_t)ft.size();
-          int64_t wg = 0, cnt = 0;
-          std::vector<GemmTask> cand;
-          double fl = 0;
-          for (auto s : fin) {
-            const SNode& r = h->hsn[s];
-            int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb;
-            int64_t ostart = (kb / kOB) * kOB, oend = std::min<int64_t>(r.ns, ostart + kOB);
-            int64_t kbu = ostart + u * r.nb;
-            if (kbu >= oend) continue;
-            int64_t wu = std::min<int64_t>(r.nb, oend - kbu);
-            ft.push_back(FrontTile{(int32_t)s, (int32_t)kbu, wg});
-            wg += (M - oend + 255) / 256;
-            ++cnt;
-            // (b) rows below the sub-panel inside the block: [kbu+wu, oend) x [oend, M)
-            int64_t m = oend - kbu - wu;
-            if (m > 0) {
-              int64_t n1 = r.ns - oend;       // L-panel columns
-              if (n1 > 0) {
-                GemmTask g{};
-                g.A = store + r.Loff + kbu * M + kbu + wu;
-                g.B = store + r.Loff + oend * M + kbu;
-                g.C = store + r.Loff + oend * M + kbu + wu;
-                g.m = (int)m; g.n = (int)n1; g.k = (int)wu;
-                g.lda = (int)M; g.ldb = (int)M; g.ldc = (int)M;
-                cand.push_back(g);
-                fl += 2.0 * m * n1 * wu;
-              }
-              if (r.nu > 0) {                 // U12 columns
-                GemmTask g{};
-                g.A = store + r.Loff + kbu * M + kbu + wu;
-                g.B = store + r.Uoff + kbu;
-                g.C = store + r.Uoff + kbu + wu;
-                g.m = (int)m; g.n = r.nu; g.k = (int)wu;
-                g.lda = (int)M; g.ldb = r.ns; g.ldc = r.ns;
-                cand.push_back(g);
-                fl += 2.0 * m * (double)r.nu * wu;
-              }
-            }
-          }
-          L.cnt = cnt;
-          L.nwg = wg;
-          if (wg > 0) h->fac.push_back(L);
-          add_gemm_launch(cand, fl, (int)t);
-        }
-        // (c) outer trailing update with k = oend - ostart (<= 256)
+        L.cnt = (int64_t)st_tasks.size() - L.off;
+        L.nwg = wg;
+        if (wg > 0) h->fac.push_back(L);
+      }
+      std::vector<int64_t> fin;
+      int64_t nsubmax = 0;
+      for (auto s : fin_all) {
+        const SNode& r = h->hsn[s];
+        int64_t kb = t * r.nb;
+        int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
+        int64_t M = (int64_t)r.ns + r.nu;
+        if (oend == M) continue;   // nothing right of the block
+        fin.push_back(s);
+        nsubmax = std::max<int64_t>(nsubmax, (oend - ostart + r.nb - 1) / r.nb);
+      }
+      for (int64_t u = 0; u < nsubmax; ++u) {
+        // (a) U row block of sub-panel u: TRSM on columns [oend, M)
+        L = Launch();
+        L.kind = K_TRSMU;
+        L.step = (int)t;
+        L.aux = 1;   // outer mode
+        L.off = (int64_t)ft.size();
+        int64_t wg = 0, cnt = 0;
         std::vector<GemmTask> cand;
         double fl = 0;
         for (auto s : fin) {
           const SNode& r = h->hsn[s];
           int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb;
-          int64_t ostart = (kb / kOB) * kOB, oend = std::min<int64_t>(r.ns, ostart + kOB);
-          int64_t kk = oend - ostart;
-          int64_t m1 = M - oend, n1 = r.ns - oend;
-          if (m1 > 0 && n1 > 0) {       // rows [oend, M) x L-panel columns [oend, ns)
-            GemmTask g{};
-            g.A = store + r.Loff + ostart * M + oend;
-            g.B = store + r.Loff + oend * M + ostart;
-            g.C = store + r.Loff + oend * M + oend;
-            g.m = (int)m1; g.n = (int)n1; g.k = (int)kk;
-            g.lda = (int)M; g.ldb = (int)M; g.ldc = (int)M;
-            cand.push_back(g);
-            fl += 2.0 * m1 * n1 * kk;
-          }
-          int64_t m2 = r.ns - oend;
-          if (m2 > 0 && r.nu > 0) {     // rows [oend, ns) x U12 columns
-            GemmTask g{};
-            g.A = store + r.Loff + ostart * M + oend;
-            g.B = store + r.Uoff + ostart;
-            g.C = store + r.Uoff + oend;
-            g.m = (int)m2; g.n = r.nu; g.k = (int)kk;
-            g.lda = (int)M; g.ldb = r.ns; g.ldc = r.ns;
-            cand.push_back(g);
-            fl += 2.0 * m2 * (double)r.nu * kk;
+          int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
+          int64_t kbu = ostart + u * r.nb;
+          if (kbu >= oend) continue;
+          int64_t wu = std::min<int64_t>(r.nb, oend - kbu);
+          ft.push_back(FrontTile{(int32_t)s, (int32_t)kbu, wg});
+          wg += (M - oend + 255) / 256;
+          ++cnt;
+          // (b) rows below the sub-panel inside the block: [kbu+wu, oend) x [oend, M)
+          int64_t m = oend - kbu - wu;
+          if (m > 0) {
+            int64_t n1 = r.ns - oend;       // L-panel columns
+            if (n1 > 0) {
+              GemmTask g{};
+              g.A = store + r.Loff + kbu * M + kbu + wu;
+              g.B = store + r.Loff + oend * M + kbu;
+              g.C = store + r.Loff + oend * M + kbu + wu;
+              g.m = (int)m; g.n = (int)n1; g.k = (int)wu;
+              g.lda = (int)M; g.ldb = (int)M; g.ldc = (int)M;
+              cand.push_back(g);
+              fl += 2.0 * m * n1 * wu;
+            }
+            if (r.nu > 0) {                 // U12 columns
+              GemmTask g{};
+              g.A = store + r.Loff + kbu * M + kbu + wu;
+              g.B = store + r.Uoff + kbu;
+              g.C = store + r.Uoff + kbu + wu;
+              g.m = (int)m; g.n = r.nu; g.k = (int)wu;
+              g.lda = (int)M; g.ldb = r.ns; g.ldc = r.ns;
+              cand.push_back(g);
+              fl += 2.0 * m * (double)r.nu * wu;
+            }
           }
         }
-        add_gemm_launch(cand, fl, (int)t);
+        L.cnt = cnt;
+        L.nwg = wg;
+        if (wg > 0) h->fac.push_back(L);
+        add_gemm_launch(cand, fl, (int)t, K_GEMMU);
       }
+      // (c) trailing update, k = oend - ostart <= 256.  With look-ahead the columns of the next
+      // outer block [oend, oend2) are updated on the main stream and the rest (columns
+      // [oend2, ns) and the U12 rows) on the side stream, overlapping the next block's panels.
+      std::vector<GemmTask> c1, c2;
+      double fl1 = 0, fl2 = 0;
+      for (auto s : fin) {
+        const SNode& r = h->hsn[s];
+        int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb;
+        int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
+        int64_t oend2 = h->lookahead ? std::min<int64_t>(r.ns, oend + h->ob) : r.ns;
+        int64_t kk = oend - ostart;
+        int64_t m1 = M - oend;
+        auto lpart = [&](int64_t ca, int64_t cb, std::vector<GemmTask>& cand, double& fl) {
+          if (m1 <= 0 || cb <= ca) return;      // rows [oend, M) x L-panel columns [ca, cb)
+          GemmTask g{};
+          g.A = store + r.Loff + ostart * M + oend;
+          g.B = store + r.Loff + ca * M + ostart;
+          g.C = store + r.Loff + ca * M + oend;
+          g.m = (int)m1; g.n = (int)(cb - ca); g.k = (int)kk;
+          g.lda = (int)M; g.ldb = (int)M; g.ldc = (int)M;
+          cand.push_back(g);
+          fl += 2.0 * m1 * (double)(cb - ca) * kk;
+        };
+        lpart(oend, oend2, c1, fl1);
+        lpart(oend2, r.ns, h->lookahead ? c2 : c1, h->lookahead ? fl2 : fl1);
+        int64_t m2 = r.ns - oend;
+        if (m2 > 0 && r.nu > 0) {     // rows [oend, ns) x U12 columns
+          GemmTask g{};
+          g.A = store + r.Loff + ostart * M + oend;
+          g.B = store + r.Uoff + ostart;
+          g.C = store + r.Uoff + oend;
+          g.m = (int)m2; g.n = r.nu; g.k = (int)kk;
+          g.lda = (int)M; g.ldb = r.ns; g.ldc = r.ns;
+          (h->lookahead ? c2 : c1).push_back(g);
+          (h->lookahead ? fl2 : fl1) += 2.0 * m2 * (double)r.nu * kk;
+        }
+      }
+      if (!c2.empty()) {
+        Launch F;
+        F.kind = K_FORK;
+        h->fac.push_back(F);
+        add_gemm_launch(c2, fl2, (int)t, K_GEMMO, 1);
+        side_busy = true;
+      }
+      add_gemm_launch(c1, fl1, (int)t, K_GEMMO);
     }
+    join();
     // F22 -= L21 * U12 for the blocked fronts of this level
     {
       std::vector<GemmTask> cand;
@@ -691,6 +775,7 @@ static int build_schedule(smlu_handle* h) {
   HIPCHK(h->xtasks.upload(xt.data(), xt.size(), st));
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
   HIPCHK(h->gtasks.upload(gt.data(), gt.size(), st));
+  HIPCHK(h->stasks.upload(st_tasks.data(), st_tasks.size(), st));
   HIPCHK(h->swaps.alloc((size_t)max_list * kSwapStride));
   HIPCHK(h->vbuf.alloc((size_t)std::max<int64_t>(voff, 1)));
   HIPCHK(hipStreamSynchronize(st));
@@ -700,7 +785,32 @@ static int build_schedule(smlu_handle* h) {
 static int setup_device(smlu_handle* h) {
   Plan& P = h->plan;
   HIPCHK(hipSetDevice(h->device));
-  if (!h->stream) HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  // the critical path (panels, swaps, solves, next-block updates) runs on a high-priority
+  // stream; the look-ahead trailing updates on a low-priority one
+  int prio_lo = 0, prio_hi = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  if (std::getenv("SMLU_NO_PRIORITY")) prio_lo = prio_hi = 0;
+  if (!h->stream) HIPCHK(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi));
+  if (!h->side) {
+    // SMLU_SIDE_RESERVE=r: keep r CUs of every 8 (one per XCD per step) free of look-ahead work
+    const char* rs = std::getenv("SMLU_SIDE_RESERVE");
+    int reserve = rs ? std::atoi(rs) : 0;
+    if (reserve > 0) {
+      hipDeviceProp_t pr;
+      HIPCHK(hipGetDeviceProperties(&pr, h->device));
+      int ncu = pr.multiProcessorCount;
+      std::vector<uint32_t> mask((ncu + 31) / 32, 0);
+      int kept = 0;
+      for (int c = 0; c < ncu; ++c)
+        if ((c / 8) % 32 >= reserve) { mask[c / 32] |= 1u << (c % 32); ++kept; }
+      HIPCHK(hipExtStreamCreateWithCUMask(&h->side, (uint32_t)mask.size(), mask.data()));
+      std::fprintf(stderr, "smlu: side stream on %d of %d CUs\n", kept, ncu);
+    } else {
+      HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_lo));
+    }
+  }
+  if (!h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
+  if (!h->ev_join) HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
   hipStream_t st = h->stream;
   HIPCHK(h->A.alloc((size_t)std::max<int64_t>(P.nnzA, 1)));
   HIPCHK(h->Rs.alloc((size_t)P.n));
@@ -742,8 +852,10 @@ struct Timer {
   smlu_handle* h;
   size_t used = 0;
   explicit Timer(smlu_handle* hh) : h(hh) {}
-  hipError_t begin(int kind, hipEvent_t* stop) {
-    if (!h->opts.profile) { *stop = nullptr; return hipSuccess; }
+  hipStream_t st = nullptr;
+  hipError_t begin(int kind, hipEvent_t* stop, hipStream_t s) {
+    st = s;
+    if (!h->opts.profile || kind == K_FORK || kind == K_JOIN) { *stop = nullptr; return hipSuccess; }
     if (used == h->ev_pool.size()) {
       hipEvent_t a, b;
       hipError_t e = hipEventCreate(&a);
@@ -755,11 +867,11 @@ struct Timer {
     }
     h->ev_kind[used] = kind;
     *stop = h->ev_pool[used].second;
-    hipError_t e = hipEventRecord(h->ev_pool[used].first, h->stream);
+    hipError_t e = hipEventRecord(h->ev_pool[used].first, st);
     ++used;
     return e;
   }
-  hipError_t end(hipEvent_t stop) { return stop ? hipEventRecord(stop, h->stream) : hipSuccess; }
+  hipError_t end(hipEvent_t stop) { return stop ? hipEventRecord(stop, st) : hipSuccess; }
   void collect() {
     for (size_t i = 0; i < used; ++i) {
       float ms = 0;
@@ -770,8 +882,16 @@ struct Timer {
 };
 
 static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, double piv_tol) {
-  hipStream_t st = h->stream;
+  hipStream_t st = L.side ? h->side : h->stream;
   switch (L.kind) {
+    case K_FORK: {
+      hipError_t e = hipEventRecord(h->ev_fork, h->stream);
+      return e != hipSuccess ? e : hipStreamWaitEvent(h->side, h->ev_fork, 0);
+    }
+    case K_JOIN: {
+      hipError_t e = hipEventRecord(h->ev_join, h->side);
+      return e != hipSuccess ? e : hipStreamWaitEvent(h->stream, h->ev_join, 0);
+    }
     case K_MEMSET_STORE:
       return hipMemsetAsync(h->store.p + L.off, 0, (size_t)L.cnt * sizeof(double), st);
     case K_MEMSET_SCRATCH:
@@ -787,23 +907,22 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
                               h->scratch.p, h->rowperm.p, h->info.p, h->growth.p, diag_tol, piv_tol);
     case K_STEPTRSM:
       return launch_step_trsm(st, (int)L.aux, h->ftiles.p + L.off, (int)L.cnt, L.nwg, h->ftiles.p + L.off2,
-                              (int)L.cnt2, L.nwg2, L.step, kOB, h->sn.p, h->store.p, h->scratch.p, h->info.p,
-                              h->growth.p, piv_tol);
+                              (int)L.cnt2, L.nwg2, L.step, h->ob, h->sn.p, h->store.p, h->scratch.p, h->info.p,
+                              h->growth.p, piv_tol, h->fast_trsm);
     case K_LASWP:
-      return launch_laswp(st, h->ftiles.p + L.off, (int)L.cnt, h->sn.p, h->store.p, h->scratch.p, h->swaps.p,
-                          kSwapStride);
+      return launch_laswp(st, L.nwg, h->stasks.p + L.off, (int)L.cnt, h->sn.p, h->store.p, h->scratch.p,
+                          h->swaps.p, kSwapStride);
     case K_PANEL:
       return launch_panel1(st, (int)L.cnt, (int)L.aux, (int)(L.nwg & 0xffff), (int)(L.nwg >> 16), L.step,
-                           (int)L.aux2, h->ilist.p + L.off, h->sn.p,
+                           h->ilist.p + L.off, h->sn.p,
                           h->store.p, h->scratch.p, h->rowperm.p, h->swaps.p, kSwapStride, h->info.p,
                           h->growth.p, diag_tol);
     case K_TRSMU:
-      return launch_trsm_u(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, kOB, (int)L.aux, h->sn.p,
+      return launch_trsm_u(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->ob, (int)L.aux | (h->fast_trsm << 1), h->sn.p,
                            h->store.p, h->scratch.p, h->swaps.p, kSwapStride);
-    case K_TRSML:
-      return launch_trsm_l(st, L.nwg, (int)L.aux, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p,
-                           h->store.p, h->scratch.p, h->info.p, h->growth.p, piv_tol);
     case K_GEMM:
+    case K_GEMMU:
+    case K_GEMMO:
     case K_GEMM22:
       return launch_gemm(st, L.nwg, h->gtasks.p + L.off, (int)L.cnt, (int)L.aux);
   }
@@ -827,9 +946,10 @@ static int enqueue_factor(smlu_handle* h, Timer& tm, bool dbg) {
   double piv_tol = h->opts.pivot_tol;
   for (const Launch& L : h->fac) {
     hipEvent_t stop;
-    HIPCHK(tm.begin(L.kind, &stop));
+    HIPCHK(tm.begin(L.kind, &stop, L.side ? h->side : st));
     hipError_t e = run_launch(h, L, diag_tol, piv_tol);
     if (e == hipSuccess && dbg) e = hipStreamSynchronize(st);
+    if (e == hipSuccess && dbg) e = hipStreamSynchronize(h->side);
     if (e != hipSuccess) {
       char buf[256];
       std::snprintf(buf, sizeof buf, "HIP error '%s' in launch kind=%d step=%d off=%lld cnt=%lld nwg=%lld aux=%lld aux2=%lld",
@@ -934,7 +1054,7 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode)
   auto t0 = std::chrono::steady_clock::now();
   Timer tm(h);
   hipEvent_t stop;
-  HIPCHK(tm.begin(K_FWD, &stop));
+  HIPCHK(tm.begin(K_FWD, &stop, h->stream));
   double* w = h->wrk.p;
   if (mode == 0) HIPCHK(launch_perm_in(st, P.n, h->p0.p, h->Rs.p, db, w));
   if (mode == 1) HIPCHK(launch_unswap(st, P.n, h->posfirst.p, h->rowperm.p, dx, w));

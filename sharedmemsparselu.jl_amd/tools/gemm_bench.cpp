@@ -13,7 +13,10 @@ using namespace smlu;
 static void fill(std::vector<double>& v, unsigned seed) { srand(seed); for (auto& x : v) x = rand() / (double)RAND_MAX - 0.5; }
 
 int main(int argc, char** argv) {
-  struct Shape { int m, n, k; } shapes[] = {{4096, 4096, 4096}, {8192, 8192, 1024}, {16384, 16384, 64}, {12000, 12000, 6000}, {1000, 1000, 300}, {300, 5000, 32}, {777, 1333, 129}};
+  struct Shape { int m, n, k; } shapes[] = {{4096, 4096, 4096}, {8192, 8192, 1024}, {16384, 16384, 64}, {12000, 12000, 6000}, {1000, 1000, 300}, {300, 5000, 32}, {777, 1333, 129},
+                                            {18000, 192, 64}, {192, 18000, 64}, {6000, 6000, 256}, {3000, 3000, 256}, {1500, 1500, 1000}, {18000, 256, 256}};
+  const int tiles_list[] = {64, 128, 129};
+  const char* names[] = {"valu64", "valu128", "mfma128"};
   hipStream_t st; CK(hipStreamCreate(&st));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (auto sh : shapes) {
@@ -25,17 +28,26 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(A, hA.data(), hA.size() * 8, hipMemcpyHostToDevice)); CK(hipMemcpy(B, hB.data(), hB.size() * 8, hipMemcpyHostToDevice));
     CK(hipMalloc(&dt, sizeof(GemmTask)));
     double res[3] = {0, 0, 0};
+    double ref_md = 0;
+    std::vector<double> ref(hC.size());
     for (int variant = 0; variant < 3; ++variant) {
-      int tile = variant == 0 ? 64 : (variant == 1 ? 128 : 129);
+      int tile = tiles_list[variant];
       double* C = variant == 0 ? C1 : C2;
       GemmTask t{}; t.A = A; t.B = B; t.C = C; t.m = m; t.n = n; t.k = k; t.lda = lda; t.ldb = ldb; t.ldc = ldc;
-      const int ts = tile == 129 ? 128 : tile;
-      t.tiles_m = (m + ts - 1) / ts; t.tile0 = 0;
-      int64_t tiles = (int64_t)t.tiles_m * ((n + ts - 1) / ts);
+      const int tsm = tile == 129 ? 128 : tile, tsn = tsm;
+      t.tiles_m = (m + tsm - 1) / tsm; t.tile0 = 0;
+      int64_t tiles = (int64_t)t.tiles_m * ((n + tsn - 1) / tsn);
       CK(hipMemcpy(dt, &t, sizeof t, hipMemcpyHostToDevice));
       CK(hipMemcpy(C, hC.data(), hC.size() * 8, hipMemcpyHostToDevice));
       CK(launch_gemm(st, tiles, dt, 1, tile));   // one correctness pass
       CK(hipStreamSynchronize(st));
+      {
+        std::vector<double> r(hC.size());
+        CK(hipMemcpy(r.data(), C, r.size() * 8, hipMemcpyDeviceToHost));
+        if (variant == 0) ref = r;
+        else if (tile != 129)
+          for (size_t o = 0; o < r.size(); ++o) ref_md = fmax(ref_md, fabs(r[o] - ref[o]));
+      }
       int reps = (double)m * n * k > 1e11 ? 3 : 20;
       CK(hipEventRecord(e0, st));
       for (int r = 0; r < reps; ++r) CK(launch_gemm(st, tiles, dt, 1, tile));
@@ -62,7 +74,9 @@ int main(int argc, char** argv) {
     for (int j = 0; j < n; ++j) for (int i = 0; i < m; ++i) { size_t o = (size_t)j * ldc + i; md = fmax(md, fabs(r1[o] - r2[o])); mx = fmax(mx, fabs(r1[o])); }
     bool pad_ok = true;  // rows >= m inside ld padding untouched
     for (int j = 0; j < n && pad_ok; ++j) for (int i = m; i < ldc; ++i) { size_t o = (size_t)j * ldc + i; if (r2[o] != hC[o]) pad_ok = false; }
-    printf("m=%6d n=%6d k=%6d  valu64 %6.2f TF  valu128 %6.2f TF  mfma128 %6.2f TF  maxdiff(valu,mfma) %.2e (rel %.2e) pad_ok %d\n", m, n, k, res[0], res[1], res[2], md, md / mx, pad_ok);
+    printf("m=%6d n=%6d k=%6d ", m, n, k);
+    for (int v = 0; v < 3; ++v) printf(" %s %6.2f", names[v], res[v]);
+    printf("  TF | valu-vs-valu maxdiff %.1e  valu-vs-mfma rel %.1e pad_ok %d\n", ref_md, md / mx, pad_ok);
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C1)); CK(hipFree(C2)); CK(hipFree(dt));
   }
   return 0;
