@@ -164,6 +164,15 @@ def main():
         upd = F.stat("upd")
         dense_flops = F.stat("dense_flops")
         achieved = gemm_flops / (ms_gemm * 1e-3) / 1e12 if ms_gemm > 0 else None
+        n_gemm = F.stat("gemm_launches")
+        avg_us = ms_gemm * 1e3 / n_gemm if n_gemm else None
+        traffic, traffic_src = None, "not collected"
+        pmc = os.path.join(ROOT, "profiles", "r01", f"pmc_gemm_{N}.json")
+        if os.path.exists(pmc):
+            with open(pmc) as fh:
+                pm = json.load(fh)
+            traffic = pm.get("hbm_bytes_per_launch")
+            traffic_src = os.path.relpath(pmc, ROOT)
         nnzA = A.nnz
         # SURVEY §8(d) algorithmic bytes of the scatter/gather formulation, for reference
         bytes_sg = 12 * upd + 12 * nnzA + 12 * nnzLU + 16 * (n + 1)
@@ -185,12 +194,18 @@ def main():
                        "n": n, "nnzA": int(nnzA), "nnzLU": nnzLU, "upd": upd,
                        "dense_flops": dense_flops, "ordering": args.ordering,
                        "parallelism": f"replicas{world}" if world > 1 else "single"},
-            "roofline": {"bound": "mfma", "kernel": "k_gemm (fp64 VALU Schur update)",
+            "roofline": {"bound": "mfma", "kernel": "k_gemm128/k_gemm (fp64 VALU Schur update)",
                          "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
-                         "traffic": None,
-                         "note": "fp64 dense peak (vector == matrix on gfx950); achieved = gemm "
-                                 "flops per refactor / summed k_gemm event time per refactor"},
+                         "traffic": traffic,
+                         "launches_per_step": n_gemm, "avg_launch_us": avg_us,
+                         "flops_per_launch": gemm_flops / n_gemm,
+                         "algorithmic_bytes_per_launch": F.stat("gemm_bytes") / n_gemm,
+                         "note": "fp64 VALU (v_fma_f64), no MFMA; peak = MI355X fp64 dense peak; "
+                                 "achieved = GEMM flops per refactor / HIP-event time of the GEMM "
+                                 "launches per refactor (graph-captured events on the launch "
+                                 "stream); traffic = HBM bytes per launch from rocprofv3 PMC "
+                                 "(FETCH_SIZE x2 + WRITE_SIZE, " + traffic_src + ")"},
             "kernel_ms_per_step": {k: v / K for k, v in kind_ms.items()},
             "gemm_split": {"panel_tflops": (gemm_flops - F.stat("gemm22_flops")) / max((kind_ms["gemm"] + kind_ms["gemmu"] + kind_ms["gemmo"]) / K, 1e-9) / 1e9,
                            "f22_tflops": F.stat("gemm22_flops") / max(kind_ms["gemm22"] / K, 1e-9) / 1e9,

@@ -15,6 +15,7 @@
 //   k_perm_in/k_perm_out/k_unswap             ldiv!'s scale+permute / un-permute (:318-339)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 
@@ -152,16 +153,47 @@ __global__ void k_extend_add(int64_t ntasks, const int2* __restrict__ tasks,
   const double* src = scratch + c.Foff + (int64_t)tk.y * nuc;
   const int32_t* rm = relmap + c.rowptr;
   const int64_t tj = rm[tk.y];
+  // 4 independent elements per lane in flight (memory-level parallelism for short columns)
   if (tj < P.ns) {
     gdbl* col = P.L + tj * P.M;
-    for (int64_t i = lane; i < nuc; i += 64) col[rm[i]] += src[i];
+    for (int64_t i0 = lane; i0 < nuc; i0 += 256) {
+      double v[4];
+      int32_t r[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + 64 * u;
+        v[u] = i < nuc ? src[i] : 0.0;
+        r[u] = i < nuc ? rm[i] : -1;
+      }
+      double c[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) c[u] = r[u] >= 0 ? col[r[u]] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (r[u] >= 0) col[r[u]] = c[u] + v[u];
+    }
   } else {
     gdbl* colU = P.U + (tj - P.ns) * P.ns;
     gdbl* colF = P.F + (tj - P.ns) * P.nu - P.ns;
-    for (int64_t i = lane; i < nuc; i += 64) {
-      int64_t ti = rm[i];
-      if (ti < P.ns) colU[ti] += src[i];
-      else colF[ti] += src[i];
+    for (int64_t i0 = lane; i0 < nuc; i0 += 256) {
+      double v[4];
+      int32_t r[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + 64 * u;
+        v[u] = i < nuc ? src[i] : 0.0;
+        r[u] = i < nuc ? rm[i] : -1;
+      }
+      gdbl* dst[4];
+      double c[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        dst[u] = r[u] < 0 ? nullptr : (r[u] < P.ns ? colU + r[u] : colF + r[u]);
+        c[u] = dst[u] ? *dst[u] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (dst[u]) *dst[u] = c[u] + v[u];
     }
   }
 }
@@ -1007,10 +1039,8 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
 #ifndef KK_UNROLL
 #define KK_UNROLL 2
 #endif
-__global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__ tasks, int ntask) {
-  __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
-  __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
-  const int64_t b = blockIdx.x;
+__device__ __forceinline__ void gemm128_tile(const GemmTask* __restrict__ tasks, int ntask, int64_t b,
+                                             double (&As)[2][HBK_][HBM_], double (&Bs)[2][HBK_][HLDB_]) {
   const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
   const gdbl* gA = gbl(t.A);
   const gdbl* gB = gbl(t.B);
@@ -1086,6 +1116,18 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__
       const int row = m0 + 2 * tx + 32 * (i >> 1) + (i & 1);
       if (row < t.m) Cc[row] = Cc[row] - acc[i][j];
     }
+  }
+}
+
+// Tiles b = blockIdx.x + i * gridDim.x: a grid smaller than the tile count leaves CUs free for
+// the latency-bound panel chain running concurrently on the other stream (look-ahead).
+__global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__ tasks, int ntask,
+                                                    int64_t ntiles) {
+  __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
+  __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
+  for (int64_t b = blockIdx.x; b < ntiles; b += gridDim.x) {
+    gemm128_tile(tasks, ntask, b, As, Bs);
+    __syncthreads();
   }
 }
 
@@ -1515,10 +1557,12 @@ hipError_t launch_trsm_u(hipStream_t st, int64_t nwg, const FrontTile* ft, int n
   k_trsm_u<64><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, OB, mode, sn, store, scratch, swaps, swap_stride);
   return hipGetLastError();
 }
-hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask, int tile) {
+hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask, int tile,
+                       int64_t maxwg) {
   if (ntiles <= 0) return hipSuccess;
   if (tile == 129) k_gemm128_mfma<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
-  else if (tile == 128) k_gemm128<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
+  else if (tile == 128)
+    k_gemm128<<<(unsigned)(maxwg > 0 ? std::min<int64_t>(ntiles, maxwg) : ntiles), 256, 0, st>>>(tasks, ntask, ntiles);
   else k_gemm<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
   return hipGetLastError();
 }

@@ -45,7 +45,7 @@ hipError_t launch_laswp(hipStream_t, int64_t, const SwapTask*, int, const SNode*
                         int64_t);
 hipError_t launch_trsm_u(hipStream_t, int64_t, const FrontTile*, int, int, int, const SNode*, double*,
                          double*, const int32_t*, int64_t);
-hipError_t launch_gemm(hipStream_t, int64_t, const GemmTask*, int, int);
+hipError_t launch_gemm(hipStream_t, int64_t, const GemmTask*, int, int, int64_t);
 hipError_t launch_fwd_gather(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                              const int32_t*, double*, double*);
 hipError_t launch_tri_block(hipStream_t, bool, int64_t, const FrontTile*, int, int, const SNode*,
@@ -144,6 +144,8 @@ struct smlu_handle {
   std::vector<Launch> fac, fwd, bwd;
   std::vector<SNode> hsn;
   double gemm_flops = 0, gemm22_flops = 0, dense_flops = 0;
+  int64_t gemm_launches = 0, gemm128_launches = 0;
+  double gemm_bytes = 0;      // algorithmic bytes of the GEMM launches: A, B read, C read + written
   int64_t nlaunch = 0;
   // stats
   double refactor_ms = 0, solve_ms = 0, growth_max = 0;
@@ -159,7 +161,8 @@ struct smlu_handle {
   bool lookahead = false;     // SMLU_LOOKAHEAD=1: trailing updates beyond the next block on a side stream
   int ob = kOBDefault;        // outer block width (SMLU_OB overrides; multiple of 64)
   int64_t t128_min = 128;     // 128x128 GEMM tiles when a launch has at least this many
-  int fast_trsm = 1;          // batched-LDS full-width triangular solves (SMLU_SLOW_TRSM=1: off)
+  int fast_trsm = 1;
+  int64_t side_wg = 0;        // grid cap of look-ahead GEMMs (SMLU_SIDE_WG; 0 = uncapped)          // batched-LDS full-width triangular solves (SMLU_SLOW_TRSM=1: off)
   ~smlu_handle() { release_all(); }
   void release_buffers() {
     if (stream) (void)hipSetDevice(device);
@@ -288,9 +291,12 @@ static int build_schedule(smlu_handle* h) {
   h->fac.clear();
   h->lookahead = std::getenv("SMLU_LOOKAHEAD") != nullptr;
   h->fast_trsm = std::getenv("SMLU_SLOW_TRSM") ? 0 : 1;
+  if (const char* e = std::getenv("SMLU_SIDE_WG")) h->side_wg = std::atoll(e);
   if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
   if (const char* e = std::getenv("SMLU_T128MIN")) h->t128_min = std::atoll(e);
   h->gemm_flops = 0;
+  h->gemm_launches = h->gemm128_launches = 0;
+  h->gemm_bytes = 0;
   h->gemm22_flops = 0;
   h->dense_flops = P.flops;
   int64_t max_list = 1;
@@ -312,6 +318,7 @@ static int build_schedule(smlu_handle* h) {
     int64_t tiles = 0;
     const int ts = tile == 129 ? 128 : tile;
     for (auto& g : cand) {
+      h->gemm_bytes += 8.0 * ((double)g.m * g.k + (double)g.k * g.n + 2.0 * g.m * g.n);
       g.tiles_m = (g.m + ts - 1) / ts;
       g.tile0 = tiles;
       tiles += (int64_t)g.tiles_m * ((g.n + ts - 1) / ts);
@@ -322,6 +329,8 @@ static int build_schedule(smlu_handle* h) {
     L.flops = fl;
     h->fac.push_back(L);
     h->gemm_flops += fl;
+    ++h->gemm_launches;
+    if (tile != 64) ++h->gemm128_launches;
     if (step < 0) h->gemm22_flops += fl;
   };
   for (int l = 0; l < P.nlevels; ++l) {
@@ -924,7 +933,7 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
     case K_GEMMU:
     case K_GEMMO:
     case K_GEMM22:
-      return launch_gemm(st, L.nwg, h->gtasks.p + L.off, (int)L.cnt, (int)L.aux);
+      return launch_gemm(st, L.nwg, h->gtasks.p + L.off, (int)L.cnt, (int)L.aux, L.side ? h->side_wg : 0);
   }
   return hipErrorInvalidValue;
 }
@@ -1425,6 +1434,9 @@ double smlu_stat(const smlu_handle* h, const char* key) {
   if (k == "weak") return (double)h->weak;
   if (k == "gemm_flops") return h->gemm_flops;
   if (k == "gemm22_flops") return h->gemm22_flops;
+  if (k == "gemm_launches") return (double)h->gemm_launches;
+  if (k == "gemm_bytes") return h->gemm_bytes;
+  if (k == "gemm128_launches") return (double)h->gemm128_launches;
   if (k.rfind("ms_", 0) == 0) {
     std::string name = k.substr(3);
     double t = 0;

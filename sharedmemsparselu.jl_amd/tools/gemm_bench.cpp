@@ -6,7 +6,7 @@
 #include <cstdlib>
 #include <vector>
 #include "../csrc/device.hpp"
-namespace smlu { hipError_t launch_gemm(hipStream_t, int64_t, const GemmTask*, int, int); }
+namespace smlu { hipError_t launch_gemm(hipStream_t, int64_t, const GemmTask*, int, int, int64_t); }
 using namespace smlu;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %s\n", hipGetErrorString(e), #x); exit(1);} } while (0)
 
@@ -39,7 +39,7 @@ int main(int argc, char** argv) {
       int64_t tiles = (int64_t)t.tiles_m * ((n + tsn - 1) / tsn);
       CK(hipMemcpy(dt, &t, sizeof t, hipMemcpyHostToDevice));
       CK(hipMemcpy(C, hC.data(), hC.size() * 8, hipMemcpyHostToDevice));
-      CK(launch_gemm(st, tiles, dt, 1, tile));   // one correctness pass
+      CK(launch_gemm(st, tiles, dt, 1, tile, 0));   // one correctness pass
       CK(hipStreamSynchronize(st));
       {
         std::vector<double> r(hC.size());
@@ -50,7 +50,7 @@ int main(int argc, char** argv) {
       }
       int reps = (double)m * n * k > 1e11 ? 3 : 20;
       CK(hipEventRecord(e0, st));
-      for (int r = 0; r < reps; ++r) CK(launch_gemm(st, tiles, dt, 1, tile));
+      for (int r = 0; r < reps; ++r) CK(launch_gemm(st, tiles, dt, 1, tile, 0));
       CK(hipEventRecord(e1, st)); CK(hipEventSynchronize(e1));
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       res[variant] = 2.0 * m * n * (double)k * reps / (ms * 1e-3) / 1e12;
@@ -65,7 +65,7 @@ int main(int argc, char** argv) {
       int64_t tiles = (int64_t)t.tiles_m * ((n + ts - 1) / ts);
       CK(hipMemcpy(dt, &t, sizeof t, hipMemcpyHostToDevice));
       CK(hipMemcpy(C, hC.data(), hC.size() * 8, hipMemcpyHostToDevice));
-      CK(launch_gemm(st, tiles, dt, 1, tile));
+      CK(launch_gemm(st, tiles, dt, 1, tile, 0));
       CK(hipStreamSynchronize(st));
     }
     std::vector<double> r1(hC.size()), r2(hC.size());

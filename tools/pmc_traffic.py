@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Summarise the PMC passes of tools/profile_pmc.sh into profiles/<round>/pmc_gemm_<N>.json.
+
+HBM bytes per the MI355X guide's HBM/rocprofv3 section: FETCH_SIZE and WRITE_SIZE are in KiB,
+collected in separate passes; on gfx950 FETCH_SIZE counts 1/2 of the bytes of wide reads, so
+it is doubled; WRITE_SIZE is taken as is.  Usage: pmc_traffic.py N ROUND_DIR
+"""
+import csv
+import json
+import os
+import re
+import sys
+
+N = int(sys.argv[1])
+out_dir = sys.argv[2]
+base = "gpurun_out"
+
+
+def load(counter):
+    path = os.path.join(base, f"pmc_{counter}_{N}", "pmc_counter_collection.csv")
+    per = {}
+    for r in csv.DictReader(open(path)):
+        name = r["Kernel_Name"].split("(")[0]
+        d = per.setdefault(name, [0, 0.0])
+        d[0] += 1
+        d[1] += float(r["Counter_Value"])
+    return per
+
+
+def factor_stats():
+    txt = open(os.path.join(base, f"pmc_FETCH_SIZE_{N}.log")).read()
+    m = re.search(r"gemm_launches=(\d+) gemm_bytes=([\d.e+]+) gemm_flops=([\d.e+]+)", txt)
+    return int(m.group(1)), float(m.group(2)), float(m.group(3))
+
+
+fetch, write = load("FETCH_SIZE"), load("WRITE_SIZE")
+launches, alg_bytes, flops = factor_stats()
+n = sum(v[0] for v in fetch.values())
+fkb = sum(v[1] for v in fetch.values())
+wkb = sum(v[1] for v in write.values())
+hbm = 2.0 * fkb * 1024 + wkb * 1024
+res = {
+    "workload": f"3D Poisson {N}^3, one numeric factorization (eager launches)",
+    "kernels": {k: {"launches": fetch[k][0], "fetch_kib_raw": fetch[k][1],
+                    "write_kib_raw": write.get(k, [0, 0.0])[1]} for k in fetch},
+    "launches": n, "launches_expected": launches,
+    "fetch_kib_raw": fkb, "write_kib_raw": wkb,
+    "hbm_bytes_total": hbm, "hbm_bytes_per_launch": hbm / n,
+    "algorithmic_bytes_total": alg_bytes, "algorithmic_bytes_per_launch": alg_bytes / launches,
+    "traffic_over_algorithmic": hbm / alg_bytes,
+    "gemm_flops": flops,
+    "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), KiB -> bytes; WRITE_SIZE as is",
+}
+os.makedirs(out_dir, exist_ok=True)
+with open(os.path.join(out_dir, f"pmc_gemm_{N}.json"), "w") as fh:
+    json.dump(res, fh, indent=1)
+print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
