@@ -42,6 +42,14 @@ struct FrontTile {
   int64_t wg0;
 };
 
+// Extend-add task: parent front p's column tj receives cnt child columns, listed as (child,
+// child column) pairs at contrib[off, off+cnt) in child order.
+struct XCol {
+  int32_t p, tj;
+  int64_t off;
+  int32_t cnt, pad;
+};
+
 // Row swaps of one or more consecutive panels (sub-panels kb0 + u*nb, swap-list slots slot0 + u,
 // u < nsub) applied in order to the front columns [a, b) minus [c_lo, c_hi); 64 columns per
 // workgroup, workgroups numbered from wg0 within one launch (tasks sorted by wg0).

@@ -134,66 +134,69 @@ __global__ void k_scatterA(int64_t cnt, const int32_t* __restrict__ ents,
 }
 
 // ------------------------------------------------------------------------------------
-// Front assembly, part 2 (extend-add): child F22 column j -> parent front, one wave per
-// (child, column).  Rows of a child column map monotonically into the parent column.
-// Siblings run in separate passes (no two children of one parent in the same launch), so
-// the adds are race-free and the summation order is fixed (bitwise reproducible).
+// Front assembly, part 2 (extend-add): one wave per parent column; it adds the contributing
+// child F22 columns one after the other in child order (deterministic, no atomics, one
+// launch per level).  4 independent elements per lane in flight.
 // ------------------------------------------------------------------------------------
-__global__ void k_extend_add(int64_t ntasks, const int2* __restrict__ tasks,
-                             const SNode* __restrict__ sn, const int32_t* __restrict__ relmap,
-                             double* __restrict__ store, double* __restrict__ scratch) {
-  int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  int lane = threadIdx.x & 63;
+__global__ void k_extend_add(int64_t ntasks, const XCol* __restrict__ cols,
+                             const int2* __restrict__ contrib, const SNode* __restrict__ sn,
+                             const int32_t* __restrict__ relmap, double* __restrict__ store,
+                             double* __restrict__ scratch) {
+  const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
   if (w >= ntasks) return;
-  int2 tk = tasks[w];
-  const SNode c = sn[tk.x];
-  const SNode p = sn[c.parent];
+  const XCol t = cols[w];
+  const SNode p = sn[t.p];
   FrontPtrs P = front_ptrs(p, store, scratch);
-  const int64_t nuc = c.nu;
-  const double* src = scratch + c.Foff + (int64_t)tk.y * nuc;
-  const int32_t* rm = relmap + c.rowptr;
-  const int64_t tj = rm[tk.y];
-  // 4 independent elements per lane in flight (memory-level parallelism for short columns)
-  if (tj < P.ns) {
-    gdbl* col = P.L + tj * P.M;
-    for (int64_t i0 = lane; i0 < nuc; i0 += 256) {
-      double v[4];
-      int32_t r[4];
+  const int64_t tj = t.tj;
+  for (int q = 0; q < t.cnt; ++q) {
+    if (q > 0) __threadfence_block();   // the previous child's stores before this child's loads
+    const int2 ck = contrib[t.off + q];
+    const SNode c = sn[ck.x];
+    const int64_t nuc = c.nu;
+    const double* src = scratch + c.Foff + (int64_t)ck.y * nuc;
+    const int32_t* rm = relmap + c.rowptr;
+    if (tj < P.ns) {
+      gdbl* col = P.L + tj * P.M;
+      for (int64_t i0 = lane; i0 < nuc; i0 += 256) {
+        double v[4];
+        int32_t r[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t i = i0 + 64 * u;
-        v[u] = i < nuc ? src[i] : 0.0;
-        r[u] = i < nuc ? rm[i] : -1;
+        for (int u = 0; u < 4; ++u) {
+          const int64_t i = i0 + 64 * u;
+          v[u] = i < nuc ? src[i] : 0.0;
+          r[u] = i < nuc ? rm[i] : -1;
+        }
+        double cv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) cv[u] = r[u] >= 0 ? col[r[u]] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (r[u] >= 0) col[r[u]] = cv[u] + v[u];
       }
-      double c[4];
+    } else {
+      gdbl* colU = P.U + (tj - P.ns) * P.ns;
+      gdbl* colF = P.F + (tj - P.ns) * P.nu - P.ns;
+      for (int64_t i0 = lane; i0 < nuc; i0 += 256) {
+        double v[4];
+        int32_t r[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) c[u] = r[u] >= 0 ? col[r[u]] : 0.0;
+        for (int u = 0; u < 4; ++u) {
+          const int64_t i = i0 + 64 * u;
+          v[u] = i < nuc ? src[i] : 0.0;
+          r[u] = i < nuc ? rm[i] : -1;
+        }
+        gdbl* dst[4];
+        double cv[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (r[u] >= 0) col[r[u]] = c[u] + v[u];
-    }
-  } else {
-    gdbl* colU = P.U + (tj - P.ns) * P.ns;
-    gdbl* colF = P.F + (tj - P.ns) * P.nu - P.ns;
-    for (int64_t i0 = lane; i0 < nuc; i0 += 256) {
-      double v[4];
-      int32_t r[4];
+        for (int u = 0; u < 4; ++u) {
+          dst[u] = r[u] < 0 ? nullptr : (r[u] < P.ns ? colU + r[u] : colF + r[u]);
+          cv[u] = dst[u] ? *dst[u] : 0.0;
+        }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t i = i0 + 64 * u;
-        v[u] = i < nuc ? src[i] : 0.0;
-        r[u] = i < nuc ? rm[i] : -1;
+        for (int u = 0; u < 4; ++u)
+          if (dst[u]) *dst[u] = cv[u] + v[u];
       }
-      gdbl* dst[4];
-      double c[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        dst[u] = r[u] < 0 ? nullptr : (r[u] < P.ns ? colU + r[u] : colF + r[u]);
-        c[u] = dst[u] ? *dst[u] : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (dst[u]) *dst[u] = c[u] + v[u];
     }
   }
 }
@@ -698,36 +701,43 @@ __device__ __forceinline__ int find_front_tile(const FrontTile* __restrict__ ft,
 // the guarded generic loops: results are bitwise identical.
 template <int W, int LD = W, int XN = W>
 __device__ __forceinline__ void lower_unit_solve_fast(double (&x)[XN], const double* __restrict__ sT) {
+  // reads of one step in batches of at most 32 (keeps the kernel within 256 registers so that
+  // it can share a SIMD with a resident GEMM wave)
 #pragma unroll
   for (int j = 0; j < W - 1; ++j) {
-    double lc[W];
 #pragma unroll
-    for (int i = j + 1; i < W; ++i) lc[i] = sT[j * LD + i];
-    __builtin_amdgcn_sched_barrier(0);
-    const double xj = x[j];
+    for (int i0 = j + 1; i0 < W; i0 += 32) {
+      double lc[32];
 #pragma unroll
-    for (int i = j + 1; i < W; ++i) x[i] = fma(-lc[i], xj, x[i]);
-    __builtin_amdgcn_sched_barrier(0);
+      for (int i = i0; i < W && i < i0 + 32; ++i) lc[i - i0] = sT[j * LD + i];
+      __builtin_amdgcn_sched_barrier(0);
+      const double xj = x[j];
+#pragma unroll
+      for (int i = i0; i < W && i < i0 + 32; ++i) x[i] = fma(-lc[i - i0], xj, x[i]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 }
 
 // x <- x U^{-1} for a row vector x, U = sT (stored [col][row]), rd = 1/diag(U); returns max |x|
-template <int W>
-__device__ __forceinline__ double upper_right_solve_fast(double (&x)[W], const double* __restrict__ sT,
+template <int W, int LD = W, int XN = W>
+__device__ __forceinline__ double upper_right_solve_fast(double (&x)[XN], const double* __restrict__ sT,
                                                          const double* __restrict__ rd) {
   double gmax = 0.0;
 #pragma unroll
   for (int j = 0; j < W; ++j) {
-    double uc[W];
-    const double r = rd[j];
-#pragma unroll
-    for (int k = j + 1; k < W; ++k) uc[k] = sT[k * W + j];
-    __builtin_amdgcn_sched_barrier(0);
-    x[j] = x[j] * r;
+    x[j] = x[j] * rd[j];
     gmax = fmax(gmax, fabs(x[j]));
 #pragma unroll
-    for (int k = j + 1; k < W; ++k) x[k] = fma(-x[j], uc[k], x[k]);
-    __builtin_amdgcn_sched_barrier(0);
+    for (int k0 = j + 1; k0 < W; k0 += 32) {
+      double uc[32];
+#pragma unroll
+      for (int k = k0; k < W && k < k0 + 32; ++k) uc[k - k0] = sT[k * LD + j];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = k0; k < W && k < k0 + 32; ++k) x[k] = fma(-x[j], uc[k - k0], x[k]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
   return gmax;
 }
@@ -772,7 +782,7 @@ __global__ __launch_bounds__(256) void k_trsm_u(const FrontTile* __restrict__ ft
   if (col >= M) return;
   gdbl* cp = fel(f, kb, col);
   double x[W];
-  if (w == W && (mode & 2)) {
+  if (w == W) {
 #pragma unroll
     for (int j = 0; j < W; ++j) x[j] = cp[j];
     lower_unit_solve_fast<W>(x, sT);
@@ -780,7 +790,7 @@ __global__ __launch_bounds__(256) void k_trsm_u(const FrontTile* __restrict__ ft
     for (int j = 0; j < W; ++j) cp[j] = x[j];
     return;
   }
-  if (W == 64 && w == 32 && (mode & 2)) {   // 32-wide panels (mode 1 fronts)
+  if (W == 64 && w == 32) {   // 32-wide panels (mode 1 fronts)
 #pragma unroll
     for (int j = 0; j < 32; ++j) x[j] = cp[j];
     lower_unit_solve_fast<32, W>(x, sT);
@@ -820,8 +830,7 @@ __global__ __launch_bounds__(256) void k_step_trsm(const FrontTile* __restrict__
                                                    double* __restrict__ store,
                                                    double* __restrict__ scratch,
                                                    int32_t* __restrict__ info,
-                                                   double* __restrict__ growth, double piv_tol,
-                                                   int fast) {
+                                                   double* __restrict__ growth, double piv_tol) {
   __shared__ double sT[W * W];   // L_kk (role U) or U_kk (role L), [col][row]
   __shared__ double s_rd[W];     // 1 / diag(U_kk) (role L)
   __shared__ double s_red[4];
@@ -845,7 +854,7 @@ __global__ __launch_bounds__(256) void k_step_trsm(const FrontTile* __restrict__
     }
     __syncthreads();
     const int64_t col = kb + w + tile * 256 + tid;
-    if (col < oend && w == W && fast) {
+    if (col < oend && w == W) {
       gdbl* cp = fel(f, kb, col);
       double x[W];
 #pragma unroll
@@ -897,7 +906,7 @@ __global__ __launch_bounds__(256) void k_step_trsm(const FrontTile* __restrict__
   __syncthreads();
   const int64_t row = r0 + tile * 256 + tid;
   double gmax = 0.0;
-  if (row < M && w == W && fast) {
+  if (row < M && w == W) {
     double x[W];
 #pragma unroll
     for (int j = 0; j < W; ++j) x[j] = P[(int64_t)j * M + row];
@@ -996,7 +1005,7 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload((kt + 1) * GBK);
-#pragma unroll
+#pragma unroll 4
     for (int kk = 0; kk < GBK; ++kk) {
       double a[4], bb[4];
 #pragma unroll
@@ -1497,10 +1506,10 @@ hipError_t launch_scatterA(hipStream_t st, int64_t cnt, const int32_t* ents, con
   k_scatterA<<<nblk(cnt, 256), 256, 0, st>>>(cnt, ents, dest, arow, a, Rs, store, scratch);
   return hipGetLastError();
 }
-hipError_t launch_extend_add(hipStream_t st, int64_t ntasks, const int2* tasks, const SNode* sn,
-                             const int32_t* relmap, double* store, double* scratch) {
+hipError_t launch_extend_add(hipStream_t st, int64_t ntasks, const XCol* cols, const int2* contrib,
+                             const SNode* sn, const int32_t* relmap, double* store, double* scratch) {
   if (ntasks <= 0) return hipSuccess;
-  k_extend_add<<<nblk(ntasks * 64, 256), 256, 0, st>>>(ntasks, tasks, sn, relmap, store, scratch);
+  k_extend_add<<<nblk(ntasks * 64, 256), 256, 0, st>>>(ntasks, cols, contrib, sn, relmap, store, scratch);
   return hipGetLastError();
 }
 hipError_t launch_front_lds(hipStream_t st, int cnt, int Mmax, const int32_t* list, const SNode* sn,
@@ -1539,15 +1548,14 @@ hipError_t launch_laswp(hipStream_t st, int64_t nwg, const SwapTask* tasks, int 
 }
 hipError_t launch_step_trsm(hipStream_t st, int W, const FrontTile* ftU, int nftU, int64_t nU,
                             const FrontTile* ftL, int nftL, int64_t nL, int step, int OB, const SNode* sn,
-                            double* store, double* scratch, int32_t* info, double* growth, double piv_tol,
-                            int fast) {
+                            double* store, double* scratch, int32_t* info, double* growth, double piv_tol) {
   if (nU + nL <= 0) return hipSuccess;
   if (W <= 32)
     k_step_trsm<32><<<(unsigned)(nU + nL), 256, 0, st>>>(ftU, nftU, nU, ftL, nftL, step, OB, sn, store,
-                                                         scratch, info, growth, piv_tol, fast);
+                                                         scratch, info, growth, piv_tol);
   else
     k_step_trsm<64><<<(unsigned)(nU + nL), 256, 0, st>>>(ftU, nftU, nU, ftL, nftL, step, OB, sn, store,
-                                                         scratch, info, growth, piv_tol, fast);
+                                                         scratch, info, growth, piv_tol);
   return hipGetLastError();
 }
 hipError_t launch_trsm_u(hipStream_t st, int64_t nwg, const FrontTile* ft, int nft, int OB, int mode,

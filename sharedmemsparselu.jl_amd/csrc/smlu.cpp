@@ -32,15 +32,15 @@ hipError_t launch_rowscale(hipStream_t, int64_t, const int64_t*, const int32_t*,
 hipError_t launch_fill(hipStream_t, int64_t, double*, double);
 hipError_t launch_scatterA(hipStream_t, int64_t, const int32_t*, const int64_t*, const int32_t*,
                            const double*, const double*, double*, double*);
-hipError_t launch_extend_add(hipStream_t, int64_t, const int2*, const SNode*, const int32_t*, double*,
-                             double*);
+hipError_t launch_extend_add(hipStream_t, int64_t, const XCol*, const int2*, const SNode*, const int32_t*,
+                             double*, double*);
 hipError_t launch_front_lds(hipStream_t, int, int, const int32_t*, const SNode*, double*, double*,
                             int32_t*, int32_t*, double*, double, double);
 hipError_t init_kernel_attributes();
 hipError_t launch_panel1(hipStream_t, int, int, int, int, int, const int32_t*, const SNode*, double*, double*,
                          int32_t*, int32_t*, int64_t, int32_t*, double*, double);
 hipError_t launch_step_trsm(hipStream_t, int, const FrontTile*, int, int64_t, const FrontTile*, int, int64_t,
-                            int, int, const SNode*, double*, double*, int32_t*, double*, double, int);
+                            int, int, const SNode*, double*, double*, int32_t*, double*, double);
 hipError_t launch_laswp(hipStream_t, int64_t, const SwapTask*, int, const SNode*, double*, double*, const int32_t*,
                         int64_t);
 hipError_t launch_trsm_u(hipStream_t, int64_t, const FrontTile*, int, int, int, const SNode*, double*,
@@ -140,6 +140,7 @@ struct smlu_handle {
   DBuf<FrontTile> ftiles;
   DBuf<GemmTask> gtasks;
   DBuf<SwapTask> stasks;
+  DBuf<XCol> xcols;
   // schedule
   std::vector<Launch> fac, fwd, bwd;
   std::vector<SNode> hsn;
@@ -161,7 +162,6 @@ struct smlu_handle {
   bool lookahead = false;     // SMLU_LOOKAHEAD=1: trailing updates beyond the next block on a side stream
   int ob = kOBDefault;        // outer block width (SMLU_OB overrides; multiple of 64)
   int64_t t128_min = 128;     // 128x128 GEMM tiles when a launch has at least this many
-  int fast_trsm = 1;
   int64_t side_wg = 0;        // grid cap of look-ahead GEMMs (SMLU_SIDE_WG; 0 = uncapped)          // batched-LDS full-width triangular solves (SMLU_SLOW_TRSM=1: off)
   ~smlu_handle() { release_all(); }
   void release_buffers() {
@@ -178,6 +178,7 @@ struct smlu_handle {
     ftiles.free();
     gtasks.free();
     stasks.free();
+    xcols.free();
   }
   void release_graphs() {
     if (fac_exec) (void)hipGraphExecDestroy(fac_exec);
@@ -286,11 +287,11 @@ static int build_schedule(smlu_handle* h) {
   std::vector<FrontTile> ft;
   std::vector<GemmTask> gt;
   std::vector<SwapTask> st_tasks;
+  std::vector<XCol> xc;
   double* store = h->store.p;
   double* scratch = h->scratch.p;
   h->fac.clear();
   h->lookahead = std::getenv("SMLU_LOOKAHEAD") != nullptr;
-  h->fast_trsm = std::getenv("SMLU_SLOW_TRSM") ? 0 : 1;
   if (const char* e = std::getenv("SMLU_SIDE_WG")) h->side_wg = std::atoll(e);
   if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
   if (const char* e = std::getenv("SMLU_T128MIN")) h->t128_min = std::atoll(e);
@@ -354,23 +355,37 @@ static int build_schedule(smlu_handle* h) {
     L.off = P.Alev_ptr[l];
     L.cnt = P.Alev_ptr[l + 1] - P.Alev_ptr[l];
     if (L.cnt > 0) h->fac.push_back(L);
-    // extend-add passes by child rank
-    int maxrank = -1;
-    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
-      int64_t s = P.lev_sup[k];
-      maxrank = std::max<int>(maxrank, (int)(P.ch_ptr[s + 1] - P.ch_ptr[s]) - 1);
-    }
-    for (int r = 0; r <= maxrank; ++r) {
+    // extend-add: one task per (parent, target column) with its contributing child columns
+    // in child order (counting sort by target column per parent)
+    {
       L = Launch();
       L.kind = K_EXTADD;
-      L.off = (int64_t)xt.size();
+      L.off = (int64_t)xc.size();
+      std::vector<int32_t> cnt, pos;
       for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
         int64_t s = P.lev_sup[k];
-        if (P.ch_ptr[s] + r >= P.ch_ptr[s + 1]) continue;
-        int64_t c = P.ch_list[P.ch_ptr[s] + r];
-        for (int64_t j = 0; j < P.nu(c); ++j) xt.push_back(make_int2((int)c, (int)j));
+        if (P.ch_ptr[s] == P.ch_ptr[s + 1]) continue;
+        const int64_t M = P.M(s);
+        cnt.assign(M + 1, 0);
+        for (int64_t ci = P.ch_ptr[s]; ci < P.ch_ptr[s + 1]; ++ci) {
+          const int64_t c = P.ch_list[ci];
+          const int32_t* rm = P.relmap.data() + h->hsn[c].rowptr;
+          for (int64_t jc = 0; jc < P.nu(c); ++jc) ++cnt[rm[jc] + 1];
+        }
+        for (int64_t tj = 0; tj < M; ++tj) cnt[tj + 1] += cnt[tj];
+        const int64_t base = (int64_t)xt.size();
+        xt.resize(base + cnt[M]);
+        pos.assign(cnt.begin(), cnt.end() - 1);
+        for (int64_t ci = P.ch_ptr[s]; ci < P.ch_ptr[s + 1]; ++ci) {
+          const int64_t c = P.ch_list[ci];
+          const int32_t* rm = P.relmap.data() + h->hsn[c].rowptr;
+          for (int64_t jc = 0; jc < P.nu(c); ++jc) xt[base + pos[rm[jc]]++] = make_int2((int)c, (int)jc);
+        }
+        for (int64_t tj = 0; tj < M; ++tj)
+          if (cnt[tj + 1] > cnt[tj])
+            xc.push_back(XCol{(int32_t)s, (int32_t)tj, base + cnt[tj], cnt[tj + 1] - cnt[tj], 0});
       }
-      L.cnt = (int64_t)xt.size() - L.off;
+      L.cnt = (int64_t)xc.size() - L.off;
       if (L.cnt > 0) h->fac.push_back(L);
     }
     // small fronts, launched per size class so that small fronts get small LDS (occupancy)
@@ -785,6 +800,7 @@ static int build_schedule(smlu_handle* h) {
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
   HIPCHK(h->gtasks.upload(gt.data(), gt.size(), st));
   HIPCHK(h->stasks.upload(st_tasks.data(), st_tasks.size(), st));
+  HIPCHK(h->xcols.upload(xc.data(), xc.size(), st));
   HIPCHK(h->swaps.alloc((size_t)max_list * kSwapStride));
   HIPCHK(h->vbuf.alloc((size_t)std::max<int64_t>(voff, 1)));
   HIPCHK(hipStreamSynchronize(st));
@@ -909,15 +925,15 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
       return launch_scatterA(st, L.cnt, h->Alev_ent.p + L.off, h->Adest.p, h->Arow.p, h->A.p, h->Rs.p,
                              h->store.p, h->scratch.p);
     case K_EXTADD:
-      return launch_extend_add(st, L.cnt, h->xtasks.p + L.off, h->sn.p, h->relmap.p, h->store.p,
-                               h->scratch.p);
+      return launch_extend_add(st, L.cnt, h->xcols.p + L.off, h->xtasks.p, h->sn.p, h->relmap.p,
+                               h->store.p, h->scratch.p);
     case K_FRONT_LDS:
       return launch_front_lds(st, (int)L.cnt, (int)L.aux, h->ilist.p + L.off, h->sn.p, h->store.p,
                               h->scratch.p, h->rowperm.p, h->info.p, h->growth.p, diag_tol, piv_tol);
     case K_STEPTRSM:
       return launch_step_trsm(st, (int)L.aux, h->ftiles.p + L.off, (int)L.cnt, L.nwg, h->ftiles.p + L.off2,
                               (int)L.cnt2, L.nwg2, L.step, h->ob, h->sn.p, h->store.p, h->scratch.p, h->info.p,
-                              h->growth.p, piv_tol, h->fast_trsm);
+                              h->growth.p, piv_tol);
     case K_LASWP:
       return launch_laswp(st, L.nwg, h->stasks.p + L.off, (int)L.cnt, h->sn.p, h->store.p, h->scratch.p,
                           h->swaps.p, kSwapStride);
@@ -927,7 +943,7 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
                           h->store.p, h->scratch.p, h->rowperm.p, h->swaps.p, kSwapStride, h->info.p,
                           h->growth.p, diag_tol);
     case K_TRSMU:
-      return launch_trsm_u(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->ob, (int)L.aux | (h->fast_trsm << 1), h->sn.p,
+      return launch_trsm_u(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->ob, (int)L.aux, h->sn.p,
                            h->store.p, h->scratch.p, h->swaps.p, kSwapStride);
     case K_GEMM:
     case K_GEMMU:

@@ -11,7 +11,7 @@
 #include "../csrc/device.hpp"
 namespace smlu {
 hipError_t launch_step_trsm(hipStream_t, int, const FrontTile*, int, int64_t, const FrontTile*, int, int64_t,
-                            int, int, const SNode*, double*, double*, int32_t*, double*, double, int);
+                            int, int, const SNode*, double*, double*, int32_t*, double*, double);
 hipError_t launch_trsm_u(hipStream_t, int64_t, const FrontTile*, int, int, int, const SNode*, double*,
                          double*, const int32_t*, int64_t);
 hipError_t launch_panel1(hipStream_t, int, int, int, int, int, const int32_t*, const SNode*, double*, double*,
@@ -73,10 +73,10 @@ int main() {
   for (int fast = 0; fast < 2; ++fast) {
     double* d = fast ? d1 : d0;
     CK(hipMemcpy(d, h.data(), h.size() * 8, hipMemcpyHostToDevice));
-    CK(launch_step_trsm(st, 64, dft, 1, nUw, dft + 1, 1, nLw, 0, OB, dsn, d, sc, info, growth, 0.1, fast));
+    CK(launch_step_trsm(st, 64, dft, 1, nUw, dft + 1, 1, nLw, 0, OB, dsn, d, sc, info, growth, 0.1));
     CK(hipStreamSynchronize(st));
     CK(hipMemcpy(r[fast].data(), d, h.size() * 8, hipMemcpyDeviceToHost));
-    t_s[fast] = timeit([&] { (void)launch_step_trsm(st, 64, dft, 1, nUw, dft + 1, 1, nLw, 0, OB, dsn, d, sc, info, growth, 0.1, fast); }, 20);
+    t_s[fast] = timeit([&] { (void)launch_step_trsm(st, 64, dft, 1, nUw, dft + 1, 1, nLw, 0, OB, dsn, d, sc, info, growth, 0.1); }, 20);
   }
   printf("step_trsm (U 192 cols + L %lld rows, %lld WGs): generic %7.1f us  fast %7.1f us  bitwise %s\n",
          (long long)(M - nb), (long long)(nUw + nLw), t_s[0], t_s[1],
