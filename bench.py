@@ -86,11 +86,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=128, help="grid side of the 3D Poisson workload")
+    ap.add_argument("--side", "--n", dest="n", type=int, default=128,
+                    help="grid side of the 3D Poisson workload")
     ap.add_argument("--ordering", default="nd", choices=["nd", "geometric"])
     ap.add_argument("--cpu-n", type=int, default=32, help="grid side of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
+    ap.add_argument("--test-one-gpu", action="store_true",
+                    help="rehearsal: all ranks on cuda:0, gloo transport (never for measurements)")
+    ap.add_argument("--replicas", action="store_true",
+                    help="N > 1: independent replicas instead of the partitioned factorization")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -98,10 +103,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    if args.test_one_gpu:
+        local = 0
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        if args.test_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     else:
         torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
@@ -114,12 +124,18 @@ def main():
     n = A.shape[0]
     log(f"rank {rank}: generated 3D Poisson {N}^3 n={n} nnz={A.nnz} in {time.perf_counter()-t0:.1f}s")
     grid = (N, N, N) if args.ordering == "geometric" else None
+    partitioned = world > 1 and not args.replicas
     t0 = time.perf_counter()
-    F = smlu.ParallelSparseLU(A, grid=grid, device=local, profile=not args.no_profile)
+    if partitioned:   # one factorization split over the ranks (subtrees + RCCL exchanges)
+        F = smlu.DistributedSparseLU(A, device=local, ordering=args.ordering,
+                                     **({"grid": grid} if grid else {}))
+    else:
+        F = smlu.ParallelSparseLU(A, grid=grid, device=local, profile=not args.no_profile)
     t_create = time.perf_counter() - t0
     nnzLU = F.stat("nnzLU")
     log(f"rank {rank}: analysis {F.stat('analysis_ms')/1e3:.1f}s, create+first factor {t_create:.1f}s, "
-        f"nnz(L+U)={nnzLU:.4g}, upd={F.stat('upd'):.4g}, launches={F.stat('launches'):.0f}")
+        f"nnz(L+U)={nnzLU:.4g}, upd={F.stat('upd'):.4g}, launches={F.stat('launches'):.0f}"
+        + (f", segments={F.nseg}" if partitioned else ""))
 
     # C5 inputs: same pattern, new values (diag += U(0,1) from default_rng(47+r)), uploaded to HBM
     dpos = torch.from_numpy(mats.diag_positions(A)).to(dev)
@@ -137,16 +153,16 @@ def main():
 
     def step(r):
         F.refactor_device(vals[r])
-        if r >= args.warmup:
+        if r >= args.warmup and not partitioned:
             for k in kinds:
                 kind_ms[k] += F.stat("ms_" + k)
         log(f"rank {rank}: {'warmup' if r < args.warmup else 'step'} {r} refactor "
             f"{F.stat('refactor_ms_last'):.1f} ms")
 
     dt = timed_region(step, args.steps, args.warmup, torch.cuda.synchronize,
-                      dev if world > 1 else None)
+                      dev if world > 1 and not args.test_one_gpu else None)
     # one solve (reported, not the metric)
-    b = torch.rand(n, dtype=torch.float64, device=dev)
+    b = torch.from_numpy(np.random.default_rng(5).random(n)).to(dev)   # same b on every rank
     x = torch.empty_like(b)
     F.solve_device(x, b)
     torch.cuda.synchronize()
@@ -154,7 +170,11 @@ def main():
     F.solve_device(x, b)
     torch.cuda.synchronize()
     solve_ms = (time.perf_counter() - t1) * 1e3
-    # residual check of the solve on the last refactored values
+    # residual of that solve on the last refactored values (host SpMV)
+    Al = A.copy()
+    Al.data = vals[-1].cpu().numpy()
+    xh, bh = x.cpu().numpy(), b.cpu().numpy()
+    solve_residual = float(np.abs(Al @ xh - bh).max() / np.abs(bh).max())
     ms_per_step = dt / args.steps * 1e3
 
     if rank == 0:
@@ -178,14 +198,14 @@ def main():
         bytes_sg = 12 * upd + 12 * nnzA + 12 * nnzLU + 16 * (n + 1)
         res = {
             "metric": "nnz(L+U)/s + achieved HBM GB/s, 3D Poisson 128³ numeric LU, 1/2/4/8 GPU",
-            "value": nnzLU * world / (ms_per_step * 1e-3),
+            "value": nnzLU * (1 if partitioned else world) / (ms_per_step * 1e-3),
             "unit": "nnz(L+U)/s",
             "n_gpus": world,
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if partitioned else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
@@ -193,14 +213,15 @@ def main():
                                    f"new diagonal values per step, values resident in HBM)",
                        "n": n, "nnzA": int(nnzA), "nnzLU": nnzLU, "upd": upd,
                        "dense_flops": dense_flops, "ordering": args.ordering,
-                       "parallelism": f"replicas{world}" if world > 1 else "single"},
+                       "parallelism": (f"tree-partition{world} (proportional mapping, RCCL p2p)"
+                                       if partitioned else f"replicas{world}" if world > 1 else "single")},
             "roofline": {"bound": "mfma", "kernel": "k_gemm128/k_gemm (fp64 VALU Schur update)",
                          "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic,
                          "launches_per_step": n_gemm, "avg_launch_us": avg_us,
-                         "flops_per_launch": gemm_flops / n_gemm,
-                         "algorithmic_bytes_per_launch": F.stat("gemm_bytes") / n_gemm,
+                         "flops_per_launch": gemm_flops / n_gemm if n_gemm else None,
+                         "algorithmic_bytes_per_launch": F.stat("gemm_bytes") / n_gemm if n_gemm else None,
                          "note": "fp64 VALU (v_fma_f64), no MFMA; peak = MI355X fp64 dense peak; "
                                  "achieved = GEMM flops per refactor / HIP-event time of the GEMM "
                                  "launches per refactor (graph-captured events on the launch "
@@ -214,9 +235,10 @@ def main():
             "refactor_tflops": dense_flops / (ms_per_step * 1e-3) / 1e12,
             "scatter_gather_equiv_GBs": bytes_sg / (ms_per_step * 1e-3) / 1e9,
             "solve_ms": solve_ms,
+            "solve_residual": solve_residual,
             "create_s": t_create,
         }
-        if not args.no_cpu:
+        if not args.no_cpu and world == 1:
             log("cpu baseline ...")
             res["cpu_baseline"] = cpu_baseline(args.cpu_n, args.ordering, args.ordering == "geometric")
         print(json.dumps(res), flush=True)

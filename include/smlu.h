@@ -147,6 +147,38 @@ int  smlu_plan_pattern(const smlu_plan* plan, int64_t* q, int64_t* Lcolptr, int6
 int  smlu_plan_supernodes(const smlu_plan* plan, int64_t* first, int64_t* parent, int64_t* level);
 void smlu_plan_destroy(smlu_plan* plan);
 
+/* ---- multi-GPU partition ---------------------------------------------------
+ * One process per GPU.  The assembly tree is split by proportional mapping: each rank factors
+ * its subtrees with no communication; a front whose child lives on another rank receives that
+ * child's update block right before its level ("exchange point").  The library runs the
+ * segments between exchange points on its own stream; the caller moves the packed blocks
+ * between ranks (RCCL point-to-point over xGMI in the Python mirror, smlu/dist.py).  This
+ * replaces the reference's MPI shared-memory column split (src/SharedMemSparseLU.jl:101-160
+ * distributes dense chunks over ranks).
+ *
+ * Factor:  smlu_dist_set_values; for seg in 0..nseg-1: (seg > 0: exchange kind 0 before seg)
+ *          smlu_dist_factor_segment(seg).  The last segment returns the pivot status.
+ * Solve:   forward  segments (phase 0, exchange kind 1 before seg > 0; seg 0 reads b),
+ *          backward segments (phase 1, exchange kind 2 before seg > 0),
+ *          phase 2 writes this rank's rows of x (others 0); the caller sums x over ranks.
+ * Exchange (kind, seg): smlu_dist_xsizes gives per-peer send/recv counts (doubles);
+ *          smlu_dist_pack fills a device buffer with the outgoing blocks in destination-rank
+ *          order (kind 2: this rank's rows once, sent to every peer); smlu_dist_unpack takes
+ *          the incoming blocks concatenated in source-rank order. */
+int     smlu_dist_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
+                         const smlu_opts* opts, int32_t rank, int32_t nranks, smlu_handle** out);
+int64_t smlu_dist_nsegments(const smlu_handle* h);
+int     smlu_dist_set_values(smlu_handle* h, const double* nzval, int32_t on_device);
+int     smlu_dist_factor_segment(smlu_handle* h, int32_t seg);
+int     smlu_dist_solve_segment(smlu_handle* h, const double* d_b, double* d_x, int32_t phase, int32_t seg);
+int     smlu_dist_xsizes(smlu_handle* h, int32_t kind, int32_t seg, int64_t* send, int64_t* recv);
+int     smlu_dist_pack(smlu_handle* h, int32_t kind, int32_t seg, double* d_buf);
+int     smlu_dist_unpack(smlu_handle* h, int32_t kind, int32_t seg, const double* d_buf);
+/* Host-only: the partition a dist handle of `nparts` ranks would use (owner per supernode,
+ * exchange-point levels); NULL outputs are skipped. */
+int     smlu_plan_partition(const smlu_plan* plan, int32_t nparts, int32_t* owner, int32_t* xlevels,
+                            int64_t* nx);
+
 /* Library version string. */
 const char* smlu_version(void);
 

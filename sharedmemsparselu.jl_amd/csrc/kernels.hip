@@ -1465,6 +1465,12 @@ __global__ void k_perm_out(int64_t n, const int64_t* __restrict__ q, const doubl
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[q[i]] = wrk[i];
 }
+// multi-GPU: x[q[i]] = wrk[i] on the rows this rank owns, 0 elsewhere (summed over ranks)
+__global__ void k_perm_out_masked(int64_t n, const int64_t* __restrict__ q, const int8_t* __restrict__ own,
+                                  const double* __restrict__ wrk, double* __restrict__ x) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[q[i]] = own[i] ? wrk[i] : 0.0;
+}
 // final order -> pre-swap positions: out[first + rowperm[first+i]] = in[first+i]
 __global__ void k_unswap(int64_t n, const int64_t* __restrict__ pos_first,
                          const int32_t* __restrict__ rowperm, const double* __restrict__ in,
@@ -1610,6 +1616,12 @@ hipError_t launch_bwd_u12(hipStream_t st, int64_t nwg, const FrontTile* ft, int 
 hipError_t launch_perm_in(hipStream_t st, int64_t n, const int64_t* p0, const double* Rs,
                           const double* b, double* wrk) {
   k_perm_in<<<nblk(n, 256), 256, 0, st>>>(n, p0, Rs, b, wrk);
+  return hipGetLastError();
+}
+hipError_t launch_perm_out_masked(hipStream_t st, int64_t n, const int64_t* q, const int8_t* own,
+                                  const double* wrk, double* x) {
+  if (n <= 0) return hipSuccess;
+  k_perm_out_masked<<<nblk(n, 256), 256, 0, st>>>(n, q, own, wrk, x);
   return hipGetLastError();
 }
 hipError_t launch_perm_out(hipStream_t st, int64_t n, const int64_t* q, const double* wrk, double* x) {

@@ -467,6 +467,7 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
   Loff.assign(nsup, 0);
   Uoff.assign(nsup, 0);
   lev_foff.assign(nlevels + 1, 0);
+  front_flops.assign(nsup, 0.0);
   int64_t cur = 0;
   front_max = ns_max = nu_max = 0;
   stored = 0;
@@ -492,6 +493,7 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
       sum_sq = S2(fm - 1) - S2(fm - 1 - fa);
       double sum_l = fa * (fm - 1) - fa * (fa - 1) / 2;
       flops += 2 * sum_sq + sum_l;
+      front_flops[s] = 2 * sum_sq + sum_l;
     }
   }
   lev_foff[nlevels] = cur;
@@ -581,6 +583,110 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
   }
   analysis_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return "";
+}
+
+// ---------------------------------------------------------------------------------------
+// Multi-GPU partition: proportional mapping (Pothen & Sun) of the assembly tree onto ranks.
+// ---------------------------------------------------------------------------------------
+void Plan::compute_owners(int np) {
+  nparts = std::max(1, np);
+  owner.assign(nsup, 0);
+  xlevels.clear();
+  if (nparts == 1 || nsup == 0) return;
+  // subtree work (children have smaller indices than their parents)
+  std::vector<double> W(front_flops.begin(), front_flops.end());
+  for (int64_t s = 0; s < nsup; ++s)
+    if (s_parent[s] >= 0) W[s_parent[s]] += W[s];
+  std::vector<double> load(nparts, 0.0);
+  // assign a whole subtree to one rank
+  auto give = [&](int64_t root, int r) {
+    // the subtree of root is the contiguous postorder range ending at root
+    std::vector<int64_t> stack{root};
+    while (!stack.empty()) {
+      int64_t v = stack.back();
+      stack.pop_back();
+      owner[v] = r;
+      for (int64_t e = ch_ptr[v]; e < ch_ptr[v + 1]; ++e) stack.push_back(ch_list[e]);
+    }
+    load[r] += W[root];
+  };
+  struct Task { int64_t s; int r0, r1; };
+  std::vector<Task> work;
+  {
+    std::vector<int64_t> roots;
+    for (int64_t s = 0; s < nsup; ++s)
+      if (s_parent[s] < 0) roots.push_back(s);
+    // roots of the forest share all ranks as if they hung below a virtual root
+    std::sort(roots.begin(), roots.end(), [&](int64_t a, int64_t b) { return W[a] > W[b]; });
+    double tot = 0;
+    for (auto r : roots) tot += W[r];
+    int next = 0;
+    for (auto r : roots) {
+      int k = (int)std::floor(nparts * W[r] / std::max(tot, 1e-300) + 1e-9);
+      if (next >= nparts) k = 0;
+      k = std::min(k, nparts - next);
+      if (k >= 1) {
+        work.push_back({r, next, next + k});
+        next += k;
+      } else {
+        int best = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+        give(r, best);
+      }
+    }
+    if (next < nparts && !work.empty()) work.back().r1 = nparts;   // leftover ranks to the last
+  }
+  while (!work.empty()) {
+    Task t = work.back();
+    work.pop_back();
+    const int k = t.r1 - t.r0;
+    if (k <= 1) { give(t.s, t.r0); continue; }
+    owner[t.s] = t.r0;
+    load[t.r0] += front_flops[t.s];
+    std::vector<int64_t> ch(ch_list.begin() + ch_ptr[t.s], ch_list.begin() + ch_ptr[t.s + 1]);
+    if (ch.empty()) continue;
+    std::sort(ch.begin(), ch.end(), [&](int64_t a, int64_t b) { return W[a] > W[b]; });
+    double tot = 0;
+    for (auto c : ch) tot += W[c];
+    // integer rank counts by largest remainder over the children that get >= 1 rank
+    std::vector<int> cnt(ch.size(), 0);
+    int used = 0;
+    for (size_t i = 0; i < ch.size(); ++i) {
+      cnt[i] = (int)std::floor(k * W[ch[i]] / std::max(tot, 1e-300));
+      used += cnt[i];
+    }
+    while (used < k) {   // hand out the remaining ranks by largest remainder
+      size_t bi = 0;
+      double br = -1;
+      for (size_t i = 0; i < ch.size(); ++i) {
+        double rem = k * W[ch[i]] / std::max(tot, 1e-300) - cnt[i];
+        if (rem > br) { br = rem; bi = i; }
+      }
+      cnt[bi]++;
+      used++;
+    }
+    int next = t.r0;
+    for (size_t i = 0; i < ch.size(); ++i) {
+      if (cnt[i] >= 1) {
+        work.push_back({ch[i], next, next + cnt[i]});
+        next += cnt[i];
+      }
+    }
+    for (size_t i = 0; i < ch.size(); ++i) {
+      if (cnt[i] == 0) {   // small child: the least-loaded rank of this set takes it whole
+        int best = t.r0;
+        for (int r = t.r0; r < t.r1; ++r)
+          if (load[r] < load[best]) best = r;
+        give(ch[i], best);
+      }
+    }
+  }
+  std::vector<char> isx(nlevels, 0);
+  for (int64_t s = 0; s < nsup; ++s) {
+    int64_t pp = s_parent[s];
+    if (pp >= 0 && owner[pp] != owner[s]) isx[s_level[pp]] = 1;
+  }
+  for (int l = 0; l < nlevels; ++l)
+    if (isx[l]) xlevels.push_back(l);
 }
 
 }  // namespace smlu

@@ -98,6 +98,17 @@ struct Plan {
   int64_t front_max = 0, ns_max = 0, nu_max = 0;
   double analysis_ms = 0;
 
+  // ---- multi-GPU partition (compute_owners) ----
+  // owner[s] = rank that factors front s.  Proportional mapping of the assembly tree: a
+  // subtree whose rank set has one member is owned by it entirely; a front above that keeps
+  // the first rank of its set.  Exchange points are the levels of fronts with a child owned
+  // by another rank (the child's update block crosses GPUs right before that level).
+  int nparts = 1;
+  std::vector<int32_t> owner;
+  std::vector<int32_t> xlevels;               // sorted exchange-point levels
+  std::vector<double> front_flops;            // per front (same formula as `flops`)
+  void compute_owners(int nparts);
+
   std::string build(int64_t n, const int64_t* colptr, const int64_t* rowval, int index_base,
                     const PlanOptions& opt, const int64_t* pgiven = nullptr,
                     const int64_t* qgiven = nullptr);

@@ -58,6 +58,7 @@ hipError_t launch_bwd(hipStream_t, int, const int32_t*, const SNode*, const int3
                       double*, double*);
 hipError_t launch_perm_in(hipStream_t, int64_t, const int64_t*, const double*, const double*, double*);
 hipError_t launch_perm_out(hipStream_t, int64_t, const int64_t*, const double*, double*);
+hipError_t launch_perm_out_masked(hipStream_t, int64_t, const int64_t*, const int8_t*, const double*, double*);
 hipError_t launch_unswap(hipStream_t, int64_t, const int64_t*, const int32_t*, const double*, double*);
 }  // namespace smlu
 
@@ -155,8 +156,17 @@ struct smlu_handle {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   std::vector<int> ev_kind;
   int32_t* hinfo = nullptr;  // pinned
-  hipGraphExec_t fac_exec = nullptr, sol_exec = nullptr;
+  hipGraphExec_t sol_exec = nullptr;
+  std::vector<hipGraphExec_t> fac_execs;   // one captured graph per factor segment
   int fac_exec_profile = -1;
+  std::vector<std::pair<size_t, size_t>> seg_events;   // profile events of each captured segment
+  // multi-GPU partition (smlu_dist_*): this rank's fronts, segments between exchange points
+  int rank = 0, nranks = 1;
+  std::vector<size_t> fac_seg, fwd_seg, bwd_seg;   // launch index where each segment starts
+  struct XBlk { int32_t src, dst; int64_t off, cnt; };
+  std::vector<std::vector<XBlk>> xfac, xfwd;       // per exchange point: child F22 / vbuf blocks
+  std::vector<std::vector<std::vector<std::pair<int64_t, int64_t>>>> xbwd;   // [point][rank] x rows
+  DBuf<int8_t> rowown;
   size_t fac_graph_events = 0;
   bool graph_failed = false;
   bool lookahead = false;     // SMLU_LOOKAHEAD=1: trailing updates beyond the next block on a side stream
@@ -179,11 +189,14 @@ struct smlu_handle {
     gtasks.free();
     stasks.free();
     xcols.free();
+    rowown.free();
   }
   void release_graphs() {
-    if (fac_exec) (void)hipGraphExecDestroy(fac_exec);
+    for (auto& g : fac_execs)
+      if (g) (void)hipGraphExecDestroy(g);
+    fac_execs.clear();
     if (sol_exec) (void)hipGraphExecDestroy(sol_exec);
-    fac_exec = sol_exec = nullptr;
+    sol_exec = nullptr;
     fac_exec_profile = -1;
   }
   void release_all() {
@@ -206,6 +219,16 @@ struct smlu_handle {
     stream = nullptr;
   }
 };
+
+#define HIPCHK2(hh, expr)                                                            \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess) {                                                          \
+      (hh)->err = std::string("HIP error: ") + hipGetErrorString(_e) + " at " #expr; \
+      g_last_error = (hh)->err;                                                      \
+      return SMLU_ERR_HIP;                                                           \
+    }                                                                                \
+  } while (0)
 
 #define HIPCHK(expr)                                                                 \
   do {                                                                               \
@@ -291,6 +314,20 @@ static int build_schedule(smlu_handle* h) {
   double* store = h->store.p;
   double* scratch = h->scratch.p;
   h->fac.clear();
+  // this rank's fronts by level (every front when nranks == 1)
+  std::vector<int64_t> LP(P.nlevels + 1, 0);
+  std::vector<int32_t> LS;
+  for (int l = 0; l < P.nlevels; ++l) {
+    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k)
+      if (h->nranks == 1 || P.owner[P.lev_sup[k]] == h->rank) LS.push_back(P.lev_sup[k]);
+    LP[l + 1] = (int64_t)LS.size();
+  }
+  std::vector<char> isx(P.nlevels, 0);
+  if (h->nranks > 1)
+    for (auto l : P.xlevels) isx[l] = 1;
+  h->fac_seg.assign(1, 0);
+  h->fwd_seg.assign(1, 0);
+  h->bwd_seg.assign(1, 0);
   h->lookahead = std::getenv("SMLU_LOOKAHEAD") != nullptr;
   if (const char* e = std::getenv("SMLU_SIDE_WG")) h->side_wg = std::atoll(e);
   if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
@@ -336,6 +373,7 @@ static int build_schedule(smlu_handle* h) {
   };
   for (int l = 0; l < P.nlevels; ++l) {
     Launch L;
+    if (isx[l]) h->fac_seg.push_back(h->fac.size());   // exchange point before this level
     // zero this level's fronts
     L = Launch();
     L.kind = K_MEMSET_STORE;
@@ -362,8 +400,8 @@ static int build_schedule(smlu_handle* h) {
       L.kind = K_EXTADD;
       L.off = (int64_t)xc.size();
       std::vector<int32_t> cnt, pos;
-      for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
-        int64_t s = P.lev_sup[k];
+      for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {
+        int64_t s = LS[k];
         if (P.ch_ptr[s] == P.ch_ptr[s + 1]) continue;
         const int64_t M = P.M(s);
         cnt.assign(M + 1, 0);
@@ -396,8 +434,8 @@ static int build_schedule(smlu_handle* h) {
         L.kind = K_FRONT_LDS;
         L.off = (int64_t)ilist.size();
         int64_t Mmax = 0;
-        for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
-          int64_t s = P.lev_sup[k];
+        for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {
+          int64_t s = LS[k];
           if (h->hsn[s].mode != 0) continue;
           int64_t M = P.M(s);
           if (M > cls[c] || (c > 0 && M <= cls[c - 1])) continue;
@@ -413,8 +451,8 @@ static int build_schedule(smlu_handle* h) {
     std::vector<int64_t> big;
     std::unordered_map<int64_t, int64_t> bidx;   // front -> index in big (swap-list slots)
     int64_t maxsteps = 0;
-    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
-      int64_t s = P.lev_sup[k];
+    for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {
+      int64_t s = LS[k];
       const SNode& r = h->hsn[s];
       if (r.mode == 0) continue;
       bidx[s] = (int64_t)big.size();
@@ -712,9 +750,10 @@ static int build_schedule(smlu_handle* h) {
   h->bwd.clear();
   std::vector<std::vector<Launch>> bwd_levels;
   for (int l = 0; l < P.nlevels; ++l) {
+    if (isx[l]) h->fwd_seg.push_back(h->fwd.size());
     std::vector<int64_t> small, bigs;
-    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
-      int64_t s = P.lev_sup[k];
+    for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {
+      int64_t s = LS[k];
       (h->hsn[s].ns > kSolveBigNs ? bigs : small).push_back(s);
     }
     std::vector<Launch> bl;
@@ -789,8 +828,42 @@ static int build_schedule(smlu_handle* h) {
     }
     bwd_levels.push_back(bl);
   }
-  for (int l = P.nlevels - 1; l >= 0; --l)
+  for (int l = P.nlevels - 1; l >= 0; --l) {
     for (auto& L : bwd_levels[l]) h->bwd.push_back(L);
+    if (isx[l]) h->bwd_seg.push_back(h->bwd.size());   // exchange point after this level
+  }
+  // exchange lists (multi-GPU): child blocks crossing ranks before each exchange level, and
+  // per rank the solution rows of the backward segment that ends at that level
+  {
+    const size_t nx = h->nranks > 1 ? P.xlevels.size() : 0;
+    h->xfac.assign(nx, {});
+    h->xfwd.assign(nx, {});
+    h->xbwd.assign(nx, std::vector<std::vector<std::pair<int64_t, int64_t>>>(h->nranks));
+    for (size_t k = 0; k < nx; ++k) {
+      const int l = P.xlevels[k];
+      for (int64_t kk = P.lev_ptr[l]; kk < P.lev_ptr[l + 1]; ++kk) {
+        const int64_t pp = P.lev_sup[kk];
+        for (int64_t e = P.ch_ptr[pp]; e < P.ch_ptr[pp + 1]; ++e) {
+          const int64_t c = P.ch_list[e];
+          if (P.owner[c] == P.owner[pp]) continue;
+          if (P.nu(c) > 0)
+            h->xfac[k].push_back({P.owner[c], P.owner[pp], P.Foff[c], P.nu(c) * P.nu(c)});
+          h->xfwd[k].push_back({P.owner[c], P.owner[pp], h->hsn[c].voff, P.M(c)});
+        }
+      }
+      auto byrank = [](const smlu_handle::XBlk& a, const smlu_handle::XBlk& b) {
+        return a.src != b.src ? a.src < b.src : a.dst != b.dst ? a.dst < b.dst : a.off < b.off;
+      };
+      std::sort(h->xfac[k].begin(), h->xfac[k].end(), byrank);
+      std::sort(h->xfwd[k].begin(), h->xfwd[k].end(), byrank);
+      const int lhi = k + 1 < nx ? P.xlevels[k + 1] : P.nlevels;
+      for (int ll = l; ll < lhi; ++ll)
+        for (int64_t kk = P.lev_ptr[ll]; kk < P.lev_ptr[ll + 1]; ++kk) {
+          const int64_t s2 = P.lev_sup[kk];
+          h->xbwd[k][P.owner[s2]].push_back({P.s_first[s2], P.ns(s2)});
+        }
+    }
+  }
 
   h->nlaunch = (int64_t)h->fac.size();
   // upload
@@ -865,6 +938,11 @@ static int setup_device(smlu_handle* h) {
     HIPCHK(h->rowperm0.upload(id.data(), id.size(), st));
   }
   HIPCHK(h->info.alloc((size_t)std::max<int64_t>(P.nsup, 1)));
+  if (h->nranks > 1) {
+    std::vector<int8_t> own(P.n);
+    for (int64_t j = 0; j < P.n; ++j) own[j] = P.owner[P.col2s[j]] == h->rank ? 1 : 0;
+    HIPCHK(h->rowown.upload(own.data(), own.size(), st));
+  }
   HIPCHK(init_kernel_attributes());
   if (h->hinfo) HIPCHK(hipHostFree(h->hinfo));
   h->hinfo = nullptr;
@@ -955,9 +1033,16 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
 }
 
 // All device work of one numeric refactorization, in stream order (captured into a graph).
-static int enqueue_factor(smlu_handle* h, Timer& tm, bool dbg) {
+// Segment `seg` of one numeric refactorization (launches between two exchange points; the
+// whole refactor is the single segment 0 on one GPU), in stream order.
+static int enqueue_factor(smlu_handle* h, Timer& tm, bool dbg, int seg) {
   Plan& P = h->plan;
   hipStream_t st = h->stream;
+  const size_t lo = h->fac_seg[seg];
+  const size_t hi = (size_t)seg + 1 < h->fac_seg.size() ? h->fac_seg[seg + 1] : h->fac.size();
+  double diag_tol = P.given_order ? 0.0 : h->opts.diag_pivot_tol;
+  double piv_tol = h->opts.pivot_tol;
+  if (seg > 0) goto launches;
   HIPCHK(hipMemsetAsync(h->info.p, 0, sizeof(int32_t) * std::max<int64_t>(P.nsup, 1), st));
   HIPCHK(hipMemsetAsync(h->growth.p, 0, sizeof(double), st));
   // identity (local) row permutation; fronts overwrite their part
@@ -966,10 +1051,10 @@ static int enqueue_factor(smlu_handle* h, Timer& tm, bool dbg) {
     if (h->opts.scale) HIPCHK(launch_rowscale(st, P.n, h->Arowptr.p, h->Arow_ent.p, h->A.p, h->Rs.p));
     else HIPCHK(launch_fill(st, P.n, h->Rs.p, 1.0));
   }
-  // A given (p, q) order means "no pivoting on top": only a zero diagonal moves.
-  double diag_tol = P.given_order ? 0.0 : h->opts.diag_pivot_tol;
-  double piv_tol = h->opts.pivot_tol;
-  for (const Launch& L : h->fac) {
+  // A given (p, q) order means "no pivoting on top": only a zero diagonal moves (diag_tol 0).
+launches:
+  for (size_t li = lo; li < hi; ++li) {
+    const Launch& L = h->fac[li];
     hipEvent_t stop;
     HIPCHK(tm.begin(L.kind, &stop, L.side ? h->side : st));
     hipError_t e = run_launch(h, L, diag_tol, piv_tol);
@@ -987,44 +1072,52 @@ static int enqueue_factor(smlu_handle* h, Timer& tm, bool dbg) {
   return SMLU_OK;
 }
 
-static int run_factor(smlu_handle* h) {
-  Plan& P = h->plan;
+// Run factor segment `seg`: captured once into a hipGraph and replayed (the first
+// factorization runs eagerly).
+static int factor_segment(smlu_handle* h, Timer& tm, int seg) {
   hipStream_t st = h->stream;
-  HIPCHK(hipSetDevice(h->device));
-  auto t0 = std::chrono::steady_clock::now();
-  for (auto& v : h->kind_ms) v = 0;
-  Timer tm(h);
   static const bool dbg = std::getenv("SMLU_DEBUG_SYNC") != nullptr;
   static const bool nograph = std::getenv("SMLU_NO_GRAPH") != nullptr;
   const int prof = h->opts.profile ? 1 : 0;
+  const size_t nseg = h->fac_seg.size();
+  if (h->fac_execs.size() != nseg || (seg == 0 && h->fac_exec_profile != prof)) {
+    for (auto& g : h->fac_execs)
+      if (g) (void)hipGraphExecDestroy(g);
+    h->fac_execs.assign(nseg, nullptr);
+    h->seg_events.assign(nseg, {0, 0});
+  }
   bool use_graph = !dbg && !nograph && !h->graph_failed && h->have_numeric;  // first run eager
-  if (use_graph && (!h->fac_exec || h->fac_exec_profile != prof)) {
-    if (h->fac_exec) (void)hipGraphExecDestroy(h->fac_exec);
-    h->fac_exec = nullptr;
+  if (use_graph && !h->fac_execs[seg]) {
     hipGraph_t g = nullptr;
+    const size_t ev0 = tm.used;
     HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
-    int rc = enqueue_factor(h, tm, false);
+    int rc = enqueue_factor(h, tm, false, seg);
     hipError_t ec = hipStreamEndCapture(st, &g);
-    if (rc == SMLU_OK && ec == hipSuccess && g) ec = hipGraphInstantiate(&h->fac_exec, g, nullptr, nullptr, 0);
+    if (rc == SMLU_OK && ec == hipSuccess && g) ec = hipGraphInstantiate(&h->fac_execs[seg], g, nullptr, nullptr, 0);
     if (g) (void)hipGraphDestroy(g);
-    if (rc != SMLU_OK || ec != hipSuccess || !h->fac_exec) {
+    if (rc != SMLU_OK || ec != hipSuccess || !h->fac_execs[seg]) {
       (void)hipGetLastError();
       h->graph_failed = true;   // fall back to eager launches
-      h->fac_exec = nullptr;
+      h->fac_execs[seg] = nullptr;
       use_graph = false;
-      tm.used = 0;
+      tm.used = ev0;
     } else {
       h->fac_exec_profile = prof;
-      h->fac_graph_events = tm.used;
+      h->seg_events[seg] = {ev0, tm.used - ev0};
     }
   }
   if (use_graph) {
-    tm.used = h->fac_graph_events;
-    HIPCHK(hipGraphLaunch(h->fac_exec, st));
-  } else {
-    int rc = enqueue_factor(h, tm, dbg);
-    if (rc != SMLU_OK) return rc;
+    tm.used = h->seg_events[seg].first + h->seg_events[seg].second;
+    HIPCHK(hipGraphLaunch(h->fac_execs[seg], st));
+    return SMLU_OK;
   }
+  return enqueue_factor(h, tm, dbg, seg);
+}
+
+// After the last segment: pivot status of this rank's fronts.
+static int finish_factor(smlu_handle* h, Timer& tm, std::chrono::steady_clock::time_point t0) {
+  Plan& P = h->plan;
+  hipStream_t st = h->stream;
   HIPCHK(hipMemcpyAsync(h->hinfo, h->info.p, sizeof(int32_t) * P.nsup, hipMemcpyDeviceToHost, st));
   double g = 0;
   HIPCHK(hipMemcpyAsync(&g, h->growth.p, sizeof(double), hipMemcpyDeviceToHost, st));
@@ -1046,6 +1139,19 @@ static int run_factor(smlu_handle* h) {
   }
   if (rc == SMLU_SINGULAR) h->err = "matrix is singular (zero pivot column)";
   return rc;
+}
+
+static int run_factor(smlu_handle* h) {
+  HIPCHK(hipSetDevice(h->device));
+  if (h->nranks > 1) return fail(h, SMLU_ERR_STATE, "partitioned handle: use smlu_dist_factor_segment");
+  auto t0 = std::chrono::steady_clock::now();
+  for (auto& v : h->kind_ms) v = 0;
+  Timer tm(h);
+  for (size_t seg = 0; seg < h->fac_seg.size(); ++seg) {
+    int rc = factor_segment(h, tm, (int)seg);
+    if (rc != SMLU_OK) return rc;
+  }
+  return finish_factor(h, tm, t0);
 }
 
 static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w) {
@@ -1075,6 +1181,7 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w) {
 static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode) {
   // mode 0: ldiv (b -> x); 1: lsolve in place on dx (final order); 2: rsolve in place
   Plan& P = h->plan;
+  if (h->nranks > 1) return fail(h, SMLU_ERR_STATE, "partitioned handle: use smlu_dist_solve_segment");
   hipStream_t st = h->stream;
   auto t0 = std::chrono::steady_clock::now();
   Timer tm(h);
@@ -1101,7 +1208,7 @@ static bool valid_opts(const smlu_opts* o) { return o && (o->index_base == 0 || 
 
 static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
                        const int64_t* p, const int64_t* q, const double* Rs, const smlu_opts* opts,
-                       smlu_handle** out) {
+                       smlu_handle** out, int rank = 0, int nranks = 1) {
   if (!out) return fail(nullptr, SMLU_ERR_ARG, "out is NULL");
   *out = nullptr;
   if (n <= 0 || !colptr || (!rowval && n > 0) || !nzval)
@@ -1121,6 +1228,12 @@ static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, 
     return fail(nullptr, SMLU_ERR_ALLOC, "host allocation failed during analysis");
   }
   if (!e.empty()) return fail(nullptr, SMLU_ERR_ARG, e);
+  h->rank = rank;
+  h->nranks = nranks;
+  if (nranks > 1) {
+    h->plan.compute_owners(nranks);
+    h->opts.profile = 0;   // per-kind event timing is single-GPU only
+  }
   rc = setup_device(h.get());
   if (rc != SMLU_OK) { g_last_error = h->err; return rc; }
   hipStream_t st = h->stream;
@@ -1132,6 +1245,11 @@ static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, 
       HIPCHK(hipMemcpyAsync(h->Rs.p, Rs, sizeof(double) * n, hipMemcpyHostToDevice, st));
       h->given_Rs = true;
     }
+  }
+  if (nranks > 1) {   // the caller drives the segments and the exchanges (smlu_dist_*)
+    HIPCHK2(h.get(), hipStreamSynchronize(st));
+    *out = h.release();
+    return SMLU_OK;
   }
   rc = run_factor(h.get());
   *out = h.release();
@@ -1517,6 +1635,169 @@ int smlu_plan_supernodes(const smlu_plan* pl, int64_t* first, int64_t* parent, i
 }
 
 void smlu_plan_destroy(smlu_plan* p) { delete p; }
+
+// ---- multi-GPU partition (one process per GPU; exchanges driven by the caller) ----------
+int smlu_dist_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
+                     const smlu_opts* opts, int32_t rank, int32_t nranks, smlu_handle** out) {
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(nullptr, SMLU_ERR_ARG, "bad rank/nranks");
+  return create_impl(n, colptr, rowval, nzval, nullptr, nullptr, nullptr, opts, out, rank, nranks);
+}
+
+int64_t smlu_dist_nsegments(const smlu_handle* h) { return h ? (int64_t)h->fac_seg.size() : -1; }
+
+int smlu_dist_set_values(smlu_handle* h, const double* nzval, int32_t on_device) {
+  if (!h || !nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipMemcpyAsync(h->A.p, nzval, sizeof(double) * h->plan.nnzA,
+                        on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return SMLU_OK;
+}
+
+int smlu_dist_factor_segment(smlu_handle* h, int32_t seg) {
+  if (!h || seg < 0 || (size_t)seg >= h->fac_seg.size()) return fail(h, SMLU_ERR_ARG, "bad segment");
+  HIPCHK(hipSetDevice(h->device));
+  static thread_local std::chrono::steady_clock::time_point t0;
+  if (seg == 0) {
+    t0 = std::chrono::steady_clock::now();
+    for (auto& v : h->kind_ms) v = 0;
+  }
+  Timer tm(h);
+  int rc = factor_segment(h, tm, seg);
+  if (rc != SMLU_OK) return rc;
+  if ((size_t)seg + 1 == h->fac_seg.size()) return finish_factor(h, tm, t0);
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return SMLU_OK;
+}
+
+int smlu_dist_solve_segment(smlu_handle* h, const double* d_b, double* d_x, int32_t phase, int32_t seg) {
+  if (!h) return fail(nullptr, SMLU_ERR_ARG, "NULL handle");
+  if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = h->stream;
+  double* w = h->wrk.p;
+  if (phase == 0 || phase == 1) {
+    const std::vector<size_t>& sg = phase == 0 ? h->fwd_seg : h->bwd_seg;
+    const std::vector<Launch>& ls = phase == 0 ? h->fwd : h->bwd;
+    if (seg < 0 || (size_t)seg >= sg.size()) return fail(h, SMLU_ERR_ARG, "bad segment");
+    if (phase == 0 && seg == 0) {
+      if (!d_b) return fail(h, SMLU_ERR_ARG, "NULL b");
+      HIPCHK(launch_perm_in(st, h->plan.n, h->p0.p, h->Rs.p, d_b, w));
+    }
+    const size_t hi = (size_t)seg + 1 < sg.size() ? sg[seg + 1] : ls.size();
+    for (size_t i = sg[seg]; i < hi; ++i) HIPCHK(run_solve_launch(h, ls[i], w));
+  } else if (phase == 2) {
+    if (!d_x) return fail(h, SMLU_ERR_ARG, "NULL x");
+    if (h->nranks > 1) HIPCHK(launch_perm_out_masked(st, h->plan.n, h->q.p, h->rowown.p, w, d_x));
+    else HIPCHK(launch_perm_out(st, h->plan.n, h->q.p, w, d_x));
+  } else {
+    return fail(h, SMLU_ERR_ARG, "bad phase");
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  return SMLU_OK;
+}
+
+// Exchange before segment `seg` (>= 1) of kind 0 (factor: child update blocks), 1 (forward
+// solve: child update vectors) or 2 (backward solve: solution rows, every rank to every rank).
+static double* dist_base(smlu_handle* h, int kind) {
+  return kind == 0 ? h->scratch.p : kind == 1 ? h->vbuf.p : h->wrk.p;
+}
+
+static bool dist_point(const smlu_handle* h, int kind, int seg, size_t* k) {
+  const size_t nx = h->xfac.size();
+  if (seg < 1 || (size_t)seg > nx || kind < 0 || kind > 2) return false;
+  *k = kind == 2 ? nx - (size_t)seg : (size_t)seg - 1;
+  return true;
+}
+
+int smlu_dist_xsizes(smlu_handle* h, int32_t kind, int32_t seg, int64_t* send, int64_t* recv) {
+  if (!h || !send || !recv) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  size_t k;
+  if (!dist_point(h, kind, seg, &k)) return fail(h, SMLU_ERR_ARG, "bad exchange point");
+  for (int r = 0; r < h->nranks; ++r) send[r] = recv[r] = 0;
+  if (kind < 2) {
+    for (auto& b : (kind == 0 ? h->xfac : h->xfwd)[k]) {
+      if (b.src == h->rank) send[b.dst] += b.cnt;
+      if (b.dst == h->rank) recv[b.src] += b.cnt;
+    }
+  } else {
+    for (int r = 0; r < h->nranks; ++r) {
+      int64_t c = 0;
+      for (auto& rg : h->xbwd[k][r]) c += rg.second;
+      if (r == h->rank) {
+        for (int d = 0; d < h->nranks; ++d)
+          if (d != r) send[d] = c;
+      } else {
+        recv[r] = c;
+      }
+    }
+  }
+  return SMLU_OK;
+}
+
+int smlu_dist_pack(smlu_handle* h, int32_t kind, int32_t seg, double* d_buf) {
+  if (!h) return fail(nullptr, SMLU_ERR_ARG, "NULL handle");
+  size_t k;
+  if (!dist_point(h, kind, seg, &k)) return fail(h, SMLU_ERR_ARG, "bad exchange point");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = h->stream;
+  const double* base = dist_base(h, kind);
+  int64_t o = 0;
+  if (kind < 2) {   // blocks in (dst, child) order
+    for (auto& b : (kind == 0 ? h->xfac : h->xfwd)[k])
+      if (b.src == h->rank) {
+        HIPCHK(hipMemcpyAsync(d_buf + o, base + b.off, sizeof(double) * b.cnt, hipMemcpyDeviceToDevice, st));
+        o += b.cnt;
+      }
+  } else {          // this rank's rows, once (the caller sends the same buffer to every rank)
+    for (auto& rg : h->xbwd[k][h->rank]) {
+      HIPCHK(hipMemcpyAsync(d_buf + o, base + rg.first, sizeof(double) * rg.second, hipMemcpyDeviceToDevice, st));
+      o += rg.second;
+    }
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  return SMLU_OK;
+}
+
+int smlu_dist_unpack(smlu_handle* h, int32_t kind, int32_t seg, const double* d_buf) {
+  if (!h) return fail(nullptr, SMLU_ERR_ARG, "NULL handle");
+  size_t k;
+  if (!dist_point(h, kind, seg, &k)) return fail(h, SMLU_ERR_ARG, "bad exchange point");
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = h->stream;
+  double* base = dist_base(h, kind);
+  int64_t o = 0;
+  if (kind < 2) {   // blocks in (src, child) order
+    for (auto& b : (kind == 0 ? h->xfac : h->xfwd)[k])
+      if (b.dst == h->rank) {
+        HIPCHK(hipMemcpyAsync(base + b.off, d_buf + o, sizeof(double) * b.cnt, hipMemcpyDeviceToDevice, st));
+        o += b.cnt;
+      }
+  } else {          // other ranks' rows in rank order
+    for (int r = 0; r < h->nranks; ++r) {
+      if (r == h->rank) continue;
+      for (auto& rg : h->xbwd[k][r]) {
+        HIPCHK(hipMemcpyAsync(base + rg.first, d_buf + o, sizeof(double) * rg.second, hipMemcpyDeviceToDevice, st));
+        o += rg.second;
+      }
+    }
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  return SMLU_OK;
+}
+
+int smlu_plan_partition(const smlu_plan* plan, int32_t nparts, int32_t* owner, int32_t* xlevels,
+                        int64_t* nx) {
+  if (!plan || nparts < 1) return fail(nullptr, SMLU_ERR_ARG, "invalid arguments");
+  Plan P = plan->plan;   // copy: the partition is a query
+  P.compute_owners(nparts);
+  if (owner)
+    for (int64_t s = 0; s < P.nsup; ++s) owner[s] = P.owner[s];
+  if (xlevels)
+    for (size_t i = 0; i < P.xlevels.size(); ++i) xlevels[i] = P.xlevels[i];
+  if (nx) *nx = (int64_t)P.xlevels.size();
+  return SMLU_OK;
+}
 
 const char* smlu_version(void) { return "smlu 0.1.0 (gfx950, fp64, multifrontal)"; }
 

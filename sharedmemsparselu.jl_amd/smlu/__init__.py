@@ -6,7 +6,8 @@ from .api import (ParallelSparseLU, lu_, ldiv_, lsolve_, rsolve_,  # noqa: F401
                   cleanup_ParallelSparseLU_, allocate_shared, DimensionMismatch,
                   SingularException, SmluError)
 from .plan import Plan  # noqa: F401
+from .dist import DistributedSparseLU  # noqa: F401
 
 __all__ = ["ParallelSparseLU", "lu_", "ldiv_", "lsolve_", "rsolve_", "cleanup_ParallelSparseLU_",
-           "allocate_shared", "DimensionMismatch", "SingularException", "SmluError", "Plan", "build",
+           "allocate_shared", "DimensionMismatch", "SingularException", "SmluError", "Plan", "DistributedSparseLU", "build",
            "lib"]

@@ -77,6 +77,15 @@ SIGNATURES = {
     "smlu_plan_supernodes": (i32, [vp, vp, vp, vp]),
     "smlu_plan_destroy": (None, [vp]),
     "smlu_version": (ctypes.c_char_p, []),
+    "smlu_dist_create": (i32, [i64, vp, vp, vp, ctypes.POINTER(SmluOpts), i32, i32, ctypes.POINTER(vp)]),
+    "smlu_dist_nsegments": (i64, [vp]),
+    "smlu_dist_set_values": (i32, [vp, vp, i32]),
+    "smlu_dist_factor_segment": (i32, [vp, i32]),
+    "smlu_dist_solve_segment": (i32, [vp, vp, vp, i32, i32]),
+    "smlu_dist_xsizes": (i32, [vp, i32, i32, vp, vp]),
+    "smlu_dist_pack": (i32, [vp, i32, i32, vp]),
+    "smlu_dist_unpack": (i32, [vp, i32, i32, vp]),
+    "smlu_plan_partition": (i32, [vp, i32, vp, vp, i64p]),
 }
 
 _lib = None

@@ -60,6 +60,26 @@ class Plan:
         C.lib().smlu_plan_supernodes(self._h, C.ptr(first), C.ptr(parent), C.ptr(level))
         return first, parent, level
 
+    def partition(self, nparts):
+        """(owner per supernode, exchange-point levels) of an `nparts`-rank dist handle."""
+        ns = int(self.stat("nsuper"))
+        owner = np.empty(ns, np.int32)
+        xl = np.empty(int(self.stat("nlevels")) + 1, np.int32)
+        nx = ctypes.c_int64()
+        rc = C.lib().smlu_plan_partition(self._h, int(nparts), C.ptr(owner), C.ptr(xl), ctypes.byref(nx))
+        if rc != 0:
+            raise RuntimeError(f"smlu_plan_partition failed ({rc}): {C.last_error(None)}")
+        return owner, xl[:nx.value].copy()
+
+    def front_flops(self):
+        """Dense flops per supernode (the partition's work model)."""
+        first, parent, level = self.supernodes()
+        L = self.L_pattern()
+        ns = np.diff(first).astype(np.float64)
+        M = np.diff(L.indptr)[first[:-1]].astype(np.float64)
+        S2 = lambda x: x * (x + 1) * (2 * x + 1) / 6.0  # noqa: E731
+        return 2 * (S2(M - 1) - S2(M - 1 - ns)) + ns * (M - 1) - ns * (ns - 1) / 2
+
     def __del__(self):
         try:
             if self._h:
