@@ -586,99 +586,62 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
 }
 
 // ---------------------------------------------------------------------------------------
-// Multi-GPU partition: proportional mapping (Pothen & Sun) of the assembly tree onto ranks.
+// Multi-GPU partition of the assembly tree (subtree-to-rank mapping).  Repeatedly split the
+// heaviest subtree into its children (the split front stays above, as a "top" front) until no
+// subtree exceeds the per-rank share; bin-pack the subtrees onto the ranks (largest first,
+// least-loaded rank); a top front goes to the rank of its heaviest child, so the largest
+// update block never crosses GPUs.
 // ---------------------------------------------------------------------------------------
 void Plan::compute_owners(int np) {
   nparts = std::max(1, np);
   owner.assign(nsup, 0);
   xlevels.clear();
   if (nparts == 1 || nsup == 0) return;
-  // subtree work (children have smaller indices than their parents)
-  std::vector<double> W(front_flops.begin(), front_flops.end());
+  std::vector<double> W(front_flops.begin(), front_flops.end());   // subtree work
   for (int64_t s = 0; s < nsup; ++s)
     if (s_parent[s] >= 0) W[s_parent[s]] += W[s];
-  std::vector<double> load(nparts, 0.0);
-  // assign a whole subtree to one rank
-  auto give = [&](int64_t root, int r) {
-    // the subtree of root is the contiguous postorder range ending at root
-    std::vector<int64_t> stack{root};
-    while (!stack.empty()) {
-      int64_t v = stack.back();
-      stack.pop_back();
-      owner[v] = r;
-      for (int64_t e = ch_ptr[v]; e < ch_ptr[v + 1]; ++e) stack.push_back(ch_list[e]);
-    }
-    load[r] += W[root];
+  std::vector<int64_t> S;                                           // subtree roots
+  for (int64_t s = 0; s < nsup; ++s)
+    if (s_parent[s] < 0) S.push_back(s);
+  std::vector<char> top(nsup, 0);
+  auto heaviest = [&]() {
+    size_t bi = 0;
+    for (size_t i = 1; i < S.size(); ++i)
+      if (W[S[i]] > W[S[bi]]) bi = i;
+    return bi;
   };
-  struct Task { int64_t s; int r0, r1; };
-  std::vector<Task> work;
-  {
-    std::vector<int64_t> roots;
-    for (int64_t s = 0; s < nsup; ++s)
-      if (s_parent[s] < 0) roots.push_back(s);
-    // roots of the forest share all ranks as if they hung below a virtual root
-    std::sort(roots.begin(), roots.end(), [&](int64_t a, int64_t b) { return W[a] > W[b]; });
-    double tot = 0;
-    for (auto r : roots) tot += W[r];
-    int next = 0;
-    for (auto r : roots) {
-      int k = (int)std::floor(nparts * W[r] / std::max(tot, 1e-300) + 1e-9);
-      if (next >= nparts) k = 0;
-      k = std::min(k, nparts - next);
-      if (k >= 1) {
-        work.push_back({r, next, next + k});
-        next += k;
-      } else {
-        int best = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-        give(r, best);
-      }
-    }
-    if (next < nparts && !work.empty()) work.back().r1 = nparts;   // leftover ranks to the last
+  for (int it = 0; it < 64 * nparts && !S.empty(); ++it) {
+    double sub = 0;
+    for (auto v : S) sub += W[v];
+    const size_t bi = heaviest();
+    const int64_t v = S[bi];
+    if ((int)S.size() >= nparts && W[v] <= 1.05 * sub / nparts) break;
+    if (ch_ptr[v] == ch_ptr[v + 1]) break;   // a leaf cannot be split further
+    top[v] = 1;
+    S.erase(S.begin() + (long)bi);
+    for (int64_t e = ch_ptr[v]; e < ch_ptr[v + 1]; ++e) S.push_back(ch_list[e]);
   }
-  while (!work.empty()) {
-    Task t = work.back();
-    work.pop_back();
-    const int k = t.r1 - t.r0;
-    if (k <= 1) { give(t.s, t.r0); continue; }
-    owner[t.s] = t.r0;
-    load[t.r0] += front_flops[t.s];
-    std::vector<int64_t> ch(ch_list.begin() + ch_ptr[t.s], ch_list.begin() + ch_ptr[t.s + 1]);
-    if (ch.empty()) continue;
-    std::sort(ch.begin(), ch.end(), [&](int64_t a, int64_t b) { return W[a] > W[b]; });
-    double tot = 0;
-    for (auto c : ch) tot += W[c];
-    // integer rank counts by largest remainder over the children that get >= 1 rank
-    std::vector<int> cnt(ch.size(), 0);
-    int used = 0;
-    for (size_t i = 0; i < ch.size(); ++i) {
-      cnt[i] = (int)std::floor(k * W[ch[i]] / std::max(tot, 1e-300));
-      used += cnt[i];
-    }
-    while (used < k) {   // hand out the remaining ranks by largest remainder
-      size_t bi = 0;
-      double br = -1;
-      for (size_t i = 0; i < ch.size(); ++i) {
-        double rem = k * W[ch[i]] / std::max(tot, 1e-300) - cnt[i];
-        if (rem > br) { br = rem; bi = i; }
-      }
-      cnt[bi]++;
-      used++;
-    }
-    int next = t.r0;
-    for (size_t i = 0; i < ch.size(); ++i) {
-      if (cnt[i] >= 1) {
-        work.push_back({ch[i], next, next + cnt[i]});
-        next += cnt[i];
-      }
-    }
-    for (size_t i = 0; i < ch.size(); ++i) {
-      if (cnt[i] == 0) {   // small child: the least-loaded rank of this set takes it whole
-        int best = t.r0;
-        for (int r = t.r0; r < t.r1; ++r)
-          if (load[r] < load[best]) best = r;
-        give(ch[i], best);
-      }
-    }
+  std::sort(S.begin(), S.end(), [&](int64_t a, int64_t b) { return W[a] != W[b] ? W[a] > W[b] : a < b; });
+  std::vector<double> load(nparts, 0.0);
+  std::vector<int32_t> sub_owner(nsup, -1);
+  for (auto v : S) {
+    const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    load[r] += W[v];
+    sub_owner[v] = r;
+  }
+  // subtrees: every front below a subtree root takes the root's rank (parents after children,
+  // so walk from the top down: a front's owner is its parent's unless it is a subtree root)
+  for (int64_t s = nsup - 1; s >= 0; --s) {
+    if (sub_owner[s] >= 0) owner[s] = sub_owner[s];
+    else if (!top[s] && s_parent[s] >= 0) owner[s] = owner[s_parent[s]];
+  }
+  // top fronts (children before parents): the rank of the heaviest child
+  for (int64_t s = 0; s < nsup; ++s) {
+    if (!top[s]) continue;
+    int64_t best = -1;
+    for (int64_t e = ch_ptr[s]; e < ch_ptr[s + 1]; ++e)
+      if (best < 0 || W[ch_list[e]] > W[best]) best = ch_list[e];
+    owner[s] = best >= 0 ? owner[best] : 0;
   }
   std::vector<char> isx(nlevels, 0);
   for (int64_t s = 0; s < nsup; ++s) {
