@@ -1576,7 +1576,8 @@ hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, in
   if (ntiles <= 0) return hipSuccess;
   if (tile == 129) k_gemm128_mfma<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
   else if (tile == 128)
-    k_gemm128<<<(unsigned)(maxwg > 0 ? std::min<int64_t>(ntiles, maxwg) : ntiles), 256, 0, st>>>(tasks, ntask, ntiles);
+    k_gemm128<<<(unsigned)(maxwg > 0 ? std::min<int64_t>(ntiles, maxwg) : ntiles), 256, 0, st>>>(
+        tasks, ntask, ntiles);
   else k_gemm<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
   return hipGetLastError();
 }

@@ -171,7 +171,7 @@ struct smlu_handle {
   bool graph_failed = false;
   bool lookahead = false;     // SMLU_LOOKAHEAD=1: trailing updates beyond the next block on a side stream
   int ob = kOBDefault;        // outer block width (SMLU_OB overrides; multiple of 64)
-  int64_t t128_min = 128;     // 128x128 GEMM tiles when a launch has at least this many
+  int64_t t128_min = 512;     // 128x128 GEMM tiles when a launch has at least this many
   int64_t side_wg = 0;        // grid cap of look-ahead GEMMs (SMLU_SIDE_WG; 0 = uncapped)          // batched-LDS full-width triangular solves (SMLU_SLOW_TRSM=1: off)
   ~smlu_handle() { release_all(); }
   void release_buffers() {
