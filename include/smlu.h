@@ -58,8 +58,9 @@ typedef struct smlu_opts {
     int32_t device;       /* HIP device ordinal (default 0) */
     int32_t profile;      /* 1 = record per-kernel-class HIP events during refactor/solve */
     int64_t leaf_size;    /* nested-dissection leaf size (default 64) */
-    int32_t use_mfma;     /* 1 = fp64 MFMA (v_mfma_f64_16x16x4) for the dense Schur updates;
-                             default 0 = fp64 VALU, as the north star asks (same peak on gfx950) */
+    int32_t use_mfma;     /* 1 (default) = fp64 MFMA (v_mfma_f64_16x16x4) for the dense Schur
+                             updates of large launches; 0 = fp64 VALU tiles (env SMLU_VALU_GEMM).
+                             Bitwise-identical results; MFMA is faster on large tiles */
     int32_t reserved;
 } smlu_opts;
 

@@ -1,0 +1,158 @@
+// kernels_common.hpp — device helpers shared by the gfx950 kernel translation units
+// (kernels_front.hip, kernels_gemm.hip, kernels_solve.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdlib>
+
+#include "device.hpp"
+
+namespace smlu {
+
+#define WAVE 64
+
+__device__ __forceinline__ double wave_max_idx(double v, int& idx) {
+  // max |.| with smallest index on ties; 64-lane butterfly
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    double ov = __shfl_xor(v, o, 64);
+    int oi = __shfl_xor(idx, o, 64);
+    if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+  }
+  return v;
+}
+
+// 1/x with one Newton step on the hardware estimate (v_rcp_f64): ~3 dependent fp64 ops instead
+// of the ~10 of an IEEE division (a dependent fp64 op costs ~32 cycles on gfx950).  Used on the
+// sequential pivot and triangular-solve chains; results stay within a few ulp of division.
+__device__ __forceinline__ double recip(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  const double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  const double e2 = fma(-x, r, 1.0);
+  return fma(r, e2, r);
+}
+
+// Global-address-space views of plain pointers: loads through them compile to global_load
+// (vmcnt only) instead of flat_load, which also counts against lgkmcnt and so makes every LDS
+// wait inside a loop wait for the global prefetch as well.
+typedef __attribute__((address_space(1))) double gdbl;
+template <typename T>
+__device__ __forceinline__ __attribute__((address_space(1))) T* gbl(T* p) {
+  return (__attribute__((address_space(1))) T*)p;
+}
+
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+__device__ __forceinline__ void atomic_max_pos(double* addr, double v) {
+  // v >= 0: IEEE ordering of non-negative doubles matches their bit patterns as u64
+  atomicMax(reinterpret_cast<unsigned long long*>(addr), (unsigned long long)__double_as_longlong(v));
+}
+
+// info word per front: bit0 zero pivot, bit1 weak pivot, bits 2.. = 1 + first zero-pivot column
+__device__ __forceinline__ void publish_info(int32_t* info, int flag, int errcol) {
+  int v = *info | flag;
+  if (errcol >= 0 && (v >> 2) == 0) v |= (errcol + 1) << 2;
+  *info = v;
+}
+
+struct FrontPtrs {
+  gdbl* L;
+  gdbl* U;
+  gdbl* F;
+  int64_t M, ns, nu;
+};
+
+__device__ __forceinline__ FrontPtrs front_ptrs(const SNode& s, double* store, double* scratch) {
+  FrontPtrs f;
+  f.ns = s.ns;
+  f.nu = s.nu;
+  f.M = (int64_t)s.ns + s.nu;
+  f.L = gbl(store + s.Loff);
+  f.U = gbl(store + s.Uoff);
+  f.F = s.Foff >= 0 ? gbl(scratch + s.Foff) : nullptr;
+  return f;
+}
+
+__device__ __forceinline__ gdbl* fel(const FrontPtrs& f, int64_t i, int64_t j) {
+  if (j < f.ns) return f.L + j * f.M + i;
+  if (i < f.ns) return f.U + (j - f.ns) * f.ns + i;
+  return f.F + (j - f.ns) * f.nu + (i - f.ns);
+}
+
+// ------------------------------------------------------------------------------------
+// Blocked path, step 2: apply the panel's row permutation to every other column of the
+// front and compute the U row block  U[kb:kb+w, kb+w:M] = L_kk^{-1} A[kb:kb+w, kb+w:M].
+// One workgroup per 64 columns; columns outside the panel are numbered c in [0, M-w):
+// col = c < kb ? c : c + w.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int find_front_tile(const FrontTile* __restrict__ ft, int cnt, int64_t b) {
+  int lo = 0, hi = cnt - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (ft[mid].wg0 <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Full-width (w == W) triangular solves for one column / row held in registers, with the
+// triangle broadcast from LDS.  Each elimination step first issues all of its LDS reads, then
+// its FMAs (sched_barrier keeps the scheduler from interleaving them), so the LDS latency is
+// paid once per step instead of once per pair of FMAs.  Same operations in the same order as
+// the guarded generic loops: results are bitwise identical.
+template <int W, int LD = W, int XN = W>
+__device__ __forceinline__ void lower_unit_solve_fast(double (&x)[XN], const double* __restrict__ sT) {
+  // reads of one step in batches of at most 32 (keeps the kernel within 256 registers so that
+  // it can share a SIMD with a resident GEMM wave)
+#pragma unroll
+  for (int j = 0; j < W - 1; ++j) {
+#pragma unroll
+    for (int i0 = j + 1; i0 < W; i0 += 32) {
+      double lc[32];
+#pragma unroll
+      for (int i = i0; i < W && i < i0 + 32; ++i) lc[i - i0] = sT[j * LD + i];
+      __builtin_amdgcn_sched_barrier(0);
+      const double xj = x[j];
+#pragma unroll
+      for (int i = i0; i < W && i < i0 + 32; ++i) x[i] = fma(-lc[i - i0], xj, x[i]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// x <- x U^{-1} for a row vector x, U = sT (stored [col][row]), rd = 1/diag(U); returns max |x|
+template <int W, int LD = W, int XN = W>
+__device__ __forceinline__ double upper_right_solve_fast(double (&x)[XN], const double* __restrict__ sT,
+                                                         const double* __restrict__ rd) {
+  double gmax = 0.0;
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    x[j] = x[j] * rd[j];
+    gmax = fmax(gmax, fabs(x[j]));
+#pragma unroll
+    for (int k0 = j + 1; k0 < W; k0 += 32) {
+      double uc[32];
+#pragma unroll
+      for (int k = k0; k < W && k < k0 + 32; ++k) uc[k - k0] = sT[k * LD + j];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = k0; k < W && k < k0 + 32; ++k) x[k] = fma(-x[j], uc[k - k0], x[k]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  return gmax;
+}
+
+// Two-level blocking: inner panels (nb = 32/64 columns) are grouped in outer blocks of OB = 256
+// columns [ostart, oend).  mode 0 (inner step, panel at kb): apply the panel's row swaps to
+// every column outside the panel; TRSM only the columns inside the outer block [kb+w, oend).
+// mode 1 (outer phase, sub-panel at kb): TRSM rows [kb, kb+w) on the columns right of the
+// outer block [oend, M); no swaps (already applied).  kb comes from FrontTile.pad.
+}  // namespace smlu

@@ -1,6 +1,7 @@
-// kernels.hip — gfx950 (CDNA4) kernels of the multifrontal numeric refactorization and the
-// level-scheduled triangular solves.  No MFMA (north star): the dense parts run on the fp64
-// VALU (v_fma_f64), whose peak on MI355X equals the fp64 matrix peak (78.6 TFLOP/s).
+// kernels_front.hip — gfx950 (CDNA4) kernels of the multifrontal numeric refactorization:
+// assembly (scaling, scatter, extend-add), small fronts in LDS, and the latency-bound panel
+// chain of the blocked large-front path.  The dense Schur updates are in kernels_gemm.hip
+// (fp64 MFMA by default), the solves in kernels_solve.hip.
 //
 // Reference mapping (SharedMemSparseLU.jl):
 //   k_rowscale            UMFPACK SUM scaling behind lu(A) (src/SharedMemSparseLU.jl:74, Rs at :51)
@@ -12,91 +13,9 @@
 //   k_gemm*               Schur-complement (trailing) updates
 //   k_fwd_front, k_tri_block, k_fwd_gather   lsolve! (:349-367)
 //   k_bwd_front, k_bwd_u12                    rsolve! (:374-392)
-//   k_perm_in/k_perm_out/k_unswap             ldiv!'s scale+permute / un-permute (:318-339)
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <cstdint>
-#include <cstdlib>
-
-#include "device.hpp"
+#include "kernels_common.hpp"
 
 namespace smlu {
-
-#define WAVE 64
-
-__device__ __forceinline__ double wave_max_idx(double v, int& idx) {
-  // max |.| with smallest index on ties; 64-lane butterfly
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    double ov = __shfl_xor(v, o, 64);
-    int oi = __shfl_xor(idx, o, 64);
-    if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
-  }
-  return v;
-}
-
-// 1/x with one Newton step on the hardware estimate (v_rcp_f64): ~3 dependent fp64 ops instead
-// of the ~10 of an IEEE division (a dependent fp64 op costs ~32 cycles on gfx950).  Used on the
-// sequential pivot and triangular-solve chains; results stay within a few ulp of division.
-__device__ __forceinline__ double recip(double x) {
-  double r = __builtin_amdgcn_rcp(x);
-  const double e = fma(-x, r, 1.0);
-  r = fma(r, e, r);
-  const double e2 = fma(-x, r, 1.0);
-  return fma(r, e2, r);
-}
-
-// Global-address-space views of plain pointers: loads through them compile to global_load
-// (vmcnt only) instead of flat_load, which also counts against lgkmcnt and so makes every LDS
-// wait inside a loop wait for the global prefetch as well.
-typedef __attribute__((address_space(1))) double gdbl;
-template <typename T>
-__device__ __forceinline__ __attribute__((address_space(1))) T* gbl(T* p) {
-  return (__attribute__((address_space(1))) T*)p;
-}
-
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
-__device__ __forceinline__ void atomic_max_pos(double* addr, double v) {
-  // v >= 0: IEEE ordering of non-negative doubles matches their bit patterns as u64
-  atomicMax(reinterpret_cast<unsigned long long*>(addr), (unsigned long long)__double_as_longlong(v));
-}
-
-// info word per front: bit0 zero pivot, bit1 weak pivot, bits 2.. = 1 + first zero-pivot column
-__device__ __forceinline__ void publish_info(int32_t* info, int flag, int errcol) {
-  int v = *info | flag;
-  if (errcol >= 0 && (v >> 2) == 0) v |= (errcol + 1) << 2;
-  *info = v;
-}
-
-struct FrontPtrs {
-  gdbl* L;
-  gdbl* U;
-  gdbl* F;
-  int64_t M, ns, nu;
-};
-
-__device__ __forceinline__ FrontPtrs front_ptrs(const SNode& s, double* store, double* scratch) {
-  FrontPtrs f;
-  f.ns = s.ns;
-  f.nu = s.nu;
-  f.M = (int64_t)s.ns + s.nu;
-  f.L = gbl(store + s.Loff);
-  f.U = gbl(store + s.Uoff);
-  f.F = s.Foff >= 0 ? gbl(scratch + s.Foff) : nullptr;
-  return f;
-}
-
-__device__ __forceinline__ gdbl* fel(const FrontPtrs& f, int64_t i, int64_t j) {
-  if (j < f.ns) return f.L + j * f.M + i;
-  if (i < f.ns) return f.U + (j - f.ns) * f.ns + i;
-  return f.F + (j - f.ns) * f.nu + (i - f.ns);
-}
 
 // ------------------------------------------------------------------------------------
 // Row scaling: Rs[i] = 1/sum_j |a_ij| summed in column order (bitwise equal to the oracle).
@@ -678,75 +597,6 @@ __global__ __launch_bounds__(256) void k_laswp(const SwapTask* __restrict__ task
   }
 }
 
-// ------------------------------------------------------------------------------------
-// Blocked path, step 2: apply the panel's row permutation to every other column of the
-// front and compute the U row block  U[kb:kb+w, kb+w:M] = L_kk^{-1} A[kb:kb+w, kb+w:M].
-// One workgroup per 64 columns; columns outside the panel are numbered c in [0, M-w):
-// col = c < kb ? c : c + w.
-// ------------------------------------------------------------------------------------
-__device__ __forceinline__ int find_front_tile(const FrontTile* __restrict__ ft, int cnt, int64_t b) {
-  int lo = 0, hi = cnt - 1;
-  while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
-    if (ft[mid].wg0 <= b) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-
-// Full-width (w == W) triangular solves for one column / row held in registers, with the
-// triangle broadcast from LDS.  Each elimination step first issues all of its LDS reads, then
-// its FMAs (sched_barrier keeps the scheduler from interleaving them), so the LDS latency is
-// paid once per step instead of once per pair of FMAs.  Same operations in the same order as
-// the guarded generic loops: results are bitwise identical.
-template <int W, int LD = W, int XN = W>
-__device__ __forceinline__ void lower_unit_solve_fast(double (&x)[XN], const double* __restrict__ sT) {
-  // reads of one step in batches of at most 32 (keeps the kernel within 256 registers so that
-  // it can share a SIMD with a resident GEMM wave)
-#pragma unroll
-  for (int j = 0; j < W - 1; ++j) {
-#pragma unroll
-    for (int i0 = j + 1; i0 < W; i0 += 32) {
-      double lc[32];
-#pragma unroll
-      for (int i = i0; i < W && i < i0 + 32; ++i) lc[i - i0] = sT[j * LD + i];
-      __builtin_amdgcn_sched_barrier(0);
-      const double xj = x[j];
-#pragma unroll
-      for (int i = i0; i < W && i < i0 + 32; ++i) x[i] = fma(-lc[i - i0], xj, x[i]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-}
-
-// x <- x U^{-1} for a row vector x, U = sT (stored [col][row]), rd = 1/diag(U); returns max |x|
-template <int W, int LD = W, int XN = W>
-__device__ __forceinline__ double upper_right_solve_fast(double (&x)[XN], const double* __restrict__ sT,
-                                                         const double* __restrict__ rd) {
-  double gmax = 0.0;
-#pragma unroll
-  for (int j = 0; j < W; ++j) {
-    x[j] = x[j] * rd[j];
-    gmax = fmax(gmax, fabs(x[j]));
-#pragma unroll
-    for (int k0 = j + 1; k0 < W; k0 += 32) {
-      double uc[32];
-#pragma unroll
-      for (int k = k0; k < W && k < k0 + 32; ++k) uc[k - k0] = sT[k * LD + j];
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int k = k0; k < W && k < k0 + 32; ++k) x[k] = fma(-x[j], uc[k - k0], x[k]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  return gmax;
-}
-
-// Two-level blocking: inner panels (nb = 32/64 columns) are grouped in outer blocks of OB = 256
-// columns [ostart, oend).  mode 0 (inner step, panel at kb): apply the panel's row swaps to
-// every column outside the panel; TRSM only the columns inside the outer block [kb+w, oend).
-// mode 1 (outer phase, sub-panel at kb): TRSM rows [kb, kb+w) on the columns right of the
-// outer block [oend, M); no swaps (already applied).  kb comes from FrontTile.pad.
 template <int W>
 __global__ __launch_bounds__(256) void k_trsm_u(const FrontTile* __restrict__ ft, int nft, int OB,
                                                 int mode, const SNode* __restrict__ sn,
@@ -940,547 +790,6 @@ __global__ __launch_bounds__(256) void k_step_trsm(const FrontTile* __restrict__
   }
 }
 
-// ------------------------------------------------------------------------------------
-// Dense update C -= A*B (fp64 VALU).  64x64 output tile per 256-thread workgroup, 4x4 per
-// thread, K staged through LDS in slices of 16 with register prefetch of the next slice.
-// ------------------------------------------------------------------------------------
-__device__ __forceinline__ int find_gemm_task(const GemmTask* __restrict__ t, int cnt, int64_t b) {
-  int lo = 0, hi = cnt - 1;
-  while (lo < hi) {
-    int mid = (lo + hi + 1) >> 1;
-    if (t[mid].tile0 <= b) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
-
-#define GBM 64
-#define GBN 64
-#define GBK 16
-__global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks, int ntask) {
-  __shared__ double As[2][GBK][GBM + 2];
-  __shared__ double Bs[2][GBK][GBN + 2];
-  const int64_t b = blockIdx.x;
-  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
-  const gdbl* gA = gbl(t.A);
-  const gdbl* gB = gbl(t.B);
-  gdbl* gC = gbl(t.C);
-  const int64_t tl = b - t.tile0;
-  const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
-  const int m0 = tm * GBM, n0 = tn * GBN;
-  const int tid = threadIdx.x;
-  const int tx = tid & 15, ty = tid >> 4;  // 16 x 16 threads, 4x4 each
-  double acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
-  // load mapping: A slice GBM x GBK: thread -> (row = tid & 63, kk = (tid >> 6) + 4*r), r<4
-  //               B slice GBK x GBN: thread -> (kk = tid & 15, col = (tid >> 4) + 16*r), r<4
-  const int ar = tid & 63, ak = tid >> 6;
-  const int bk = tid & 15, bc = tid >> 4;
-  double ra[4], rb[4];
-  const int K = t.k;
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      int kk = ak + 4 * r;
-      int row = m0 + ar;
-      ra[r] = (row < t.m && k0 + kk < K) ? gA[(int64_t)(k0 + kk) * t.lda + row] : 0.0;
-      int col = n0 + bc + 16 * r;
-      rb[r] = (col < t.n && k0 + bk < K) ? gB[(int64_t)col * t.ldb + k0 + bk] : 0.0;
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      As[buf][ak + 4 * r][ar] = ra[r];
-      Bs[buf][bk][bc + 16 * r] = rb[r];
-    }
-  };
-  int nk = (K + GBK - 1) / GBK;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * GBK);
-#pragma unroll 4
-    for (int kk = 0; kk < GBK; ++kk) {
-      double a[4], bb[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = As[cur][kk][tx + 16 * i];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bb[j] = Bs[cur][kk][ty + 16 * j];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], bb[j], acc[i][j]);
-    }
-    if (kt + 1 < nk) sstore(cur ^ 1);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    int col = n0 + ty + 16 * j;
-    if (col >= t.n) continue;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      int row = m0 + tx + 16 * i;
-      if (row < t.m) {
-        gdbl* c = gC + (int64_t)col * t.ldc + row;
-        *c = *c - acc[i][j];
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Dense update C -= A*B, large tiles: 128x128 output tile per 256-thread workgroup, 8x8
-// accumulators per thread (128 VGPRs), K staged through double-buffered LDS in slices of 16
-// with the next slice prefetched into registers.  Each thread owns rows {2tx,2tx+1}+32i and
-// columns {2ty,2ty+1}+32j so every fragment read is one conflict-free ds_read_b128.
-// Per k: 8 ds_read_b128 feed 64 v_fma_f64 (0.25 doubles of LDS per FMA).
-// ------------------------------------------------------------------------------------
-#define HBM_ 128
-#define HBK_ 16
-#define HLDB_ (HBM_ + 2)
-#ifndef KK_UNROLL
-#define KK_UNROLL 2
-#endif
-__device__ __forceinline__ void gemm128_tile(const GemmTask* __restrict__ tasks, int ntask, int64_t b,
-                                             double (&As)[2][HBK_][HBM_], double (&Bs)[2][HBK_][HLDB_]) {
-  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
-  const gdbl* gA = gbl(t.A);
-  const gdbl* gB = gbl(t.B);
-  gdbl* gC = gbl(t.C);
-  const int64_t tl = b - t.tile0;
-  const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
-  const int m0 = tm * HBM_, n0 = tn * HBM_;
-  const int tid = threadIdx.x;
-  const int tx = tid & 15, ty = tid >> 4;
-  double acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = 0.0;
-  // global->register mapping: A: row = tid & 127, k = (tid >> 7) + 2r ; B: k = tid & 15, col = (tid >> 4) + 16r
-  const int ar = tid & 127, ak = tid >> 7;
-  const int bk = tid & 15, bc = tid >> 4;
-  const int K = t.k;
-  const int arow = m0 + ar;
-  const bool arow_ok = arow < t.m;
-  const gdbl* Ap = gA + arow;
-  double ra[8], rb[8];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int kk = k0 + ak + 2 * r;
-      ra[r] = (arow_ok && kk < K) ? Ap[(int64_t)kk * t.lda] : 0.0;
-      const int col = n0 + bc + 16 * r;
-      rb[r] = (col < t.n && k0 + bk < K) ? gB[(int64_t)col * t.ldb + k0 + bk] : 0.0;
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      As[buf][ak + 2 * r][ar] = ra[r];
-      Bs[buf][bk][bc + 16 * r] = rb[r];
-    }
-  };
-  const int nk = (K + HBK_ - 1) / HBK_;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * HBK_);
-#pragma unroll KK_UNROLL
-    for (int kk = 0; kk < HBK_; ++kk) {
-      double a[8], bb[8];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const double2 v = *reinterpret_cast<const double2*>(&As[cur][kk][2 * tx + 32 * i]);
-        a[2 * i] = v.x;
-        a[2 * i + 1] = v.y;
-        const double2 w = *reinterpret_cast<const double2*>(&Bs[cur][kk][2 * ty + 32 * i]);
-        bb[2 * i] = w.x;
-        bb[2 * i + 1] = w.y;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = fma(a[i], bb[j], acc[i][j]);
-    }
-    if (kt + 1 < nk) sstore(cur ^ 1);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int col = n0 + 2 * ty + 32 * (j >> 1) + (j & 1);
-    if (col >= t.n) continue;
-    gdbl* Cc = gC + (int64_t)col * t.ldc;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = m0 + 2 * tx + 32 * (i >> 1) + (i & 1);
-      if (row < t.m) Cc[row] = Cc[row] - acc[i][j];
-    }
-  }
-}
-
-// Tiles b = blockIdx.x + i * gridDim.x: a grid smaller than the tile count leaves CUs free for
-// the latency-bound panel chain running concurrently on the other stream (look-ahead).
-__global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__ tasks, int ntask,
-                                                    int64_t ntiles) {
-  __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
-  __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
-  for (int64_t b = blockIdx.x; b < ntiles; b += gridDim.x) {
-    gemm128_tile(tasks, ntask, b, As, Bs);
-    __syncthreads();
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Optional fp64 MFMA variant of the same 128x128 tile (opts.use_mfma; default off: the north
-// star asks for no MFMA).  v_mfma_f64_16x16x4_f64; each wave owns a 64x64 quadrant = 4x4
-// blocks.  The product is formed as C^T = B^T A^T so that the accumulator's lane index runs
-// along C's rows (column-major C stays coalesced): lane l of block (bi,bj) holds
-// C[row = 16 bi + (l & 15)][col = 16 bj + (l >> 4) + 4 r], r = 0..3.
-// ------------------------------------------------------------------------------------
-typedef double v4d __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restrict__ tasks, int ntask) {
-  __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
-  __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
-  const int64_t b = blockIdx.x;
-  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
-  const gdbl* gA = gbl(t.A);
-  const gdbl* gB = gbl(t.B);
-  gdbl* gC = gbl(t.C);
-  const int64_t tl = b - t.tile0;
-  const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
-  const int m0 = tm * HBM_, n0 = tn * HBM_;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wr = (wv & 1) * 64, wc = (wv >> 1) * 64;   // wave quadrant (rows, cols)
-  v4d acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (v4d){0.0, 0.0, 0.0, 0.0};
-  const int ar = tid & 127, ak = tid >> 7;
-  const int bk = tid & 15, bc = tid >> 4;
-  const int K = t.k;
-  const int arow = m0 + ar;
-  const bool arow_ok = arow < t.m;
-  const gdbl* Ap = gA + arow;
-  double ra[8], rb[8];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int kk = k0 + ak + 2 * r;
-      ra[r] = (arow_ok && kk < K) ? Ap[(int64_t)kk * t.lda] : 0.0;
-      const int col = n0 + bc + 16 * r;
-      rb[r] = (col < t.n && k0 + bk < K) ? gB[(int64_t)col * t.ldb + k0 + bk] : 0.0;
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      As[buf][ak + 2 * r][ar] = ra[r];
-      Bs[buf][bk][bc + 16 * r] = rb[r];
-    }
-  };
-  const int nk = (K + HBK_ - 1) / HBK_;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  const int li = lane & 15, lk = lane >> 4;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * HBK_);
-#pragma unroll
-    for (int kq = 0; kq < HBK_ / 4; ++kq) {
-      const int k = kq * 4 + lk;
-      double fa[4], fb[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = As[cur][k][wr + 16 * i + li];   // A[row][k]
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = Bs[cur][k][wc + 16 * j + li];   // B[k][col]
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[j], fa[i], acc[i][j], 0, 0, 0);
-    }
-    if (kt + 1 < nk) sstore(cur ^ 1);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = m0 + wr + 16 * i + li;
-    if (row >= t.m) continue;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int col = n0 + wc + 16 * j + lk + 4 * r;
-        if (col < t.n) {
-          gdbl* c = gC + (int64_t)col * t.ldc + row;
-          *c = *c - acc[i][j][r];
-        }
-      }
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Solves.  Front vectors v_s (M doubles) live in vbuf[voff[s]].
-// Forward (L): gather own rows + children's update vectors, apply the front's row
-// permutation, unit-lower solve of the diagonal block in 64-column blocks (one wave does
-// the block by shuffles, all waves apply the block to the rows below), leave
-// v[ns:M) = update vector for the parent.
-// ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_fwd_front(const int32_t* __restrict__ list,
-                                                   const SNode* __restrict__ sn,
-                                                   const int32_t* __restrict__ chlist,
-                                                   const int32_t* __restrict__ relmap,
-                                                   const int32_t* __restrict__ rowperm,
-                                                   const double* __restrict__ store,
-                                                   double* __restrict__ x,
-                                                   double* __restrict__ vbuf) {
-  __shared__ double xs[64];
-  const SNode s = sn[list[blockIdx.x]];
-  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
-  double* v = vbuf + s.voff;
-  double* xo = x + s.first;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int64_t i = tid; i < M; i += 256) v[i] = i < ns ? xo[i] : 0.0;
-  __syncthreads();
-  for (int c = s.chbeg; c < s.chend; ++c) {
-    const SNode ch = sn[chlist[c]];
-    const double* u = vbuf + ch.voff + ch.ns;
-    const int32_t* rm = relmap + ch.rowptr;
-    for (int64_t i = tid; i < ch.nu; i += 256) v[rm[i]] += u[i];
-    __syncthreads();
-  }
-  // permuted diagonal-block right-hand side -> x positions (owned by this front)
-  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[rowperm[s.first + i]];
-  __syncthreads();
-  for (int64_t i = tid; i < ns; i += 256) v[i] = xo[i];
-  __syncthreads();
-  const double* Lp = store + s.Loff;
-  for (int64_t jb = 0; jb < ns; jb += 64) {
-    const int bw = (int)min<int64_t>(64, ns - jb);
-    if (wv == 0) {
-      double xi = lane < bw ? v[jb + lane] : 0.0;
-      for (int j = 0; j < bw; ++j) {
-        double xj = __shfl(xi, j, 64);
-        if (lane > j && lane < bw) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
-      }
-      if (lane < bw) {
-        xs[lane] = xi;
-        v[jb + lane] = xi;
-      }
-    }
-    __syncthreads();
-    for (int64_t i = jb + bw + tid; i < M; i += 256) {
-      double acc = 0.0;
-      for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
-      v[i] -= acc;
-    }
-    __syncthreads();
-  }
-  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[i];
-}
-
-// Backward (U): x_s -= U12 * x[R_s]; then upper solve of the diagonal block from the bottom.
-__global__ __launch_bounds__(256) void k_bwd_front(const int32_t* __restrict__ list,
-                                                   const SNode* __restrict__ sn,
-                                                   const int32_t* __restrict__ rows,
-                                                   const double* __restrict__ store,
-                                                   double* __restrict__ x,
-                                                   double* __restrict__ vbuf) {
-  __shared__ double xs[64];
-  const SNode s = sn[list[blockIdx.x]];
-  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns, nu = s.nu;
-  double* v = vbuf + s.voff;
-  double* xo = x + s.first;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int32_t* R = rows + s.rowptr;
-  for (int64_t i = tid; i < nu; i += 256) v[ns + i] = x[R[i]];
-  __syncthreads();
-  const double* U12 = store + s.Uoff;
-  for (int64_t i = tid; i < ns; i += 256) {
-    double acc = 0.0;
-    for (int64_t j = 0; j < nu; ++j) acc = fma(U12[j * ns + i], v[ns + j], acc);
-    v[i] = xo[i] - acc;
-  }
-  __syncthreads();
-  const double* Lp = store + s.Loff;  // U11 in the upper triangle of the L panel
-  for (int64_t jb = ((ns - 1) / 64) * 64; jb >= 0; jb -= 64) {
-    const int bw = (int)min<int64_t>(64, ns - jb);
-    if (wv == 0) {
-      double xi = lane < bw ? v[jb + lane] : 0.0;
-      for (int j = bw - 1; j >= 0; --j) {
-        if (lane == j) xi = xi * recip(Lp[(jb + j) * M + jb + j]);
-        double xj = __shfl(xi, j, 64);
-        if (lane < j) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
-      }
-      if (lane < bw) {
-        xs[lane] = xi;
-        v[jb + lane] = xi;
-      }
-    }
-    __syncthreads();
-    for (int64_t i = tid; i < jb; i += 256) {
-      double acc = 0.0;
-      for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
-      v[i] -= acc;
-    }
-    __syncthreads();
-  }
-  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[i];
-}
-
-// ------------------------------------------------------------------------------------
-// Solves for large fronts (ns > 256): the diagonal block sweep is split over workgroups.
-// k_fwd_gather: front vector = own rows + children's update vectors, row permutation.
-// k_fwd_block (step t, jb = 64t): every workgroup re-solves the 64x64 unit-lower diagonal
-//   block from v (read-only in this launch), applies it to its 256-row chunk below; chunk 0
-//   publishes the solved block into x.  k_bwd_u12: x_s -= U12 x[R_s] by row chunks.
-// k_bwd_block: same as k_fwd_block for U11 from the bottom block up.
-// ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_fwd_gather(const int32_t* __restrict__ list,
-                                                    const SNode* __restrict__ sn,
-                                                    const int32_t* __restrict__ chlist,
-                                                    const int32_t* __restrict__ relmap,
-                                                    const int32_t* __restrict__ rowperm,
-                                                    double* __restrict__ x, double* __restrict__ vbuf) {
-  const SNode s = sn[list[blockIdx.x]];
-  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
-  double* v = vbuf + s.voff;
-  double* xo = x + s.first;
-  const int tid = threadIdx.x;
-  for (int64_t i = tid; i < M; i += 256) v[i] = i < ns ? xo[i] : 0.0;
-  __syncthreads();
-  for (int c = s.chbeg; c < s.chend; ++c) {
-    const SNode ch = sn[chlist[c]];
-    const double* u = vbuf + ch.voff + ch.ns;
-    const int32_t* rm = relmap + ch.rowptr;
-    for (int64_t i = tid; i < ch.nu; i += 256) v[rm[i]] += u[i];
-    __syncthreads();
-  }
-  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[rowperm[s.first + i]];
-  __syncthreads();
-  for (int64_t i = tid; i < ns; i += 256) v[i] = xo[i];
-}
-
-template <bool UPPER>
-__global__ __launch_bounds__(256) void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step,
-                                                   const SNode* __restrict__ sn,
-                                                   const double* __restrict__ store,
-                                                   double* __restrict__ x, double* __restrict__ vbuf) {
-  __shared__ double xs[64];
-  const int64_t b = blockIdx.x;
-  const int fi = find_front_tile(ft, nft, b);
-  const SNode s = sn[ft[fi].s];
-  const int64_t chunk = b - ft[fi].wg0;
-  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
-  const int64_t nblk = (ns + 63) / 64;
-  const int64_t jb = UPPER ? (nblk - 1 - step) * 64 : (int64_t)step * 64;
-  const int bw = (int)min<int64_t>(64, ns - jb);
-  double* v = vbuf + s.voff;
-  const double* Lp = store + s.Loff;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (wv == 0) {
-    double xi = lane < bw ? v[jb + lane] : 0.0;
-    if (!UPPER) {
-      for (int j = 0; j < bw; ++j) {
-        double xj = __shfl(xi, j, 64);
-        if (lane > j && lane < bw) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
-      }
-    } else {
-      for (int j = bw - 1; j >= 0; --j) {
-        if (lane == j) xi = xi * recip(Lp[(jb + j) * M + jb + j]);
-        double xj = __shfl(xi, j, 64);
-        if (lane < j) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
-      }
-    }
-    if (lane < bw) {
-      xs[lane] = xi;
-      if (chunk == 0) x[s.first + jb + lane] = xi;
-    }
-  }
-  __syncthreads();
-  // rows updated by this chunk: forward -> [jb+bw, M), backward -> [0, jb)
-  const int64_t r0 = UPPER ? chunk * 256 : jb + bw + chunk * 256;
-  const int64_t r1 = UPPER ? jb : M;
-  const int64_t i = r0 + tid;
-  if (i < r1 && i < r0 + 256) {
-    double acc = 0.0;
-    for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
-    v[i] -= acc;
-  }
-}
-
-// x_s[i] (in v) = x[first+i] - sum_j U12[i,j] * x[R_j], 256 rows per workgroup
-__global__ __launch_bounds__(256) void k_bwd_u12(const FrontTile* __restrict__ ft, int nft,
-                                                 const SNode* __restrict__ sn,
-                                                 const int32_t* __restrict__ rows,
-                                                 const double* __restrict__ store,
-                                                 const double* __restrict__ x,
-                                                 double* __restrict__ vbuf) {
-  __shared__ double xr[256];
-  const int64_t b = blockIdx.x;
-  const int fi = find_front_tile(ft, nft, b);
-  const SNode s = sn[ft[fi].s];
-  const int64_t chunk = b - ft[fi].wg0;
-  const int64_t ns = s.ns, nu = s.nu;
-  const int32_t* R = rows + s.rowptr;
-  const double* U12 = store + s.Uoff;
-  const int tid = threadIdx.x;
-  const int64_t i = chunk * 256 + tid;
-  double acc = 0.0;
-  for (int64_t j0 = 0; j0 < nu; j0 += 256) {
-    __syncthreads();
-    if (j0 + tid < nu) xr[tid] = x[R[j0 + tid]];
-    __syncthreads();
-    const int cnt = (int)min<int64_t>(256, nu - j0);
-    if (i < ns)
-      for (int j = 0; j < cnt; ++j) acc = fma(U12[(j0 + j) * ns + i], xr[j], acc);
-  }
-  if (i < ns) vbuf[s.voff + i] = x[s.first + i] - acc;
-}
-
-// wrk[i] = Rs[p0[i]] * b[p0[i]]
-__global__ void k_perm_in(int64_t n, const int64_t* __restrict__ p0, const double* __restrict__ Rs,
-                          const double* __restrict__ b, double* __restrict__ wrk) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    int64_t r = p0[i];
-    wrk[i] = Rs[r] * b[r];
-  }
-}
-// x[q[i]] = wrk[i]
-__global__ void k_perm_out(int64_t n, const int64_t* __restrict__ q, const double* __restrict__ wrk,
-                           double* __restrict__ x) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) x[q[i]] = wrk[i];
-}
-// multi-GPU: x[q[i]] = wrk[i] on the rows this rank owns, 0 elsewhere (summed over ranks)
-__global__ void k_perm_out_masked(int64_t n, const int64_t* __restrict__ q, const int8_t* __restrict__ own,
-                                  const double* __restrict__ wrk, double* __restrict__ x) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) x[q[i]] = own[i] ? wrk[i] : 0.0;
-}
-// final order -> pre-swap positions: out[first + rowperm[first+i]] = in[first+i]
-__global__ void k_unswap(int64_t n, const int64_t* __restrict__ pos_first,
-                         const int32_t* __restrict__ rowperm, const double* __restrict__ in,
-                         double* __restrict__ out) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    int64_t f = pos_first[i];
-    out[f + rowperm[i]] = in[i];
-  }
-}
 
 // ------------------------------------------------------------------------------------
 // Host-side launch wrappers (called from smlu.cpp)
@@ -1569,69 +878,6 @@ hipError_t launch_trsm_u(hipStream_t st, int64_t nwg, const FrontTile* ft, int n
                          int64_t swap_stride) {
   if (nwg <= 0) return hipSuccess;
   k_trsm_u<64><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, OB, mode, sn, store, scratch, swaps, swap_stride);
-  return hipGetLastError();
-}
-hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask, int tile,
-                       int64_t maxwg) {
-  if (ntiles <= 0) return hipSuccess;
-  if (tile == 129) k_gemm128_mfma<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
-  else if (tile == 128)
-    k_gemm128<<<(unsigned)(maxwg > 0 ? std::min<int64_t>(ntiles, maxwg) : ntiles), 256, 0, st>>>(
-        tasks, ntask, ntiles);
-  else k_gemm<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
-  return hipGetLastError();
-}
-hipError_t launch_fwd(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
-                      const int32_t* chlist, const int32_t* relmap, const int32_t* rowperm,
-                      const double* store, double* x, double* vbuf) {
-  if (cnt <= 0) return hipSuccess;
-  k_fwd_front<<<cnt, 256, 0, st>>>(list, sn, chlist, relmap, rowperm, store, x, vbuf);
-  return hipGetLastError();
-}
-hipError_t launch_bwd(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
-                      const int32_t* rows, const double* store, double* x, double* vbuf) {
-  if (cnt <= 0) return hipSuccess;
-  k_bwd_front<<<cnt, 256, 0, st>>>(list, sn, rows, store, x, vbuf);
-  return hipGetLastError();
-}
-hipError_t launch_fwd_gather(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
-                             const int32_t* chlist, const int32_t* relmap, const int32_t* rowperm,
-                             double* x, double* vbuf) {
-  if (cnt <= 0) return hipSuccess;
-  k_fwd_gather<<<cnt, 256, 0, st>>>(list, sn, chlist, relmap, rowperm, x, vbuf);
-  return hipGetLastError();
-}
-hipError_t launch_tri_block(hipStream_t st, bool upper, int64_t nwg, const FrontTile* ft, int nft,
-                            int step, const SNode* sn, const double* store, double* x, double* vbuf) {
-  if (nwg <= 0) return hipSuccess;
-  if (upper) k_tri_block<true><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, x, vbuf);
-  else k_tri_block<false><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, x, vbuf);
-  return hipGetLastError();
-}
-hipError_t launch_bwd_u12(hipStream_t st, int64_t nwg, const FrontTile* ft, int nft, const SNode* sn,
-                          const int32_t* rows, const double* store, const double* x, double* vbuf) {
-  if (nwg <= 0) return hipSuccess;
-  k_bwd_u12<<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sn, rows, store, x, vbuf);
-  return hipGetLastError();
-}
-hipError_t launch_perm_in(hipStream_t st, int64_t n, const int64_t* p0, const double* Rs,
-                          const double* b, double* wrk) {
-  k_perm_in<<<nblk(n, 256), 256, 0, st>>>(n, p0, Rs, b, wrk);
-  return hipGetLastError();
-}
-hipError_t launch_perm_out_masked(hipStream_t st, int64_t n, const int64_t* q, const int8_t* own,
-                                  const double* wrk, double* x) {
-  if (n <= 0) return hipSuccess;
-  k_perm_out_masked<<<nblk(n, 256), 256, 0, st>>>(n, q, own, wrk, x);
-  return hipGetLastError();
-}
-hipError_t launch_perm_out(hipStream_t st, int64_t n, const int64_t* q, const double* wrk, double* x) {
-  k_perm_out<<<nblk(n, 256), 256, 0, st>>>(n, q, wrk, x);
-  return hipGetLastError();
-}
-hipError_t launch_unswap(hipStream_t st, int64_t n, const int64_t* pos_first, const int32_t* rowperm,
-                         const double* in, double* out) {
-  k_unswap<<<nblk(n, 256), 256, 0, st>>>(n, pos_first, rowperm, in, out);
   return hipGetLastError();
 }
 

@@ -1,0 +1,340 @@
+// kernels_gemm.hip — dense fp64 Schur-complement updates C -= A*B (VALU 64/128 tiles, MFMA 128 tile).
+#include "kernels_common.hpp"
+
+namespace smlu {
+
+// ------------------------------------------------------------------------------------
+// Dense update C -= A*B (fp64 VALU).  64x64 output tile per 256-thread workgroup, 4x4 per
+// thread, K staged through LDS in slices of 16 with register prefetch of the next slice.
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int find_gemm_task(const GemmTask* __restrict__ t, int cnt, int64_t b) {
+  int lo = 0, hi = cnt - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (t[mid].tile0 <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+#define GBM 64
+#define GBN 64
+#define GBK 16
+__global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks, int ntask) {
+  __shared__ double As[2][GBK][GBM + 2];
+  __shared__ double Bs[2][GBK][GBN + 2];
+  const int64_t b = blockIdx.x;
+  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+  const gdbl* gA = gbl(t.A);
+  const gdbl* gB = gbl(t.B);
+  gdbl* gC = gbl(t.C);
+  const int64_t tl = b - t.tile0;
+  const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int tid = threadIdx.x;
+  const int tx = tid & 15, ty = tid >> 4;  // 16 x 16 threads, 4x4 each
+  double acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+  // load mapping: A slice GBM x GBK: thread -> (row = tid & 63, kk = (tid >> 6) + 4*r), r<4
+  //               B slice GBK x GBN: thread -> (kk = tid & 15, col = (tid >> 4) + 16*r), r<4
+  const int ar = tid & 63, ak = tid >> 6;
+  const int bk = tid & 15, bc = tid >> 4;
+  double ra[4], rb[4];
+  const int K = t.k;
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int kk = ak + 4 * r;
+      int row = m0 + ar;
+      ra[r] = (row < t.m && k0 + kk < K) ? gA[(int64_t)(k0 + kk) * t.lda + row] : 0.0;
+      int col = n0 + bc + 16 * r;
+      rb[r] = (col < t.n && k0 + bk < K) ? gB[(int64_t)col * t.ldb + k0 + bk] : 0.0;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      As[buf][ak + 4 * r][ar] = ra[r];
+      Bs[buf][bk][bc + 16 * r] = rb[r];
+    }
+  };
+  int nk = (K + GBK - 1) / GBK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * GBK);
+#pragma unroll 4
+    for (int kk = 0; kk < GBK; ++kk) {
+      double a[4], bb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = As[cur][kk][tx + 16 * i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bb[j] = Bs[cur][kk][ty + 16 * j];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], bb[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  // epilogue: every C load issued before any store (the compiler cannot reorder a load past a
+  // possibly aliasing store, so an interleaved read-modify-write pays one memory round trip
+  // per element)
+  double cv[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + ty + 16 * j;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + tx + 16 * i;
+      cv[i][j] = (col < t.n && row < t.m) ? gC[(int64_t)col * t.ldc + row] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + ty + 16 * j;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + tx + 16 * i;
+      if (col < t.n && row < t.m) gC[(int64_t)col * t.ldc + row] = cv[i][j] - acc[i][j];
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Dense update C -= A*B, large tiles: 128x128 output tile per 256-thread workgroup, 8x8
+// accumulators per thread (128 VGPRs), K staged through double-buffered LDS in slices of 16
+// with the next slice prefetched into registers.  Each thread owns rows {2tx,2tx+1}+32i and
+// columns {2ty,2ty+1}+32j so every fragment read is one conflict-free ds_read_b128.
+// Per k: 8 ds_read_b128 feed 64 v_fma_f64 (0.25 doubles of LDS per FMA).
+// ------------------------------------------------------------------------------------
+#define HBM_ 128
+#define HBK_ 16
+#define HLDB_ (HBM_ + 2)
+#ifndef KK_UNROLL
+#define KK_UNROLL 2
+#endif
+__device__ __forceinline__ void gemm128_tile(const GemmTask* __restrict__ tasks, int ntask, int64_t b,
+                                             double (&As)[2][HBK_][HBM_], double (&Bs)[2][HBK_][HLDB_]) {
+  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+  const gdbl* gA = gbl(t.A);
+  const gdbl* gB = gbl(t.B);
+  gdbl* gC = gbl(t.C);
+  const int64_t tl = b - t.tile0;
+  const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
+  const int m0 = tm * HBM_, n0 = tn * HBM_;
+  const int tid = threadIdx.x;
+  const int tx = tid & 15, ty = tid >> 4;
+  double acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0.0;
+  // global->register mapping: A: row = tid & 127, k = (tid >> 7) + 2r ; B: k = tid & 15, col = (tid >> 4) + 16r
+  const int ar = tid & 127, ak = tid >> 7;
+  const int bk = tid & 15, bc = tid >> 4;
+  const int K = t.k;
+  const int arow = m0 + ar;
+  const bool arow_ok = arow < t.m;
+  const gdbl* Ap = gA + arow;
+  double ra[8], rb[8];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int kk = k0 + ak + 2 * r;
+      ra[r] = (arow_ok && kk < K) ? Ap[(int64_t)kk * t.lda] : 0.0;
+      const int col = n0 + bc + 16 * r;
+      rb[r] = (col < t.n && k0 + bk < K) ? gB[(int64_t)col * t.ldb + k0 + bk] : 0.0;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      As[buf][ak + 2 * r][ar] = ra[r];
+      Bs[buf][bk][bc + 16 * r] = rb[r];
+    }
+  };
+  const int nk = (K + HBK_ - 1) / HBK_;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * HBK_);
+#pragma unroll KK_UNROLL
+    for (int kk = 0; kk < HBK_; ++kk) {
+      double a[8], bb[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double2 v = *reinterpret_cast<const double2*>(&As[cur][kk][2 * tx + 32 * i]);
+        a[2 * i] = v.x;
+        a[2 * i + 1] = v.y;
+        const double2 w = *reinterpret_cast<const double2*>(&Bs[cur][kk][2 * ty + 32 * i]);
+        bb[2 * i] = w.x;
+        bb[2 * i + 1] = w.y;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = fma(a[i], bb[j], acc[i][j]);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  // epilogue in 4 batches of 2 columns: 16 C loads in flight, then 16 stores
+#pragma unroll
+  for (int jb = 0; jb < 8; jb += 2) {
+    double cv[2][8];
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = jb + jj;
+      const int col = n0 + 2 * ty + 32 * (j >> 1) + (j & 1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = m0 + 2 * tx + 32 * (i >> 1) + (i & 1);
+        cv[jj][i] = (col < t.n && row < t.m) ? gC[(int64_t)col * t.ldc + row] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = jb + jj;
+      const int col = n0 + 2 * ty + 32 * (j >> 1) + (j & 1);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int row = m0 + 2 * tx + 32 * (i >> 1) + (i & 1);
+        if (col < t.n && row < t.m) gC[(int64_t)col * t.ldc + row] = cv[jj][i] - acc[i][j];
+      }
+    }
+  }
+}
+
+// Tiles b = blockIdx.x + i * gridDim.x: a grid smaller than the tile count leaves CUs free for
+// the latency-bound panel chain running concurrently on the other stream (look-ahead).
+__global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__ tasks, int ntask,
+                                                    int64_t ntiles) {
+  __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
+  __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
+  for (int64_t b = blockIdx.x; b < ntiles; b += gridDim.x) {
+    gemm128_tile(tasks, ntask, b, As, Bs);
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Optional fp64 MFMA variant of the same 128x128 tile (opts.use_mfma; default off: the north
+// star asks for no MFMA).  v_mfma_f64_16x16x4_f64; each wave owns a 64x64 quadrant = 4x4
+// blocks.  The product is formed as C^T = B^T A^T so that the accumulator's lane index runs
+// along C's rows (column-major C stays coalesced): lane l of block (bi,bj) holds
+// C[row = 16 bi + (l & 15)][col = 16 bj + (l >> 4) + 4 r], r = 0..3.
+// ------------------------------------------------------------------------------------
+typedef double v4d __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restrict__ tasks, int ntask) {
+  __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
+  __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
+  const int64_t b = blockIdx.x;
+  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+  const gdbl* gA = gbl(t.A);
+  const gdbl* gB = gbl(t.B);
+  gdbl* gC = gbl(t.C);
+  const int64_t tl = b - t.tile0;
+  const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
+  const int m0 = tm * HBM_, n0 = tn * HBM_;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = (wv & 1) * 64, wc = (wv >> 1) * 64;   // wave quadrant (rows, cols)
+  v4d acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (v4d){0.0, 0.0, 0.0, 0.0};
+  const int ar = tid & 127, ak = tid >> 7;
+  const int bk = tid & 15, bc = tid >> 4;
+  const int K = t.k;
+  const int arow = m0 + ar;
+  const bool arow_ok = arow < t.m;
+  const gdbl* Ap = gA + arow;
+  double ra[8], rb[8];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int kk = k0 + ak + 2 * r;
+      ra[r] = (arow_ok && kk < K) ? Ap[(int64_t)kk * t.lda] : 0.0;
+      const int col = n0 + bc + 16 * r;
+      rb[r] = (col < t.n && k0 + bk < K) ? gB[(int64_t)col * t.ldb + k0 + bk] : 0.0;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      As[buf][ak + 2 * r][ar] = ra[r];
+      Bs[buf][bk][bc + 16 * r] = rb[r];
+    }
+  };
+  const int nk = (K + HBK_ - 1) / HBK_;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  const int li = lane & 15, lk = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * HBK_);
+#pragma unroll
+    for (int kq = 0; kq < HBK_ / 4; ++kq) {
+      const int k = kq * 4 + lk;
+      double fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = As[cur][k][wr + 16 * i + li];   // A[row][k]
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = Bs[cur][k][wc + 16 * j + li];   // B[k][col]
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  // epilogue per 16-row block: its 16 C loads in flight, then 16 stores
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = m0 + wr + 16 * i + li;
+    double cv[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = n0 + wc + 16 * j + lk + 4 * r;
+        cv[j][r] = (row < t.m && col < t.n) ? gC[(int64_t)col * t.ldc + row] : 0.0;
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = n0 + wc + 16 * j + lk + 4 * r;
+        if (row < t.m && col < t.n) gC[(int64_t)col * t.ldc + row] = cv[j][r] - acc[i][j][r];
+      }
+  }
+}
+
+
+// ------------------------------------------------------------------------------------
+// Host-side launch wrappers (called from smlu.cpp)
+// ------------------------------------------------------------------------------------
+hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask, int tile,
+                       int64_t maxwg) {
+  if (ntiles <= 0) return hipSuccess;
+  if (tile == 129) k_gemm128_mfma<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
+  else if (tile == 128)
+    k_gemm128<<<(unsigned)(maxwg > 0 ? std::min<int64_t>(ntiles, maxwg) : ntiles), 256, 0, st>>>(
+        tasks, ntask, ntiles);
+  else k_gemm<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
+  return hipGetLastError();
+}
+
+}  // namespace smlu

@@ -1,0 +1,318 @@
+// kernels_solve.hip — level-scheduled forward/backward solves (lsolve!/rsolve!, src/SharedMemSparseLU.jl:349-392)
+// and ldiv!'s scale/permute steps (:318-339).
+#include "kernels_common.hpp"
+
+namespace smlu {
+
+// ------------------------------------------------------------------------------------
+// Solves.  Front vectors v_s (M doubles) live in vbuf[voff[s]].
+// Forward (L): gather own rows + children's update vectors, apply the front's row
+// permutation, unit-lower solve of the diagonal block in 64-column blocks (one wave does
+// the block by shuffles, all waves apply the block to the rows below), leave
+// v[ns:M) = update vector for the parent.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fwd_front(const int32_t* __restrict__ list,
+                                                   const SNode* __restrict__ sn,
+                                                   const int32_t* __restrict__ chlist,
+                                                   const int32_t* __restrict__ relmap,
+                                                   const int32_t* __restrict__ rowperm,
+                                                   const double* __restrict__ store,
+                                                   double* __restrict__ x,
+                                                   double* __restrict__ vbuf) {
+  __shared__ double xs[64];
+  const SNode s = sn[list[blockIdx.x]];
+  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
+  double* v = vbuf + s.voff;
+  double* xo = x + s.first;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int64_t i = tid; i < M; i += 256) v[i] = i < ns ? xo[i] : 0.0;
+  __syncthreads();
+  for (int c = s.chbeg; c < s.chend; ++c) {
+    const SNode ch = sn[chlist[c]];
+    const double* u = vbuf + ch.voff + ch.ns;
+    const int32_t* rm = relmap + ch.rowptr;
+    for (int64_t i = tid; i < ch.nu; i += 256) v[rm[i]] += u[i];
+    __syncthreads();
+  }
+  // permuted diagonal-block right-hand side -> x positions (owned by this front)
+  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[rowperm[s.first + i]];
+  __syncthreads();
+  for (int64_t i = tid; i < ns; i += 256) v[i] = xo[i];
+  __syncthreads();
+  const double* Lp = store + s.Loff;
+  for (int64_t jb = 0; jb < ns; jb += 64) {
+    const int bw = (int)min<int64_t>(64, ns - jb);
+    if (wv == 0) {
+      double xi = lane < bw ? v[jb + lane] : 0.0;
+      for (int j = 0; j < bw; ++j) {
+        double xj = __shfl(xi, j, 64);
+        if (lane > j && lane < bw) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
+      }
+      if (lane < bw) {
+        xs[lane] = xi;
+        v[jb + lane] = xi;
+      }
+    }
+    __syncthreads();
+    for (int64_t i = jb + bw + tid; i < M; i += 256) {
+      double acc = 0.0;
+      for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
+      v[i] -= acc;
+    }
+    __syncthreads();
+  }
+  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[i];
+}
+
+// Backward (U): x_s -= U12 * x[R_s]; then upper solve of the diagonal block from the bottom.
+__global__ __launch_bounds__(256) void k_bwd_front(const int32_t* __restrict__ list,
+                                                   const SNode* __restrict__ sn,
+                                                   const int32_t* __restrict__ rows,
+                                                   const double* __restrict__ store,
+                                                   double* __restrict__ x,
+                                                   double* __restrict__ vbuf) {
+  __shared__ double xs[64];
+  const SNode s = sn[list[blockIdx.x]];
+  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns, nu = s.nu;
+  double* v = vbuf + s.voff;
+  double* xo = x + s.first;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int32_t* R = rows + s.rowptr;
+  for (int64_t i = tid; i < nu; i += 256) v[ns + i] = x[R[i]];
+  __syncthreads();
+  const double* U12 = store + s.Uoff;
+  for (int64_t i = tid; i < ns; i += 256) {
+    double acc = 0.0;
+    for (int64_t j = 0; j < nu; ++j) acc = fma(U12[j * ns + i], v[ns + j], acc);
+    v[i] = xo[i] - acc;
+  }
+  __syncthreads();
+  const double* Lp = store + s.Loff;  // U11 in the upper triangle of the L panel
+  for (int64_t jb = ((ns - 1) / 64) * 64; jb >= 0; jb -= 64) {
+    const int bw = (int)min<int64_t>(64, ns - jb);
+    if (wv == 0) {
+      double xi = lane < bw ? v[jb + lane] : 0.0;
+      for (int j = bw - 1; j >= 0; --j) {
+        if (lane == j) xi = xi * recip(Lp[(jb + j) * M + jb + j]);
+        double xj = __shfl(xi, j, 64);
+        if (lane < j) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
+      }
+      if (lane < bw) {
+        xs[lane] = xi;
+        v[jb + lane] = xi;
+      }
+    }
+    __syncthreads();
+    for (int64_t i = tid; i < jb; i += 256) {
+      double acc = 0.0;
+      for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
+      v[i] -= acc;
+    }
+    __syncthreads();
+  }
+  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[i];
+}
+
+// ------------------------------------------------------------------------------------
+// Solves for large fronts (ns > 256): the diagonal block sweep is split over workgroups.
+// k_fwd_gather: front vector = own rows + children's update vectors, row permutation.
+// k_fwd_block (step t, jb = 64t): every workgroup re-solves the 64x64 unit-lower diagonal
+//   block from v (read-only in this launch), applies it to its 256-row chunk below; chunk 0
+//   publishes the solved block into x.  k_bwd_u12: x_s -= U12 x[R_s] by row chunks.
+// k_bwd_block: same as k_fwd_block for U11 from the bottom block up.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_fwd_gather(const int32_t* __restrict__ list,
+                                                    const SNode* __restrict__ sn,
+                                                    const int32_t* __restrict__ chlist,
+                                                    const int32_t* __restrict__ relmap,
+                                                    const int32_t* __restrict__ rowperm,
+                                                    double* __restrict__ x, double* __restrict__ vbuf) {
+  const SNode s = sn[list[blockIdx.x]];
+  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
+  double* v = vbuf + s.voff;
+  double* xo = x + s.first;
+  const int tid = threadIdx.x;
+  for (int64_t i = tid; i < M; i += 256) v[i] = i < ns ? xo[i] : 0.0;
+  __syncthreads();
+  for (int c = s.chbeg; c < s.chend; ++c) {
+    const SNode ch = sn[chlist[c]];
+    const double* u = vbuf + ch.voff + ch.ns;
+    const int32_t* rm = relmap + ch.rowptr;
+    for (int64_t i = tid; i < ch.nu; i += 256) v[rm[i]] += u[i];
+    __syncthreads();
+  }
+  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[rowperm[s.first + i]];
+  __syncthreads();
+  for (int64_t i = tid; i < ns; i += 256) v[i] = xo[i];
+}
+
+template <bool UPPER>
+__global__ __launch_bounds__(256) void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step,
+                                                   const SNode* __restrict__ sn,
+                                                   const double* __restrict__ store,
+                                                   double* __restrict__ x, double* __restrict__ vbuf) {
+  __shared__ double xs[64];
+  const int64_t b = blockIdx.x;
+  const int fi = find_front_tile(ft, nft, b);
+  const SNode s = sn[ft[fi].s];
+  const int64_t chunk = b - ft[fi].wg0;
+  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
+  const int64_t nblk = (ns + 63) / 64;
+  const int64_t jb = UPPER ? (nblk - 1 - step) * 64 : (int64_t)step * 64;
+  const int bw = (int)min<int64_t>(64, ns - jb);
+  double* v = vbuf + s.voff;
+  const double* Lp = store + s.Loff;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (wv == 0) {
+    double xi = lane < bw ? v[jb + lane] : 0.0;
+    if (!UPPER) {
+      for (int j = 0; j < bw; ++j) {
+        double xj = __shfl(xi, j, 64);
+        if (lane > j && lane < bw) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
+      }
+    } else {
+      for (int j = bw - 1; j >= 0; --j) {
+        if (lane == j) xi = xi * recip(Lp[(jb + j) * M + jb + j]);
+        double xj = __shfl(xi, j, 64);
+        if (lane < j) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
+      }
+    }
+    if (lane < bw) {
+      xs[lane] = xi;
+      if (chunk == 0) x[s.first + jb + lane] = xi;
+    }
+  }
+  __syncthreads();
+  // rows updated by this chunk: forward -> [jb+bw, M), backward -> [0, jb)
+  const int64_t r0 = UPPER ? chunk * 256 : jb + bw + chunk * 256;
+  const int64_t r1 = UPPER ? jb : M;
+  const int64_t i = r0 + tid;
+  if (i < r1 && i < r0 + 256) {
+    double acc = 0.0;
+    for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
+    v[i] -= acc;
+  }
+}
+
+// x_s[i] (in v) = x[first+i] - sum_j U12[i,j] * x[R_j], 256 rows per workgroup
+__global__ __launch_bounds__(256) void k_bwd_u12(const FrontTile* __restrict__ ft, int nft,
+                                                 const SNode* __restrict__ sn,
+                                                 const int32_t* __restrict__ rows,
+                                                 const double* __restrict__ store,
+                                                 const double* __restrict__ x,
+                                                 double* __restrict__ vbuf) {
+  __shared__ double xr[256];
+  const int64_t b = blockIdx.x;
+  const int fi = find_front_tile(ft, nft, b);
+  const SNode s = sn[ft[fi].s];
+  const int64_t chunk = b - ft[fi].wg0;
+  const int64_t ns = s.ns, nu = s.nu;
+  const int32_t* R = rows + s.rowptr;
+  const double* U12 = store + s.Uoff;
+  const int tid = threadIdx.x;
+  const int64_t i = chunk * 256 + tid;
+  double acc = 0.0;
+  for (int64_t j0 = 0; j0 < nu; j0 += 256) {
+    __syncthreads();
+    if (j0 + tid < nu) xr[tid] = x[R[j0 + tid]];
+    __syncthreads();
+    const int cnt = (int)min<int64_t>(256, nu - j0);
+    if (i < ns)
+      for (int j = 0; j < cnt; ++j) acc = fma(U12[(j0 + j) * ns + i], xr[j], acc);
+  }
+  if (i < ns) vbuf[s.voff + i] = x[s.first + i] - acc;
+}
+
+// wrk[i] = Rs[p0[i]] * b[p0[i]]
+__global__ void k_perm_in(int64_t n, const int64_t* __restrict__ p0, const double* __restrict__ Rs,
+                          const double* __restrict__ b, double* __restrict__ wrk) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    int64_t r = p0[i];
+    wrk[i] = Rs[r] * b[r];
+  }
+}
+// x[q[i]] = wrk[i]
+__global__ void k_perm_out(int64_t n, const int64_t* __restrict__ q, const double* __restrict__ wrk,
+                           double* __restrict__ x) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[q[i]] = wrk[i];
+}
+// multi-GPU: x[q[i]] = wrk[i] on the rows this rank owns, 0 elsewhere (summed over ranks)
+__global__ void k_perm_out_masked(int64_t n, const int64_t* __restrict__ q, const int8_t* __restrict__ own,
+                                  const double* __restrict__ wrk, double* __restrict__ x) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[q[i]] = own[i] ? wrk[i] : 0.0;
+}
+// final order -> pre-swap positions: out[first + rowperm[first+i]] = in[first+i]
+__global__ void k_unswap(int64_t n, const int64_t* __restrict__ pos_first,
+                         const int32_t* __restrict__ rowperm, const double* __restrict__ in,
+                         double* __restrict__ out) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    int64_t f = pos_first[i];
+    out[f + rowperm[i]] = in[i];
+  }
+}
+
+
+// ------------------------------------------------------------------------------------
+// Host-side launch wrappers (called from smlu.cpp)
+// ------------------------------------------------------------------------------------
+static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+hipError_t launch_fwd(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
+                      const int32_t* chlist, const int32_t* relmap, const int32_t* rowperm,
+                      const double* store, double* x, double* vbuf) {
+  if (cnt <= 0) return hipSuccess;
+  k_fwd_front<<<cnt, 256, 0, st>>>(list, sn, chlist, relmap, rowperm, store, x, vbuf);
+  return hipGetLastError();
+}
+hipError_t launch_bwd(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
+                      const int32_t* rows, const double* store, double* x, double* vbuf) {
+  if (cnt <= 0) return hipSuccess;
+  k_bwd_front<<<cnt, 256, 0, st>>>(list, sn, rows, store, x, vbuf);
+  return hipGetLastError();
+}
+hipError_t launch_fwd_gather(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
+                             const int32_t* chlist, const int32_t* relmap, const int32_t* rowperm,
+                             double* x, double* vbuf) {
+  if (cnt <= 0) return hipSuccess;
+  k_fwd_gather<<<cnt, 256, 0, st>>>(list, sn, chlist, relmap, rowperm, x, vbuf);
+  return hipGetLastError();
+}
+hipError_t launch_tri_block(hipStream_t st, bool upper, int64_t nwg, const FrontTile* ft, int nft,
+                            int step, const SNode* sn, const double* store, double* x, double* vbuf) {
+  if (nwg <= 0) return hipSuccess;
+  if (upper) k_tri_block<true><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, x, vbuf);
+  else k_tri_block<false><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, x, vbuf);
+  return hipGetLastError();
+}
+hipError_t launch_bwd_u12(hipStream_t st, int64_t nwg, const FrontTile* ft, int nft, const SNode* sn,
+                          const int32_t* rows, const double* store, const double* x, double* vbuf) {
+  if (nwg <= 0) return hipSuccess;
+  k_bwd_u12<<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sn, rows, store, x, vbuf);
+  return hipGetLastError();
+}
+hipError_t launch_perm_in(hipStream_t st, int64_t n, const int64_t* p0, const double* Rs,
+                          const double* b, double* wrk) {
+  k_perm_in<<<nblk(n, 256), 256, 0, st>>>(n, p0, Rs, b, wrk);
+  return hipGetLastError();
+}
+hipError_t launch_perm_out_masked(hipStream_t st, int64_t n, const int64_t* q, const int8_t* own,
+                                  const double* wrk, double* x) {
+  if (n <= 0) return hipSuccess;
+  k_perm_out_masked<<<nblk(n, 256), 256, 0, st>>>(n, q, own, wrk, x);
+  return hipGetLastError();
+}
+hipError_t launch_perm_out(hipStream_t st, int64_t n, const int64_t* q, const double* wrk, double* x) {
+  k_perm_out<<<nblk(n, 256), 256, 0, st>>>(n, q, wrk, x);
+  return hipGetLastError();
+}
+hipError_t launch_unswap(hipStream_t st, int64_t n, const int64_t* pos_first, const int32_t* rowperm,
+                         const double* in, double* out) {
+  k_unswap<<<nblk(n, 256), 256, 0, st>>>(n, pos_first, rowperm, in, out);
+  return hipGetLastError();
+}
+
+
+}  // namespace smlu

@@ -1274,7 +1274,7 @@ void smlu_default_opts(smlu_opts* o) {
   o->device = 0;
   o->profile = 0;
   o->leaf_size = 64;
-  o->use_mfma = std::getenv("SMLU_MFMA") ? 1 : 0;
+  o->use_mfma = std::getenv("SMLU_VALU_GEMM") ? 0 : 1;   // fp64 MFMA by default
 }
 
 int smlu_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,

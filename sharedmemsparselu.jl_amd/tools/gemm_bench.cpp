@@ -15,11 +15,16 @@ static void fill(std::vector<double>& v, unsigned seed) { srand(seed); for (auto
 int main(int argc, char** argv) {
   struct Shape { int m, n, k; } shapes[] = {{4096, 4096, 4096}, {8192, 8192, 1024}, {16384, 16384, 64}, {12000, 12000, 6000}, {1000, 1000, 300}, {300, 5000, 32}, {777, 1333, 129},
                                             {18000, 192, 64}, {192, 18000, 64}, {6000, 6000, 256}, {3000, 3000, 256}, {1500, 1500, 1000}, {18000, 256, 256}};
+  std::vector<Shape> sv(std::begin(shapes), std::end(shapes));
+  if (argc > 1) {   // shapes from the command line: m,n,k ...
+    sv.clear();
+    for (int a = 1; a < argc; ++a) { Shape x; if (sscanf(argv[a], "%d,%d,%d", &x.m, &x.n, &x.k) == 3) sv.push_back(x); }
+  }
   const int tiles_list[] = {64, 128, 129};
   const char* names[] = {"valu64", "valu128", "mfma128"};
   hipStream_t st; CK(hipStreamCreate(&st));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-  for (auto sh : shapes) {
+  for (auto sh : sv) {
     int m = sh.m, n = sh.n, k = sh.k, lda = m + 3, ldb = k + 1, ldc = m + 5;
     std::vector<double> hA((size_t)lda * k), hB((size_t)ldb * n), hC((size_t)ldc * n);
     fill(hA, 1); fill(hB, 2); fill(hC, 3);
