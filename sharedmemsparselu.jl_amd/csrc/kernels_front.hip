@@ -597,6 +597,7 @@ __global__ __launch_bounds__(256) void k_laswp(const SwapTask* __restrict__ task
   }
 }
 
+
 template <int W>
 __global__ __launch_bounds__(256) void k_trsm_u(const FrontTile* __restrict__ ft, int nft, int OB,
                                                 int mode, const SNode* __restrict__ sn,

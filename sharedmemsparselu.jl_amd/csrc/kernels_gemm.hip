@@ -17,19 +17,41 @@ __device__ __forceinline__ int find_gemm_task(const GemmTask* __restrict__ t, in
   return lo;
 }
 
+
+// Tile placement.  (1) XCD-aware remap (bijective for any grid): the workgroups that share an
+// XCD (same blockIdx % 8) get one contiguous range of tile indices; with in-order dispatch the
+// tiles an XCD runs at the same time are then neighbours.  (2) Grouped order inside a task:
+// groups of 8 tile rows, column-major inside a group, so 64 neighbouring tiles form an 8 x 8
+// block of C and share 8 A row blocks and 8 B column blocks in that XCD's L2.
+__device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nwg) {
+  const int64_t q = nwg >> 3, r = nwg & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+template <int TS>
+__device__ __forceinline__ void tile_rc(const GemmTask& t, int64_t tl, int& tm, int& tn) {
+  constexpr int GM = 8;
+  const int64_t tiles_n = (t.n + TS - 1) / TS;
+  const int64_t g = tl / (GM * tiles_n);
+  const int first = (int)(g * GM);
+  const int gm = min(GM, t.tiles_m - first);
+  const int64_t in = tl - g * GM * tiles_n;
+  tm = first + (int)(in % gm);
+  tn = (int)(in / gm);
+}
+
 #define GBM 64
 #define GBN 64
 #define GBK 16
 __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks, int ntask) {
   __shared__ double As[2][GBK][GBM + 2];
   __shared__ double Bs[2][GBK][GBN + 2];
-  const int64_t b = blockIdx.x;
+  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
   const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
   const gdbl* gA = gbl(t.A);
   const gdbl* gB = gbl(t.B);
   gdbl* gC = gbl(t.C);
-  const int64_t tl = b - t.tile0;
-  const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
+  int tm, tn;
+  tile_rc<GBM>(t, b - t.tile0, tm, tn);
   const int m0 = tm * GBM, n0 = tn * GBN;
   const int tid = threadIdx.x;
   const int tx = tid & 15, ty = tid >> 4;  // 16 x 16 threads, 4x4 each
@@ -126,8 +148,8 @@ __device__ __forceinline__ void gemm128_tile(const GemmTask* __restrict__ tasks,
   const gdbl* gA = gbl(t.A);
   const gdbl* gB = gbl(t.B);
   gdbl* gC = gbl(t.C);
-  const int64_t tl = b - t.tile0;
-  const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
+  int tm, tn;
+  tile_rc<HBM_>(t, b - t.tile0, tm, tn);
   const int m0 = tm * HBM_, n0 = tn * HBM_;
   const int tid = threadIdx.x;
   const int tx = tid & 15, ty = tid >> 4;
@@ -221,7 +243,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__
   __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
   __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
   for (int64_t b = blockIdx.x; b < ntiles; b += gridDim.x) {
-    gemm128_tile(tasks, ntask, b, As, Bs);
+    gemm128_tile(tasks, ntask, (int64_t)gridDim.x == ntiles ? xcd_remap(b, ntiles) : b, As, Bs);
     __syncthreads();
   }
 }
@@ -242,8 +264,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
   const gdbl* gA = gbl(t.A);
   const gdbl* gB = gbl(t.B);
   gdbl* gC = gbl(t.C);
-  const int64_t tl = b - t.tile0;
-  const int tm = (int)(tl % t.tiles_m), tn = (int)(tl / t.tiles_m);
+  int tm, tn;
+  tile_rc<HBM_>(t, b - t.tile0, tm, tn);
   const int m0 = tm * HBM_, n0 = tn * HBM_;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = (wv & 1) * 64, wc = (wv >> 1) * 64;   // wave quadrant (rows, cols)
@@ -321,6 +343,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
       }
   }
 }
+
 
 
 // ------------------------------------------------------------------------------------

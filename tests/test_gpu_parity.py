@@ -138,3 +138,39 @@ def test_blocked_tile_mode_dominant(gpu):
     smlu.ldiv_(x, F, b)
     assert isapprox(x, np.linalg.solve(D, b), DENSE_TOL, DENSE_TOL)
     factor_parity(A, F, rtol=1e-11)
+
+
+def _tile_pivoting_matrix(n, seed):
+    """Dense matrix whose 64x64 diagonal blocks dominate their rows but whose diagonal entries are
+    tiny, so the diagonal-tile panel (mode 2, ns > 512) must exchange rows inside every tile."""
+    rng = np.random.default_rng(seed)
+    D = rng.random((n, n))
+    for b0 in range(0, n, 64):
+        b1 = min(n, b0 + 64)
+        blk = rng.random((b1 - b0, b1 - b0)) * n
+        np.fill_diagonal(blk, 1e-3)
+        D[b0:b1, b0:b1] += blk
+    return D
+
+
+@pytest.mark.parametrize("n", [700, 1100])
+def test_blocked_tile_mode_pivoting(gpu, n):
+    # diagonal-tile pivoting with real row exchanges (k_panel_tile64); parity with the oracle run
+    # on the GPU's own final (p, q) and a solve against LAPACK
+    D = _tile_pivoting_matrix(n, 11 + n)
+    A = sp.csc_matrix(D)
+    F = smlu.ParallelSparseLU(A)
+    assert not np.array_equal(F.p, F.q), "expected row exchanges"
+    b = np.random.default_rng(n).random(n)
+    x = np.empty(n)
+    smlu.ldiv_(x, F, b)
+    ctol = max(DENSE_TOL, 8 * np.finfo(float).eps * np.linalg.cond(D))
+    assert isapprox(x, np.linalg.solve(D, b), ctol, ctol)
+    factor_parity(A, F, rtol=1e-10)
+    # refactor with new values (same pattern): pivots chosen afresh
+    D2 = _tile_pivoting_matrix(n, 99 + n)
+    smlu.lu_(F, sp.csc_matrix(D2))
+    smlu.ldiv_(x, F, b)
+    ctol = max(DENSE_TOL, 8 * np.finfo(float).eps * np.linalg.cond(D2))
+    assert isapprox(x, np.linalg.solve(D2, b), ctol, ctol)
+    factor_parity(sp.csc_matrix(D2), F, rtol=1e-10)
