@@ -155,4 +155,62 @@ __device__ __forceinline__ double upper_right_solve_fast(double (&x)[XN], const 
 // every column outside the panel; TRSM only the columns inside the outer block [kb+w, oend).
 // mode 1 (outer phase, sub-panel at kb): TRSM rows [kb, kb+w) on the columns right of the
 // outer block [oend, M); no swaps (already applied).  kb comes from FrontTile.pad.
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// LDS hand-off inside one wave (no workgroup barrier): stores complete and become visible to
+// the wave's later loads, and the compiler may not move LDS accesses across it.
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// One wave solves a bw x bw (bw <= 64) diagonal block stored column-major at D (ld M): unit
+// lower (UPPER = false, forward) or upper with its diagonal (UPPER = true, backward); lane i
+// holds x_i.  Row i of the block is loaded into registers up front (64 independent loads, one
+// memory latency), so the 64-step chain only waits on readlane broadcasts, never on memory.
+template <bool UPPER>
+__device__ __forceinline__ double tri64(double xi, const double* __restrict__ D, int64_t M, int bw,
+                                        int lane) {
+  double row[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) row[j] = (lane < bw && j < bw) ? D[(int64_t)j * M + lane] : 0.0;
+  if (!UPPER) {
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      if (j < bw) {
+        const double xj = readlane_f64(xi, j);
+        if (lane > j) xi = fma(-row[j], xj, xi);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 63; j >= 0; --j) {
+      if (j < bw) {
+        if (lane == j) xi = xi * recip(row[j]);
+        const double xj = readlane_f64(xi, j);
+        if (lane < j) xi = fma(-row[j], xj, xi);
+      }
+    }
+  }
+  return xi;
+}
+
+// acc += sum_{j < bw} D[j*M + i] * xs[j] (bw <= 64) in ascending j: all loads issued up front.
+__device__ __forceinline__ double dot64(const double* __restrict__ D, int64_t M, int64_t i, int bw,
+                                        const double* __restrict__ xs, double acc) {
+  double d[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) d[j] = j < bw ? D[(int64_t)j * M + i] : 0.0;
+#pragma unroll
+  for (int j = 0; j < 64; ++j)
+    if (j < bw) acc = fma(d[j], xs[j], acc);
+  return acc;
+}
+
 }  // namespace smlu

@@ -427,12 +427,6 @@ __global__ __launch_bounds__(64 * NW) void k_panel_reg(const int32_t* __restrict
 // same arithmetic, with every broadcast done by v_readlane from the owning lane instead of
 // through LDS -- no LDS traffic and no barriers on the per-column chain.  who (position ->
 // thread) is kept one entry per lane.
-__device__ __forceinline__ double readlane_f64(double v, int lane) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
 
 template <int W>
 __global__ __launch_bounds__(64) void k_panel_wave(const int32_t* __restrict__ list, int step,

@@ -44,21 +44,14 @@ __global__ __launch_bounds__(256) void k_fwd_front(const int32_t* __restrict__ l
     const int bw = (int)min<int64_t>(64, ns - jb);
     if (wv == 0) {
       double xi = lane < bw ? v[jb + lane] : 0.0;
-      for (int j = 0; j < bw; ++j) {
-        double xj = __shfl(xi, j, 64);
-        if (lane > j && lane < bw) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
-      }
+      xi = tri64<false>(xi, Lp + jb * M + jb, M, bw, lane);
       if (lane < bw) {
         xs[lane] = xi;
         v[jb + lane] = xi;
       }
     }
     __syncthreads();
-    for (int64_t i = jb + bw + tid; i < M; i += 256) {
-      double acc = 0.0;
-      for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
-      v[i] -= acc;
-    }
+    for (int64_t i = jb + bw + tid; i < M; i += 256) v[i] -= dot64(Lp + jb * M, M, i, bw, xs, 0.0);
     __syncthreads();
   }
   for (int64_t i = tid; i < ns; i += 256) xo[i] = v[i];
@@ -83,6 +76,7 @@ __global__ __launch_bounds__(256) void k_bwd_front(const int32_t* __restrict__ l
   const double* U12 = store + s.Uoff;
   for (int64_t i = tid; i < ns; i += 256) {
     double acc = 0.0;
+#pragma unroll 8
     for (int64_t j = 0; j < nu; ++j) acc = fma(U12[j * ns + i], v[ns + j], acc);
     v[i] = xo[i] - acc;
   }
@@ -92,22 +86,14 @@ __global__ __launch_bounds__(256) void k_bwd_front(const int32_t* __restrict__ l
     const int bw = (int)min<int64_t>(64, ns - jb);
     if (wv == 0) {
       double xi = lane < bw ? v[jb + lane] : 0.0;
-      for (int j = bw - 1; j >= 0; --j) {
-        if (lane == j) xi = xi * recip(Lp[(jb + j) * M + jb + j]);
-        double xj = __shfl(xi, j, 64);
-        if (lane < j) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
-      }
+      xi = tri64<true>(xi, Lp + jb * M + jb, M, bw, lane);
       if (lane < bw) {
         xs[lane] = xi;
         v[jb + lane] = xi;
       }
     }
     __syncthreads();
-    for (int64_t i = tid; i < jb; i += 256) {
-      double acc = 0.0;
-      for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
-      v[i] -= acc;
-    }
+    for (int64_t i = tid; i < jb; i += 256) v[i] -= dot64(Lp + jb * M, M, i, bw, xs, 0.0);
     __syncthreads();
   }
   for (int64_t i = tid; i < ns; i += 256) xo[i] = v[i];
@@ -165,18 +151,7 @@ __global__ __launch_bounds__(256) void k_tri_block(const FrontTile* __restrict__
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (wv == 0) {
     double xi = lane < bw ? v[jb + lane] : 0.0;
-    if (!UPPER) {
-      for (int j = 0; j < bw; ++j) {
-        double xj = __shfl(xi, j, 64);
-        if (lane > j && lane < bw) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
-      }
-    } else {
-      for (int j = bw - 1; j >= 0; --j) {
-        if (lane == j) xi = xi * recip(Lp[(jb + j) * M + jb + j]);
-        double xj = __shfl(xi, j, 64);
-        if (lane < j) xi = fma(-Lp[(jb + j) * M + jb + lane], xj, xi);
-      }
-    }
+    xi = tri64<UPPER>(xi, Lp + jb * M + jb, M, bw, lane);
     if (lane < bw) {
       xs[lane] = xi;
       if (chunk == 0) x[s.first + jb + lane] = xi;
@@ -187,21 +162,20 @@ __global__ __launch_bounds__(256) void k_tri_block(const FrontTile* __restrict__
   const int64_t r0 = UPPER ? chunk * 256 : jb + bw + chunk * 256;
   const int64_t r1 = UPPER ? jb : M;
   const int64_t i = r0 + tid;
-  if (i < r1 && i < r0 + 256) {
-    double acc = 0.0;
-    for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
-    v[i] -= acc;
-  }
+  if (i < r1 && i < r0 + 256) v[i] -= dot64(Lp + jb * M, M, i, bw, xs, 0.0);
 }
 
 // x_s[i] (in v) = x[first+i] - sum_j U12[i,j] * x[R_j], 256 rows per workgroup
+// 64 rows per workgroup; wave w sums the columns [w*nu/4, (w+1)*nu/4) (x[R] staged in LDS
+// per 64-column chunk, 8 loads in flight), the four partial sums combined in wave order.
 __global__ __launch_bounds__(256) void k_bwd_u12(const FrontTile* __restrict__ ft, int nft,
                                                  const SNode* __restrict__ sn,
                                                  const int32_t* __restrict__ rows,
                                                  const double* __restrict__ store,
                                                  const double* __restrict__ x,
                                                  double* __restrict__ vbuf) {
-  __shared__ double xr[256];
+  __shared__ double xr[4][64];
+  __shared__ double part[4][64];
   const int64_t b = blockIdx.x;
   const int fi = find_front_tile(ft, nft, b);
   const SNode s = sn[ft[fi].s];
@@ -209,18 +183,24 @@ __global__ __launch_bounds__(256) void k_bwd_u12(const FrontTile* __restrict__ f
   const int64_t ns = s.ns, nu = s.nu;
   const int32_t* R = rows + s.rowptr;
   const double* U12 = store + s.Uoff;
-  const int tid = threadIdx.x;
-  const int64_t i = chunk * 256 + tid;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t i = chunk * 64 + lane;
+  const int64_t j0 = nu * wv / 4, j1 = nu * (wv + 1) / 4;
   double acc = 0.0;
-  for (int64_t j0 = 0; j0 < nu; j0 += 256) {
-    __syncthreads();
-    if (j0 + tid < nu) xr[tid] = x[R[j0 + tid]];
-    __syncthreads();
-    const int cnt = (int)min<int64_t>(256, nu - j0);
-    if (i < ns)
-      for (int j = 0; j < cnt; ++j) acc = fma(U12[(j0 + j) * ns + i], xr[j], acc);
+  for (int64_t jc = j0; jc < j1; jc += 64) {
+    const int cnt = (int)min<int64_t>(64, j1 - jc);
+    if (lane < cnt) xr[wv][lane] = x[R[jc + lane]];
+    wave_lds_sync();
+    if (i < ns) {
+#pragma unroll 8
+      for (int j = 0; j < cnt; ++j) acc = fma(U12[(jc + j) * ns + i], xr[wv][j], acc);
+    }
+    wave_lds_sync();   // every lane's reads of this chunk before the next chunk overwrites it
   }
-  if (i < ns) vbuf[s.voff + i] = x[s.first + i] - acc;
+  part[wv][lane] = acc;
+  __syncthreads();
+  if (wv == 0 && i < ns)
+    vbuf[s.voff + i] = x[s.first + i] - (((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
 }
 
 // wrk[i] = Rs[p0[i]] * b[p0[i]]

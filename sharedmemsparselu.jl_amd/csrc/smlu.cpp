@@ -783,7 +783,7 @@ static int build_schedule(smlu_handle* h) {
       int64_t wg = 0;
       for (auto s : bigs) {
         ft.push_back(FrontTile{(int32_t)s, 0, wg});
-        wg += (h->hsn[s].ns + 255) / 256;
+        wg += (h->hsn[s].ns + 63) / 64;   // k_bwd_u12: 64 rows per workgroup
       }
       U.cnt = (int64_t)bigs.size();
       U.nwg = wg;
