@@ -11,6 +11,32 @@ namespace smlu {
 // the block by shuffles, all waves apply the block to the rows below), leave
 // v[ns:M) = update vector for the parent.
 // ------------------------------------------------------------------------------------
+// Small-front solves (one workgroup per front): the bw x bw diagonal block is staged in LDS by
+// all 256 threads (coalesced), then one wave runs the shuffle-free chain from LDS.
+__device__ __forceinline__ void stage_block(double* __restrict__ sD, const double* __restrict__ D,
+                                            int64_t M, int bw, int tid) {
+  for (int idx = tid; idx < bw * 64; idx += 256) {
+    const int i = idx & 63, j = idx >> 6;
+    if (i < bw) sD[j * 65 + i] = D[(int64_t)j * M + i];
+  }
+}
+template <bool UPPER>
+__device__ __forceinline__ double tri_lds(double xi, const double* __restrict__ sD, int bw, int lane) {
+  if (!UPPER) {
+    for (int j = 0; j < bw; ++j) {
+      const double xj = readlane_f64(xi, j);
+      if (lane > j && lane < bw) xi = fma(-sD[j * 65 + lane], xj, xi);
+    }
+  } else {
+    for (int j = bw - 1; j >= 0; --j) {
+      if (lane == j) xi = xi * recip(sD[j * 65 + j]);
+      const double xj = readlane_f64(xi, j);
+      if (lane < j) xi = fma(-sD[j * 65 + lane], xj, xi);
+    }
+  }
+  return xi;
+}
+
 __global__ __launch_bounds__(256) void k_fwd_front(const int32_t* __restrict__ list,
                                                    const SNode* __restrict__ sn,
                                                    const int32_t* __restrict__ chlist,
@@ -20,6 +46,7 @@ __global__ __launch_bounds__(256) void k_fwd_front(const int32_t* __restrict__ l
                                                    double* __restrict__ x,
                                                    double* __restrict__ vbuf) {
   __shared__ double xs[64];
+  __shared__ double sD[64 * 65];
   const SNode s = sn[list[blockIdx.x]];
   const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
   double* v = vbuf + s.voff;
@@ -42,16 +69,23 @@ __global__ __launch_bounds__(256) void k_fwd_front(const int32_t* __restrict__ l
   const double* Lp = store + s.Loff;
   for (int64_t jb = 0; jb < ns; jb += 64) {
     const int bw = (int)min<int64_t>(64, ns - jb);
+    stage_block(sD, Lp + jb * M + jb, M, bw, tid);
+    __syncthreads();
     if (wv == 0) {
       double xi = lane < bw ? v[jb + lane] : 0.0;
-      xi = tri64<false>(xi, Lp + jb * M + jb, M, bw, lane);
+      xi = tri_lds<false>(xi, sD, bw, lane);
       if (lane < bw) {
         xs[lane] = xi;
         v[jb + lane] = xi;
       }
     }
     __syncthreads();
-    for (int64_t i = jb + bw + tid; i < M; i += 256) v[i] -= dot64(Lp + jb * M, M, i, bw, xs, 0.0);
+    for (int64_t i = jb + bw + tid; i < M; i += 256) {
+      double acc = 0.0;
+#pragma unroll 8
+      for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
+      v[i] -= acc;
+    }
     __syncthreads();
   }
   for (int64_t i = tid; i < ns; i += 256) xo[i] = v[i];
@@ -65,6 +99,7 @@ __global__ __launch_bounds__(256) void k_bwd_front(const int32_t* __restrict__ l
                                                    double* __restrict__ x,
                                                    double* __restrict__ vbuf) {
   __shared__ double xs[64];
+  __shared__ double sD[64 * 65];
   const SNode s = sn[list[blockIdx.x]];
   const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns, nu = s.nu;
   double* v = vbuf + s.voff;
@@ -84,16 +119,23 @@ __global__ __launch_bounds__(256) void k_bwd_front(const int32_t* __restrict__ l
   const double* Lp = store + s.Loff;  // U11 in the upper triangle of the L panel
   for (int64_t jb = ((ns - 1) / 64) * 64; jb >= 0; jb -= 64) {
     const int bw = (int)min<int64_t>(64, ns - jb);
+    stage_block(sD, Lp + jb * M + jb, M, bw, tid);
+    __syncthreads();
     if (wv == 0) {
       double xi = lane < bw ? v[jb + lane] : 0.0;
-      xi = tri64<true>(xi, Lp + jb * M + jb, M, bw, lane);
+      xi = tri_lds<true>(xi, sD, bw, lane);
       if (lane < bw) {
         xs[lane] = xi;
         v[jb + lane] = xi;
       }
     }
     __syncthreads();
-    for (int64_t i = tid; i < jb; i += 256) v[i] -= dot64(Lp + jb * M, M, i, bw, xs, 0.0);
+    for (int64_t i = tid; i < jb; i += 256) {
+      double acc = 0.0;
+#pragma unroll 8
+      for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
+      v[i] -= acc;
+    }
     __syncthreads();
   }
   for (int64_t i = tid; i < ns; i += 256) xo[i] = v[i];
