@@ -61,7 +61,10 @@ typedef struct smlu_opts {
     int32_t use_mfma;     /* 1 (default) = fp64 MFMA (v_mfma_f64_16x16x4) for the dense Schur
                              updates of large launches; 0 = fp64 VALU tiles (env SMLU_VALU_GEMM).
                              Bitwise-identical results; MFMA is faster on large tiles */
-    int32_t reserved;
+    int32_t refine;       /* iterative-refinement steps in smlu_solve*: -1 (default) = up to 3 only
+                             when the last factorization flagged weak pivots (the pivot-failure
+                             fallback of the diagonal-tile pivoting); 0 = never;
+                             k > 0 = up to k steps (stops when the residual stops halving) */
 } smlu_opts;
 
 typedef struct smlu_handle smlu_handle;
@@ -101,6 +104,20 @@ int smlu_solve(smlu_handle* h, const double* b, double* x);
 
 /* Same with device pointers (x == b allowed). */
 int smlu_solve_device(smlu_handle* h, const double* d_b, double* d_x);
+
+/* ldiv! with nrhs right-hand sides: column j of B (ldb >= n) -> column j of X (ldx >= n),
+ * host memory, X == B allowed.  The reference's ldiv! is generic over the vector type
+ * (src/SharedMemSparseLU.jl:286); multiple RHS are SURVEY §8f-4. */
+int smlu_solve_multi(smlu_handle* h, int64_t nrhs, const double* B, int64_t ldb, double* X, int64_t ldx);
+
+/* Same with device pointers. */
+int smlu_solve_multi_device(smlu_handle* h, int64_t nrhs, const double* d_B, int64_t ldb, double* d_X,
+                            int64_t ldx);
+
+/* ParallelSparseLU(A::SparseMatrixCSC{Float64,Int32}) — Int32 index arrays;
+ * converted to the Int64 path on the host. */
+int smlu_create_i32(int64_t n, const int32_t* colptr, const int32_t* rowval, const double* nzval,
+                    const smlu_opts* opts, smlu_handle** out);
 
 /* lsolve!(F, x) — src/SharedMemSparseLU.jl:349-367: in place L \ x on an already
  * row-permuted and scaled host vector (x in the reference's F.p order). */

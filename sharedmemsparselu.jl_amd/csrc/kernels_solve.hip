@@ -278,6 +278,37 @@ __global__ void k_unswap(int64_t n, const int64_t* __restrict__ pos_first,
 }
 
 
+
+// ------------------------------------------------------------------------------------
+// Iterative refinement (pivot-failure fallback): r = b - A x by rows of A (entries of a row in
+// column order, deterministic), max |r_i| into *nrm; x += d.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_residual(int64_t n, const int64_t* __restrict__ rowptr,
+                                                  const int32_t* __restrict__ ent,
+                                                  const int32_t* __restrict__ acol,
+                                                  const double* __restrict__ a,
+                                                  const double* __restrict__ x,
+                                                  const double* __restrict__ b, double* __restrict__ r,
+                                                  double* __restrict__ nrm) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double ri = 0.0;
+  if (i < n) {
+    double acc = 0.0;
+    for (int64_t e = rowptr[i]; e < rowptr[i + 1]; ++e) {
+      const int32_t k = ent[e];
+      acc = fma(a[k], x[acol[k]], acc);
+    }
+    ri = b[i] - acc;
+    r[i] = ri;
+  }
+  const double m = wave_max(fabs(ri));
+  if ((threadIdx.x & 63) == 0 && m > 0.0) atomic_max_pos(nrm, m);
+}
+__global__ void k_axpy1(int64_t n, const double* __restrict__ d, double* __restrict__ x) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] += d[i];
+}
+
 // ------------------------------------------------------------------------------------
 // Host-side launch wrappers (called from smlu.cpp)
 // ------------------------------------------------------------------------------------
@@ -313,6 +344,18 @@ hipError_t launch_bwd_u12(hipStream_t st, int64_t nwg, const FrontTile* ft, int 
                           const int32_t* rows, const double* store, const double* x, double* vbuf) {
   if (nwg <= 0) return hipSuccess;
   k_bwd_u12<<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sn, rows, store, x, vbuf);
+  return hipGetLastError();
+}
+hipError_t launch_residual(hipStream_t st, int64_t n, const int64_t* rowptr, const int32_t* ent,
+                           const int32_t* acol, const double* a, const double* x, const double* b,
+                           double* r, double* nrm) {
+  if (n <= 0) return hipSuccess;
+  k_residual<<<nblk(n, 256), 256, 0, st>>>(n, rowptr, ent, acol, a, x, b, r, nrm);
+  return hipGetLastError();
+}
+hipError_t launch_axpy1(hipStream_t st, int64_t n, const double* d, double* x) {
+  if (n <= 0) return hipSuccess;
+  k_axpy1<<<nblk(n, 256), 256, 0, st>>>(n, d, x);
   return hipGetLastError();
 }
 hipError_t launch_perm_in(hipStream_t st, int64_t n, const int64_t* p0, const double* Rs,

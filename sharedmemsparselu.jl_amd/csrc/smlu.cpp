@@ -56,6 +56,9 @@ hipError_t launch_fwd(hipStream_t, int, const int32_t*, const SNode*, const int3
                       const int32_t*, const double*, double*, double*);
 hipError_t launch_bwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*,
                       double*, double*);
+hipError_t launch_residual(hipStream_t, int64_t, const int64_t*, const int32_t*, const int32_t*,
+                           const double*, const double*, const double*, double*, double*);
+hipError_t launch_axpy1(hipStream_t, int64_t, const double*, double*);
 hipError_t launch_perm_in(hipStream_t, int64_t, const int64_t*, const double*, const double*, double*);
 hipError_t launch_perm_out(hipStream_t, int64_t, const int64_t*, const double*, double*);
 hipError_t launch_perm_out_masked(hipStream_t, int64_t, const int64_t*, const int8_t*, const double*, double*);
@@ -134,6 +137,10 @@ struct smlu_handle {
   bool given_Rs = false;
   // device buffers
   DBuf<double> A, Rs, store, scratch, wrk, wrk2, vbuf, growth;
+  DBuf<double> ref_b, ref_r, ref_d, ref_nrm;   // iterative refinement (allocated on first use)
+  DBuf<int32_t> Acol;                          // column of each A entry (residuals)
+  int refine_steps = 0;
+  double refine_resid = -1;
   DBuf<int64_t> Arowptr, Adest, p0, q, posfirst;
   DBuf<int32_t> Arow_ent, Arow, Alev_ent, rows, relmap, chlist, ilist, rowperm, rowperm0, info, swaps;
   DBuf<SNode> sn;
@@ -177,7 +184,8 @@ struct smlu_handle {
   void release_buffers() {
     if (stream) (void)hipSetDevice(device);
     release_graphs();
-    DBuf<double>* d[] = {&A, &Rs, &store, &scratch, &wrk, &wrk2, &vbuf, &growth};
+    DBuf<double>* d[] = {&A, &Rs, &store, &scratch, &wrk, &wrk2, &vbuf, &growth, &ref_b, &ref_r, &ref_d, &ref_nrm};
+    Acol.free();
     for (auto* b : d) b->free();
     DBuf<int64_t>* l[] = {&Arowptr, &Adest, &p0, &q, &posfirst};
     for (auto* b : l) b->free();
@@ -1275,11 +1283,22 @@ void smlu_default_opts(smlu_opts* o) {
   o->profile = 0;
   o->leaf_size = 64;
   o->use_mfma = std::getenv("SMLU_VALU_GEMM") ? 0 : 1;   // fp64 MFMA by default
+  o->refine = -1;
 }
 
 int smlu_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
                 const smlu_opts* opts, smlu_handle** out) {
   return create_impl(n, colptr, rowval, nzval, nullptr, nullptr, nullptr, opts, out);
+}
+
+int smlu_create_i32(int64_t n, const int32_t* colptr, const int32_t* rowval, const double* nzval,
+                    const smlu_opts* opts, smlu_handle** out) {
+  if (!out || !colptr || n <= 0) return fail(nullptr, SMLU_ERR_ARG, "invalid matrix arguments");
+  const int64_t base = opts ? opts->index_base : 1;
+  const int64_t nnz = (int64_t)colptr[n] - base;
+  if (nnz < 0 || (nnz > 0 && !rowval)) return fail(nullptr, SMLU_ERR_ARG, "invalid matrix arguments");
+  std::vector<int64_t> cp(colptr, colptr + n + 1), rv(rowval, rowval + nnz);
+  return smlu_create(n, cp.data(), rv.data(), nzval, opts, out);
 }
 
 int smlu_create_with_pivots(int64_t n, const int64_t* colptr, const int64_t* rowval,
@@ -1332,11 +1351,60 @@ int smlu_refactor_csc(smlu_handle* h, int64_t n, const int64_t* colptr, const in
   return run_factor(h);
 }
 
+// ldiv! plus iterative refinement on the original (unscaled) A: x <- x + A \ (b - A x).  The
+// diagonal-tile pivoting of large fronts cannot always keep growth below 1/pivot_tol; when a
+// refactor flags such weak pivots (h->weak), refine = -1 applies up to 3 steps (the pivot-
+// failure fallback).  Stops when the residual max-norm stops halving.
+static int solve_refined(smlu_handle* h, const double* db, double* dx) {
+  const int steps = h->opts.refine < 0 ? (h->weak > 0 ? 3 : 0) : h->opts.refine;
+  h->refine_steps = 0;
+  h->refine_resid = -1;
+  if (steps == 0) return run_solve_dev(h, db, dx, 0);
+  Plan& P = h->plan;
+  const int64_t n = P.n;
+  hipStream_t st = h->stream;
+  if (!h->ref_b.p) {
+    HIPCHK(h->ref_b.alloc((size_t)n));
+    HIPCHK(h->ref_r.alloc((size_t)n));
+    HIPCHK(h->ref_d.alloc((size_t)n));
+    HIPCHK(h->ref_nrm.alloc(1));
+  }
+  if (!h->Acol.p) {
+    std::vector<int32_t> ac((size_t)std::max<int64_t>(P.nnzA, 1));
+    for (int64_t c = 0; c < n; ++c)
+      for (int64_t e = P.Acolptr[c]; e < P.Acolptr[c + 1]; ++e) ac[e] = (int32_t)c;
+    HIPCHK(h->Acol.upload(ac.data(), ac.size(), st));
+  }
+  HIPCHK(hipMemcpyAsync(h->ref_b.p, db, sizeof(double) * n, hipMemcpyDeviceToDevice, st));   // db may alias dx
+  int rc = run_solve_dev(h, h->ref_b.p, dx, 0);
+  if (rc != SMLU_OK) return rc;
+  const double ms = h->solve_ms;
+  double prev = HUGE_VAL;
+  for (int it = 0; it < steps; ++it) {
+    HIPCHK(hipMemsetAsync(h->ref_nrm.p, 0, sizeof(double), st));
+    HIPCHK(launch_residual(st, n, h->Arowptr.p, h->Arow_ent.p, h->Acol.p, h->A.p, dx, h->ref_b.p, h->ref_r.p,
+                           h->ref_nrm.p));
+    double nrm = 0;
+    HIPCHK(hipMemcpyAsync(&nrm, h->ref_nrm.p, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    h->refine_resid = nrm;
+    if (nrm == 0.0 || nrm > 0.5 * prev) break;
+    prev = nrm;
+    rc = run_solve_dev(h, h->ref_r.p, h->ref_d.p, 0);
+    if (rc != SMLU_OK) return rc;
+    HIPCHK(launch_axpy1(st, n, h->ref_d.p, dx));
+    ++h->refine_steps;
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  h->solve_ms = ms;   // the plain solve's time (refinement steps reported separately)
+  return SMLU_OK;
+}
+
 int smlu_solve_device(smlu_handle* h, const double* d_b, double* d_x) {
   if (!h || !d_b || !d_x) return fail(h, SMLU_ERR_ARG, "NULL argument");
   if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
   HIPCHK(hipSetDevice(h->device));
-  return run_solve_dev(h, d_b, d_x, 0);
+  return solve_refined(h, d_b, d_x);
 }
 
 int smlu_solve(smlu_handle* h, const double* b, double* x) {
@@ -1345,9 +1413,40 @@ int smlu_solve(smlu_handle* h, const double* b, double* x) {
   HIPCHK(hipSetDevice(h->device));
   int64_t n = h->plan.n;
   HIPCHK(hipMemcpyAsync(h->wrk2.p, b, sizeof(double) * n, hipMemcpyHostToDevice, h->stream));
-  int rc = run_solve_dev(h, h->wrk2.p, h->wrk2.p, 0);
+  int rc = solve_refined(h, h->wrk2.p, h->wrk2.p);
   if (rc != SMLU_OK) return rc;
   HIPCHK(hipMemcpyAsync(x, h->wrk2.p, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return SMLU_OK;
+}
+
+// Multiple right-hand sides: one solve per column, reusing the captured solve schedule.
+int smlu_solve_multi_device(smlu_handle* h, int64_t nrhs, const double* d_B, int64_t ldb, double* d_X,
+                            int64_t ldx) {
+  if (!h || nrhs < 0 || (nrhs > 0 && (!d_B || !d_X))) return fail(h, SMLU_ERR_ARG, "invalid arguments");
+  if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
+  const int64_t n = h->plan.n;
+  if (ldb < n || ldx < n) return fail(h, SMLU_ERR_ARG, "leading dimension smaller than n");
+  HIPCHK(hipSetDevice(h->device));
+  for (int64_t j = 0; j < nrhs; ++j) {
+    int rc = solve_refined(h, d_B + j * ldb, d_X + j * ldx);
+    if (rc != SMLU_OK) return rc;
+  }
+  return SMLU_OK;
+}
+
+int smlu_solve_multi(smlu_handle* h, int64_t nrhs, const double* B, int64_t ldb, double* X, int64_t ldx) {
+  if (!h || nrhs < 0 || (nrhs > 0 && (!B || !X))) return fail(h, SMLU_ERR_ARG, "invalid arguments");
+  if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
+  const int64_t n = h->plan.n;
+  if (ldb < n || ldx < n) return fail(h, SMLU_ERR_ARG, "leading dimension smaller than n");
+  HIPCHK(hipSetDevice(h->device));
+  for (int64_t j = 0; j < nrhs; ++j) {
+    HIPCHK(hipMemcpyAsync(h->wrk2.p, B + j * ldb, sizeof(double) * n, hipMemcpyHostToDevice, h->stream));
+    int rc = solve_refined(h, h->wrk2.p, h->wrk2.p);
+    if (rc != SMLU_OK) return rc;
+    HIPCHK(hipMemcpyAsync(X + j * ldx, h->wrk2.p, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
+  }
   HIPCHK(hipStreamSynchronize(h->stream));
   return SMLU_OK;
 }
@@ -1566,6 +1665,8 @@ double smlu_stat(const smlu_handle* h, const char* key) {
   if (k == "solve_ms_last") return h->solve_ms;
   if (k == "growth_max") return h->growth_max;
   if (k == "weak") return (double)h->weak;
+  if (k == "refine_steps") return (double)h->refine_steps;
+  if (k == "refine_residual") return h->refine_resid;
   if (k == "gemm_flops") return h->gemm_flops;
   if (k == "gemm22_flops") return h->gemm22_flops;
   if (k == "gemm_launches") return (double)h->gemm_launches;

@@ -47,7 +47,7 @@ class SmluOpts(ctypes.Structure):
         ("profile", i32),
         ("leaf_size", i64),
         ("use_mfma", i32),
-        ("reserved", i32),
+        ("refine", i32),
     ]
 
 
@@ -63,6 +63,9 @@ SIGNATURES = {
     "smlu_refactor_csc": (i32, [vp, i64, vp, vp, vp]),
     "smlu_solve": (i32, [vp, vp, vp]),
     "smlu_solve_device": (i32, [vp, vp, vp]),
+    "smlu_solve_multi": (i32, [vp, i64, vp, i64, vp, i64]),
+    "smlu_solve_multi_device": (i32, [vp, i64, vp, i64, vp, i64]),
+    "smlu_create_i32": (i32, [i64, vp, vp, vp, ctypes.POINTER(SmluOpts), ctypes.POINTER(vp)]),
     "smlu_lsolve": (i32, [vp, vp]),
     "smlu_rsolve": (i32, [vp, vp]),
     "smlu_get_sizes": (i32, [vp, i64p, i64p, i64p]),

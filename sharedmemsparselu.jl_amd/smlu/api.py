@@ -64,7 +64,8 @@ class ParallelSparseLU:
 
     def __init__(self, A, chunk_size=None, *, ordering="auto", grid=None, device=0,
                  profile=False, p=None, q=None, Rs=None, pivot_tol=None, diag_pivot_tol=None,
-                 leaf_size=None, relax=True, use_mfma=None):
+                 leaf_size=None, relax=True, use_mfma=None, refine=None,
+                 int32_indices=False):
         A = _csc(A)
         m, n = A.shape
         if m != n:
@@ -88,6 +89,8 @@ class ParallelSparseLU:
             kw["leaf_size"] = int(leaf_size)
         if use_mfma is not None:
             kw["use_mfma"] = 1 if use_mfma else 0
+        if refine is not None:
+            kw["refine"] = int(refine)
         self._opts = C.default_opts(**kw)
         self.m, self.n = m, n
         self.chunk_size = chunk_size
@@ -103,6 +106,12 @@ class ParallelSparseLU:
             rc = L.smlu_create_with_pivots(n, C.ptr(self._colptr), C.ptr(self._rowval), C.ptr(vals),
                                            C.ptr(pp), C.ptr(qq), C.ptr(rs), ctypes.byref(self._opts),
                                            ctypes.byref(h))
+        elif int32_indices:
+            # SparseMatrixCSC{Float64,Int32}: the Int32 entry point
+            cp32 = np.ascontiguousarray(A.indptr, dtype=np.int32)
+            ri32 = np.ascontiguousarray(A.indices, dtype=np.int32)
+            rc = L.smlu_create_i32(n, C.ptr(cp32), C.ptr(ri32), C.ptr(vals),
+                                   ctypes.byref(self._opts), ctypes.byref(h))
         else:
             rc = L.smlu_create(n, C.ptr(self._colptr), C.ptr(self._rowval), C.ptr(vals),
                                ctypes.byref(self._opts), ctypes.byref(h))
@@ -217,6 +226,18 @@ def ldiv_(x, F: ParallelSparseLU, b):
         raise DimensionMismatch(f"`x` does not have same size as F: length(x)={len(x)}, F.n={F.n}")
     if len(b) != F.n:
         raise DimensionMismatch(f"`b` does not have same size as F: length(b)={len(b)}, F.n={F.n}")
+    if np.ndim(b) == 2 or np.ndim(x) == 2:
+        # several right-hand sides (columns), SURVEY §8f-4: one C-ABI call, column-major buffers
+        if np.shape(x) != np.shape(b):
+            raise DimensionMismatch(f"`x` has size {np.shape(x)}, `b` has size {np.shape(b)}")
+        nrhs = np.shape(b)[1]
+        bb = np.asfortranarray(b, dtype=np.float64)
+        xx = x if (isinstance(x, np.ndarray) and x.dtype == np.float64 and x.flags.f_contiguous) \
+            else np.empty((F.n, nrhs), order="F")
+        _check(C.lib().smlu_solve_multi(F._h, nrhs, C.ptr(bb), F.n, C.ptr(xx), F.n), F._h)
+        if xx is not x:
+            x[:, :] = xx
+        return x
     bb = np.ascontiguousarray(b, dtype=np.float64)
     xx = x if (isinstance(x, np.ndarray) and x.dtype == np.float64 and x.flags.c_contiguous) \
         else np.empty(F.n)

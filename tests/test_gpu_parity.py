@@ -174,3 +174,75 @@ def test_blocked_tile_mode_pivoting(gpu, n):
     ctol = max(DENSE_TOL, 8 * np.finfo(float).eps * np.linalg.cond(D2))
     assert isapprox(x, np.linalg.solve(D2, b), ctol, ctol)
     factor_parity(sp.csc_matrix(D2), F, rtol=1e-10)
+
+
+def _weak_tile_matrix(n, seed):
+    """Dense matrix whose 64x64 diagonal blocks are tiny next to the rows below them: the
+    diagonal-tile pivoting of large fronts has to accept pivots that fail the threshold test
+    (growth > 1/pivot_tol), which the refactor flags as weak pivots."""
+    rng = np.random.default_rng(seed)
+    D = rng.random((n, n))
+    for b0 in range(0, n, 64):
+        b1 = min(n, b0 + 64)
+        D[b0:b1, b0:b1] = 1e-2 * rng.random((b1 - b0, b1 - b0)) + 1e-2 * np.eye(b1 - b0)
+    return D
+
+
+def test_weak_pivots_trigger_refinement(gpu):
+    # SURVEY §8f-2: pivot-failure fallback.  refine=-1 (default) refines only when the
+    # factorization flagged weak pivots; the refined solution meets the dense tolerance.
+    n = 700
+    D = _weak_tile_matrix(n, 21)
+    A = sp.csc_matrix(D)
+    b = np.random.default_rng(4).random(n)
+    xref = np.linalg.solve(D, b)
+    ctol = max(DENSE_TOL, 8 * np.finfo(float).eps * np.linalg.cond(D))
+    F0 = smlu.ParallelSparseLU(A, refine=0)
+    assert F0.stat("weak") > 0, "expected weak pivots in the diagonal-tile path"
+    x0 = np.empty(n)
+    smlu.ldiv_(x0, F0, b)
+    assert F0.stat("refine_steps") == 0
+    F = smlu.ParallelSparseLU(A)
+    x = np.empty(n)
+    smlu.ldiv_(x, F, b)
+    assert F.stat("refine_steps") >= 1
+    e0 = np.linalg.norm(x0 - xref) / np.linalg.norm(xref)
+    e1 = np.linalg.norm(x - xref) / np.linalg.norm(xref)
+    assert e1 <= e0
+    assert isapprox(x, xref, ctol, ctol), (e0, e1)
+    # well-conditioned factorization: no refinement by default, refine=k forces it
+    P = mats.poisson3d(12)
+    G = smlu.ParallelSparseLU(P)
+    xb = np.empty(P.shape[0])
+    smlu.ldiv_(xb, G, np.ones(P.shape[0]))
+    assert G.stat("weak") == 0 and G.stat("refine_steps") == 0
+    G2 = smlu.ParallelSparseLU(P, refine=2)
+    smlu.ldiv_(xb, G2, np.ones(P.shape[0]))
+    assert G2.stat("refine_residual") >= 0
+    assert isapprox(xb, spla.spsolve(P, np.ones(P.shape[0])), TOL, TOL)
+
+
+def test_solve_multiple_rhs(gpu):
+    # ldiv! with a matrix of right-hand sides (SURVEY §8f-4): equals column-by-column solves
+    A = mats.poisson2d(40)
+    n = A.shape[0]
+    F = smlu.ParallelSparseLU(A)
+    B = np.random.default_rng(8).random((n, 5))
+    X = np.empty((n, 5))
+    smlu.ldiv_(X, F, B)
+    for j in range(5):
+        xj = np.empty(n)
+        smlu.ldiv_(xj, F, B[:, j])
+        assert np.array_equal(xj, X[:, j])
+        assert isapprox(xj, spla.spsolve(A, B[:, j]), TOL, TOL)
+    with pytest.raises(smlu.DimensionMismatch):
+        smlu.ldiv_(np.empty((n, 4)), F, B)
+
+
+def test_int32_indices(gpu):
+    # SparseMatrixCSC{Float64,Int32} through smlu_create_i32: same factors as the Int64 path
+    A = mats.poisson3d(10)
+    F64 = smlu.ParallelSparseLU(A)
+    F32 = smlu.ParallelSparseLU(A, int32_indices=True)
+    assert np.array_equal(F64.p, F32.p) and np.array_equal(F64.q, F32.q)
+    assert abs(F64.L - F32.L).max() == 0 and abs(F64.U - F32.U).max() == 0
