@@ -215,14 +215,15 @@ def main():
                        "dense_flops": dense_flops, "ordering": args.ordering,
                        "parallelism": (f"tree-partition{world} (proportional mapping, RCCL p2p)"
                                        if partitioned else f"replicas{world}" if world > 1 else "single")},
-            "roofline": {"bound": "mfma", "kernel": "k_gemm128/k_gemm (fp64 VALU Schur update)",
+            "roofline": {"bound": "mfma", "kernel": "k_gemm128_mfma + k_gemm (fp64 Schur-complement updates)",
                          "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic,
                          "launches_per_step": n_gemm, "avg_launch_us": avg_us,
                          "flops_per_launch": gemm_flops / n_gemm if n_gemm else None,
                          "algorithmic_bytes_per_launch": F.stat("gemm_bytes") / n_gemm if n_gemm else None,
-                         "note": "fp64 VALU (v_fma_f64), no MFMA; peak = MI355X fp64 dense peak; "
+                         "note": "fp64 MFMA (v_mfma_f64_16x16x4) 128x128 tiles for large launches, fp64 VALU "
+                                 "64x64 tiles for small ones; peak = MI355X fp64 dense peak; "
                                  "achieved = GEMM flops per refactor / HIP-event time of the GEMM "
                                  "launches per refactor (graph-captured events on the launch "
                                  "stream); traffic = HBM bytes per launch from rocprofv3 PMC "
