@@ -55,11 +55,18 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
   const int m0 = tm * GBM, n0 = tn * GBN;
   const int tid = threadIdx.x;
   const int tx = tid & 15, ty = tid >> 4;  // 16 x 16 threads, 4x4 each
+  // accumulators start from C (its loads overlap the first K slice's), B is staged negated:
+  // acc = C + sum(A * -B), and the epilogue is stores only
   double acc[4][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + ty + 16 * j;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = 0.0;
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + tx + 16 * i;
+      acc[i][j] = (col < t.n && row < t.m) ? gC[(int64_t)col * t.ldc + row] : 0.0;
+    }
+  }
   // load mapping: A slice GBM x GBK: thread -> (row = tid & 63, kk = (tid >> 6) + 4*r), r<4
   //               B slice GBK x GBN: thread -> (kk = tid & 15, col = (tid >> 4) + 16*r), r<4
   const int ar = tid & 63, ak = tid >> 6;
@@ -80,7 +87,7 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       As[buf][ak + 4 * r][ar] = ra[r];
-      Bs[buf][bk][bc + 16 * r] = rb[r];
+      Bs[buf][bk][bc + 16 * r] = -rb[r];
     }
   };
   int nk = (K + GBK - 1) / GBK;
@@ -105,26 +112,13 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
     if (kt + 1 < nk) sstore(cur ^ 1);
     __syncthreads();
   }
-  // epilogue: every C load issued before any store (the compiler cannot reorder a load past a
-  // possibly aliasing store, so an interleaved read-modify-write pays one memory round trip
-  // per element)
-  double cv[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = n0 + ty + 16 * j;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = m0 + tx + 16 * i;
-      cv[i][j] = (col < t.n && row < t.m) ? gC[(int64_t)col * t.ldc + row] : 0.0;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + ty + 16 * j;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = m0 + tx + 16 * i;
-      if (col < t.n && row < t.m) gC[(int64_t)col * t.ldc + row] = cv[i][j] - acc[i][j];
+      if (col < t.n && row < t.m) gC[(int64_t)col * t.ldc + row] = acc[i][j];
     }
   }
 }
@@ -269,11 +263,21 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
   const int m0 = tm * HBM_, n0 = tn * HBM_;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wr = (wv & 1) * 64, wc = (wv >> 1) * 64;   // wave quadrant (rows, cols)
+  // accumulators start from C (loads overlap the first K slice's), B staged negated in LDS:
+  // acc = C + sum(A * -B); the epilogue is stores only
+  const int li = lane & 15, lk = lane >> 4;
   v4d acc[4][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 4; ++i) {
+    const int row = m0 + wr + 16 * i + li;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (v4d){0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = n0 + wc + 16 * j + lk + 4 * r;
+        acc[i][j][r] = (row < t.m && col < t.n) ? gC[(int64_t)col * t.ldc + row] : 0.0;
+      }
+  }
   const int ar = tid & 127, ak = tid >> 7;
   const int bk = tid & 15, bc = tid >> 4;
   const int K = t.k;
@@ -294,14 +298,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       As[buf][ak + 2 * r][ar] = ra[r];
-      Bs[buf][bk][bc + 16 * r] = rb[r];
+      Bs[buf][bk][bc + 16 * r] = -rb[r];
     }
   };
   const int nk = (K + HBK_ - 1) / HBK_;
   gload(0);
   sstore(0);
   __syncthreads();
-  const int li = lane & 15, lk = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload((kt + 1) * HBK_);
@@ -322,24 +325,15 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
     if (kt + 1 < nk) sstore(cur ^ 1);
     __syncthreads();
   }
-  // epilogue per 16-row block: its 16 C loads in flight, then 16 stores
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = m0 + wr + 16 * i + li;
-    double cv[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int col = n0 + wc + 16 * j + lk + 4 * r;
-        cv[j][r] = (row < t.m && col < t.n) ? gC[(int64_t)col * t.ldc + row] : 0.0;
-      }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int col = n0 + wc + 16 * j + lk + 4 * r;
-        if (row < t.m && col < t.n) gC[(int64_t)col * t.ldc + row] = cv[j][r] - acc[i][j][r];
+        if (row < t.m && col < t.n) gC[(int64_t)col * t.ldc + row] = acc[i][j][r];
       }
   }
 }
