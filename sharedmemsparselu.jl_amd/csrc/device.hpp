@@ -24,7 +24,9 @@ struct SNode {
 };
 
 // C(m x n, ldc) -= A(m x k, lda) * B(k x n, ldb), column-major; tiles of 64 x 64 numbered
-// from tile0 within one launch (tasks sorted by tile0).
+// from tile0 within one launch (tasks sorted by tile0).  C may alias A (C = A, n <= tile width)
+// or B (C = B, m <= tile height): every tile reads all of its A rows / B columns before it
+// stores, which the GEMM-form triangular solves use (C - (I - T^-1) C = T^-1 C).
 struct GemmTask {
   const double* A;
   const double* B;
@@ -32,6 +34,7 @@ struct GemmTask {
   int32_t m, n, k;
   int32_t lda, ldb, ldc;
   int32_t tiles_m;
+  int32_t gsid = -1; // >= 0: growth check of the result (GEMM-form TRSM of front gsid's L rows)
   int64_t tile0;
 };
 

@@ -39,10 +39,25 @@ __device__ __forceinline__ void tile_rc(const GemmTask& t, int64_t tl, int& tm, 
   tn = (int)(in / gm);
 }
 
+// Growth check of a GEMM-form triangular solve (task.gsid >= 0): max |result| of the tile, folded
+// into growth[0] and the front's weak-pivot bit exactly as k_step_trsm does for its L rows.
+struct GrowthArgs {
+  int32_t* info;
+  double* growth;
+  double piv_tol;
+};
+__device__ __forceinline__ void tile_growth(const GrowthArgs& ga, int sid, double g) {
+  g = wave_max(g);
+  if ((threadIdx.x & 63) == 0 && g > 0.0) {
+    atomic_max_pos(&ga.growth[0], g);
+    if (g > 1.0 / ga.piv_tol) atomicOr(&ga.info[sid], 2);
+  }
+}
+
 #define GBM 64
 #define GBN 64
 #define GBK 16
-__global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks, int ntask) {
+__global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks, int ntask, GrowthArgs ga) {
   __shared__ double As[2][GBK][GBM + 2];
   __shared__ double Bs[2][GBK][GBN + 2];
   const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
@@ -112,15 +127,20 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
     if (kt + 1 < nk) sstore(cur ^ 1);
     __syncthreads();
   }
+  double gmax = 0.0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int col = n0 + ty + 16 * j;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = m0 + tx + 16 * i;
-      if (col < t.n && row < t.m) gC[(int64_t)col * t.ldc + row] = acc[i][j];
+      if (col < t.n && row < t.m) {
+        gC[(int64_t)col * t.ldc + row] = acc[i][j];
+        gmax = fmax(gmax, fabs(acc[i][j]));
+      }
     }
   }
+  if (t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
 }
 
 // ------------------------------------------------------------------------------------
@@ -250,7 +270,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__
 // C[row = 16 bi + (l & 15)][col = 16 bj + (l >> 4) + 4 r], r = 0..3.
 // ------------------------------------------------------------------------------------
 typedef double v4d __attribute__((ext_vector_type(4)));
-__global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restrict__ tasks, int ntask) {
+__global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restrict__ tasks, int ntask,
+                                                         GrowthArgs ga) {
   __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
   __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
   const int64_t b = blockIdx.x;
@@ -325,6 +346,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
     if (kt + 1 < nk) sstore(cur ^ 1);
     __syncthreads();
   }
+  double gmax = 0.0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = m0 + wr + 16 * i + li;
@@ -333,24 +355,119 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int col = n0 + wc + 16 * j + lk + 4 * r;
-        if (row < t.m && col < t.n) gC[(int64_t)col * t.ldc + row] = acc[i][j][r];
+        if (row < t.m && col < t.n) {
+          gC[(int64_t)col * t.ldc + row] = acc[i][j][r];
+          gmax = fmax(gmax, fabs(acc[i][j][r]));
+        }
       }
   }
+  if (t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
 }
 
 
 
 // ------------------------------------------------------------------------------------
+// Inverses of a factored 64 x 64 diagonal tile for the GEMM-form triangular solves:
+//   NL = I - L_kk^{-1} (L unit lower: the strictly lower part of the tile),
+//   NU = I - U_kk^{-1} (U upper with its diagonal),
+// column-major with ld 64 at tinv + slot * 8192 (NL) and + 4096 (NU).  A partial panel
+// (w < 64) is padded with the identity, so NL/NU vanish outside the w x w block.
+// 8 workgroups per front (4 for NL, 4 for NU); a wave computes 4 columns at once by column
+// sweep: lane i holds row i, step j broadcasts the finished entry j by v_readlane and every
+// lane below (L) / above (U) subtracts its tile entry times it -- one LDS read feeds 4 FMAs.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_tri_inv(const int32_t* __restrict__ list, int step,
+                                                 const SNode* __restrict__ sn,
+                                                 double* __restrict__ store,
+                                                 double* __restrict__ scratch,
+                                                 double* __restrict__ tinv) {
+  __shared__ double sD[64 * 65];   // tile [col][row], ld 65
+  const int item = blockIdx.x >> 3, part = blockIdx.x & 7;
+  const int sid = list[2 * item];
+  const int64_t slot = list[2 * item + 1];
+  const SNode s = sn[sid];
+  FrontPtrs f = front_ptrs(s, store, scratch);
+  const int64_t M = f.M;
+  const int kb = step * s.nb;
+  const int w = min(s.nb, (int)f.ns - kb);
+  const gdbl* D = f.L + (int64_t)kb * M + kb;
+  {
+    double v[16];   // all 16 loads in flight before the LDS stores
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int idx = threadIdx.x + 256 * u, i = idx & 63, j = idx >> 6;
+      v[u] = (i < w && j < w) ? D[(int64_t)j * M + i] : (i == j ? 1.0 : 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int idx = threadIdx.x + 256 * u, i = idx & 63, j = idx >> 6;
+      sD[j * 65 + i] = v[u];
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool upper = part >= 4;
+  const int c0 = ((part & 3) * 4 + wv) * 4;   // this wave's columns c0 .. c0+3
+  double z[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) z[r] = lane == c0 + r ? 1.0 : 0.0;
+  double* out = tinv + slot * 8192 + (upper ? 4096 : 0);
+  if (!upper) {
+    // L z = e_c: z_j is final at step j; rows i > j subtract L[i][j] z_j
+#pragma unroll 4
+    for (int j = 0; j < 63; ++j) {
+      const double lij = sD[j * 65 + lane];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double zj = readlane_f64(z[r], j);
+        if (lane > j) z[r] = fma(-lij, zj, z[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[(int64_t)(c0 + r) * 64 + lane] = lane > c0 + r ? -z[r] : 0.0;
+  } else {
+    // U y = e_c: y_j is final at step j after its division; rows i < j subtract U[i][j] y_j
+    const double rd = recip(sD[lane * 65 + lane]);
+#pragma unroll 4
+    for (int j = 63; j >= 0; --j) {
+      const double uij = sD[j * 65 + lane];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (lane == j) z[r] *= rd;
+        const double yj = readlane_f64(z[r], j);
+        if (lane < j) z[r] = fma(-uij, yj, z[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = c0 + r;
+      out[(int64_t)c * 64 + lane] = lane == c ? 1.0 - z[r] : (lane < c ? -z[r] : 0.0);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Host-side launch wrappers (called from smlu.cpp)
 // ------------------------------------------------------------------------------------
-hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask, int tile,
-                       int64_t maxwg) {
+hipError_t launch_gemm_g(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask, int tile,
+                         int64_t maxwg, int32_t* info, double* growth, double piv_tol) {
   if (ntiles <= 0) return hipSuccess;
-  if (tile == 129) k_gemm128_mfma<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
-  else if (tile == 128)
+  const GrowthArgs ga{info, growth, piv_tol};
+  if (tile == 129) k_gemm128_mfma<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  else if (tile == 128)   // VALU 128 tile (SMLU_VALU_GEMM only): no growth epilogue
     k_gemm128<<<(unsigned)(maxwg > 0 ? std::min<int64_t>(ntiles, maxwg) : ntiles), 256, 0, st>>>(
         tasks, ntask, ntiles);
-  else k_gemm<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask);
+  else k_gemm<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  return hipGetLastError();
+}
+hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask, int tile,
+                       int64_t maxwg) {
+  return launch_gemm_g(st, ntiles, tasks, ntask, tile, maxwg, nullptr, nullptr, 1.0);
+}
+hipError_t launch_tri_inv(hipStream_t st, int cnt, int step, const int32_t* list, const SNode* sn,
+                          double* store, double* scratch, double* tinv) {
+  if (cnt <= 0) return hipSuccess;
+  k_tri_inv<<<(unsigned)cnt * 8, 256, 0, st>>>(list, step, sn, store, scratch, tinv);
   return hipGetLastError();
 }
 

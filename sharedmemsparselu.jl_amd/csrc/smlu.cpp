@@ -46,6 +46,8 @@ hipError_t launch_laswp(hipStream_t, int64_t, const SwapTask*, int, const SNode*
 hipError_t launch_trsm_u(hipStream_t, int64_t, const FrontTile*, int, int, int, const SNode*, double*,
                          double*, const int32_t*, int64_t);
 hipError_t launch_gemm(hipStream_t, int64_t, const GemmTask*, int, int, int64_t);
+hipError_t launch_gemm_g(hipStream_t, int64_t, const GemmTask*, int, int, int64_t, int32_t*, double*, double);
+hipError_t launch_tri_inv(hipStream_t, int, int, const int32_t*, const SNode*, double*, double*, double*);
 hipError_t launch_fwd_gather(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                              const int32_t*, double*, double*);
 hipError_t launch_tri_block(hipStream_t, bool, int64_t, const FrontTile*, int, int, const SNode*,
@@ -81,11 +83,11 @@ thread_local std::string g_last_error;
 enum Kind : int {
   K_MEMSET_STORE, K_MEMSET_SCRATCH, K_SCATTER, K_EXTADD, K_FRONT_LDS, K_PANEL, K_TRSMU, K_TRSML,
   K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_GEMM22, K_LASWP, K_STEPTRSM, K_GEMMU,
-  K_GEMMO, K_FORK, K_JOIN, K_NKIND
+  K_GEMMO, K_FORK, K_JOIN, K_TRIINV, K_NKIND
 };
 const char* kKindName[K_NKIND] = {"memset", "memset", "assemble", "assemble", "small", "panel",
                                   "trsm", "trsm", "gemm", "solve", "solve", "solve", "solve",
-                                  "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "sync", "sync"};
+                                  "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "sync", "sync", "trsm"};
 constexpr int kSolveBigNs = 256;  // fronts with more pivots use the multi-workgroup solve
 
 struct Launch {
@@ -137,6 +139,7 @@ struct smlu_handle {
   bool given_Rs = false;
   // device buffers
   DBuf<double> A, Rs, store, scratch, wrk, wrk2, vbuf, growth;
+  DBuf<double> tinv;   // per (front, sub-panel) slot: I - L_kk^-1 and I - U_kk^-1 (GEMM-form TRSM)
   DBuf<double> ref_b, ref_r, ref_d, ref_nrm;   // iterative refinement (allocated on first use)
   DBuf<int32_t> Acol;                          // column of each A entry (residuals)
   int refine_steps = 0;
@@ -179,12 +182,15 @@ struct smlu_handle {
   bool lookahead = false;     // SMLU_LOOKAHEAD=1: trailing updates beyond the next block on a side stream
   int ob = kOBDefault;        // outer block width (SMLU_OB overrides; multiple of 64)
   int64_t t128_min = 512;     // 128x128 GEMM tiles when a launch has at least this many
-  int64_t side_wg = 0;        // grid cap of look-ahead GEMMs (SMLU_SIDE_WG; 0 = uncapped)          // batched-LDS full-width triangular solves (SMLU_SLOW_TRSM=1: off)
+  bool trsm_gemm = true;      // GEMM-form triangular solves of the blocked fronts
+  bool trsm_gemm64_only = false;   // SMLU_TRSM_GEMM=2: only for diagonal-tile (nb = 64) fronts
+  int64_t side_wg = 0;        // grid cap of look-ahead GEMMs (SMLU_SIDE_WG; 0 = uncapped)
   ~smlu_handle() { release_all(); }
   void release_buffers() {
     if (stream) (void)hipSetDevice(device);
     release_graphs();
-    DBuf<double>* d[] = {&A, &Rs, &store, &scratch, &wrk, &wrk2, &vbuf, &growth, &ref_b, &ref_r, &ref_d, &ref_nrm};
+    DBuf<double>* d[] = {&A, &Rs, &store, &scratch, &wrk, &wrk2, &vbuf, &growth, &ref_b, &ref_r, &ref_d, &ref_nrm,
+                         &tinv};
     Acol.free();
     for (auto* b : d) b->free();
     DBuf<int64_t>* l[] = {&Arowptr, &Adest, &p0, &q, &posfirst};
@@ -340,6 +346,15 @@ static int build_schedule(smlu_handle* h) {
   if (const char* e = std::getenv("SMLU_SIDE_WG")) h->side_wg = std::atoll(e);
   if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
   if (const char* e = std::getenv("SMLU_T128MIN")) h->t128_min = std::atoll(e);
+  // GEMM-form TRSM (k_tri_inv + GEMM tasks) needs the growth epilogue of the MFMA/64 tiles
+  {
+    const char* e = std::getenv("SMLU_TRSM_GEMM");
+    const int v = e ? std::atoi(e) : 2;   // 2 measured best: 32-wide panels keep k_step_trsm
+    h->trsm_gemm = h->opts.use_mfma && v != 0;
+    h->trsm_gemm64_only = v == 2;
+  }
+  // GEMM tasks whose A or B operand lives in the tinv buffer (allocated after the schedule)
+  std::vector<std::pair<int64_t, int64_t>> tinv_patch;   // (gt index * 2 + operand B?, offset)
   h->gemm_flops = 0;
   h->gemm_launches = h->gemm128_launches = 0;
   h->gemm_bytes = 0;
@@ -349,8 +364,9 @@ static int build_schedule(smlu_handle* h) {
   // GEMM launches: 128x128 tiles when the launch has enough of them to fill the GPU,
   // otherwise 64x64 tiles (same per-element arithmetic, bitwise-identical results).
   auto add_gemm_launch = [&](std::vector<GemmTask>& cand, double fl, int step, int kind = K_GEMM,
-                             int side = 0) {
+                             int side = 0, const std::vector<int64_t>* tpatch = nullptr) {
     if (cand.empty()) return;
+    const bool count = kind != K_TRSML;   // GEMM-form TRSM is accounted as "trsm", not GEMM
     int64_t t128 = 0;
     for (auto& g : cand) t128 += (int64_t)((g.m + 127) / 128) * ((g.n + 127) / 128);
     int tile = t128 >= h->t128_min ? 128 : 64;
@@ -363,8 +379,10 @@ static int build_schedule(smlu_handle* h) {
     L.aux = tile;
     int64_t tiles = 0;
     const int ts = tile == 129 ? 128 : tile;
-    for (auto& g : cand) {
-      h->gemm_bytes += 8.0 * ((double)g.m * g.k + (double)g.k * g.n + 2.0 * g.m * g.n);
+    for (size_t i = 0; i < cand.size(); ++i) {
+      GemmTask& g = cand[i];
+      if (count) h->gemm_bytes += 8.0 * ((double)g.m * g.k + (double)g.k * g.n + 2.0 * g.m * g.n);
+      if (tpatch && (*tpatch)[i] >= 0) tinv_patch.push_back({(int64_t)gt.size(), (*tpatch)[i]});
       g.tiles_m = (g.m + ts - 1) / ts;
       g.tile0 = tiles;
       tiles += (int64_t)g.tiles_m * ((g.n + ts - 1) / ts);
@@ -374,11 +392,14 @@ static int build_schedule(smlu_handle* h) {
     L.nwg = tiles;
     L.flops = fl;
     h->fac.push_back(L);
+    if (!count) return;
     h->gemm_flops += fl;
     ++h->gemm_launches;
     if (tile != 64) ++h->gemm128_launches;
     if (step < 0) h->gemm22_flops += fl;
   };
+  // tinv operand encoding in tpatch: offset * 2 + (1 if the operand is B, 0 if A)
+  auto tinv_slot_off = [](int64_t slot, bool upper) { return slot * 8192 + (upper ? 4096 : 0); };
   for (int l = 0; l < P.nlevels; ++l) {
     Launch L;
     if (isx[l]) h->fac_seg.push_back(h->fac.size());   // exchange point before this level
@@ -519,6 +540,23 @@ static int build_schedule(smlu_handle* h) {
         }
         if (pos != act.size()) return fail(h, SMLU_ERR_ARG, "internal: panel classes");
       }
+      auto gform = [&](int64_t s) {
+        return h->trsm_gemm && (h->hsn[s].nb == kNbTile || !h->trsm_gemm64_only);
+      };
+      // inverses of the diagonal tiles of the GEMM-form fronts (I - L_kk^-1, I - U_kk^-1)
+      {
+        L = Launch();
+        L.kind = K_TRIINV;
+        L.step = (int)t;
+        L.off = (int64_t)ilist.size();
+        for (auto s : act) {
+          if (!gform(s)) continue;
+          ilist.push_back((int32_t)s);
+          ilist.push_back((int32_t)slot_of(s, t % (h->ob / h->hsn[s].nb)));
+        }
+        L.cnt = ((int64_t)ilist.size() - L.off) / 2;
+        if (L.cnt > 0) h->fac.push_back(L);
+      }
       // row swaps inside the outer block (the other columns get them at the end of the block)
       {
         L = Launch();
@@ -545,8 +583,10 @@ static int build_schedule(smlu_handle* h) {
         T.kind = K_STEPTRSM;
         T.step = (int)t;
         T.off = (int64_t)ft.size();
-        int64_t wgU = 0, W = 32;
+        int64_t wgU = 0, W = 32, ntri = 0;
         for (auto s : act) {
+          if (gform(s)) continue;
+          ++ntri;
           const SNode& r = h->hsn[s];
           int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
           int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
@@ -554,21 +594,56 @@ static int build_schedule(smlu_handle* h) {
           wgU += (oend - kb - w + 255) / 256;
           W = std::max<int64_t>(W, w);
         }
-        T.cnt = (int64_t)act.size();
+        T.cnt = ntri;
         T.nwg = wgU;
         T.off2 = (int64_t)ft.size();
         int64_t wgL = 0;
         for (auto s : act) {
+          if (gform(s)) continue;
           const SNode& r = h->hsn[s];
           int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
           int64_t R = r.mode == 1 ? r.ns - kb : w;
           ft.push_back(FrontTile{(int32_t)s, (int32_t)kb, wgL});
           wgL += (M - kb - R + 255) / 256;
         }
-        T.cnt2 = (int64_t)act.size();
+        T.cnt2 = ntri;
         T.nwg2 = wgL;
         T.aux = W;
         if (wgU + wgL > 0) h->fac.push_back(T);
+      }
+      // GEMM-form step TRSM of the blocked fronts, in place (R = rows the panel finished:
+      // w for diagonal-tile panels, every fully-summed row for full-candidate panels):
+      //   U rows [kb, kb+w) x columns [kb+w, oend):  C - (I - L_kk^-1) C = L_kk^-1 C
+      //   L rows [kb+R, M) x columns [kb, kb+w):     C - C (I - U_kk^-1) = C U_kk^-1 (+ growth)
+      {
+        std::vector<GemmTask> cand;
+        std::vector<int64_t> tp;
+        for (auto s : act) {
+          if (!gform(s)) continue;
+          const SNode& r = h->hsn[s];
+          int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
+          int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
+          const int64_t slot = slot_of(s, t % (h->ob / r.nb));
+          if (oend - kb - w > 0) {
+            GemmTask g{};
+            g.B = g.C = store + r.Loff + (kb + w) * M + kb;
+            g.m = (int)w; g.n = (int)(oend - kb - w); g.k = (int)w;
+            g.lda = 64; g.ldb = (int)M; g.ldc = (int)M;
+            cand.push_back(g);
+            tp.push_back(tinv_slot_off(slot, false) * 2);
+          }
+          const int64_t R = r.mode == 1 ? r.ns - kb : w;   // rows the panel already finished
+          if (M - kb - R > 0) {
+            GemmTask g{};
+            g.A = g.C = store + r.Loff + kb * M + kb + R;
+            g.m = (int)(M - kb - R); g.n = (int)w; g.k = (int)w;
+            g.lda = (int)M; g.ldb = 64; g.ldc = (int)M;
+            g.gsid = (int32_t)s;
+            cand.push_back(g);
+            tp.push_back(tinv_slot_off(slot, true) * 2 + 1);
+          }
+        }
+        add_gemm_launch(cand, 0.0, (int)t, K_TRSML, 0, &tp);
       }
       // inner trailing update: rows [kb+w, M) x columns [kb+w, oend) of the outer block
       {
@@ -642,7 +717,8 @@ static int build_schedule(smlu_handle* h) {
         L.aux = 1;   // outer mode
         L.off = (int64_t)ft.size();
         int64_t wg = 0, cnt = 0;
-        std::vector<GemmTask> cand;
+        std::vector<GemmTask> cand, ctri;
+        std::vector<int64_t> tp;
         double fl = 0;
         for (auto s : fin) {
           const SNode& r = h->hsn[s];
@@ -651,9 +727,29 @@ static int build_schedule(smlu_handle* h) {
           int64_t kbu = ostart + u * r.nb;
           if (kbu >= oend) continue;
           int64_t wu = std::min<int64_t>(r.nb, oend - kbu);
-          ft.push_back(FrontTile{(int32_t)s, (int32_t)kbu, wg});
-          wg += (M - oend + 255) / 256;
-          ++cnt;
+          if (gform(s)) {   // U rows [kbu, kbu+wu) right of the block: L_uu^-1 C, in place
+            const int64_t off = tinv_slot_off(slot_of(s, u), false) * 2;
+            if (r.ns - oend > 0) {
+              GemmTask g{};
+              g.B = g.C = store + r.Loff + oend * M + kbu;
+              g.m = (int)wu; g.n = (int)(r.ns - oend); g.k = (int)wu;
+              g.lda = 64; g.ldb = (int)M; g.ldc = (int)M;
+              ctri.push_back(g);
+              tp.push_back(off);
+            }
+            if (r.nu > 0) {
+              GemmTask g{};
+              g.B = g.C = store + r.Uoff + kbu;
+              g.m = (int)wu; g.n = r.nu; g.k = (int)wu;
+              g.lda = 64; g.ldb = r.ns; g.ldc = r.ns;
+              ctri.push_back(g);
+              tp.push_back(off);
+            }
+          } else {
+            ft.push_back(FrontTile{(int32_t)s, (int32_t)kbu, wg});
+            wg += (M - oend + 255) / 256;
+            ++cnt;
+          }
           // (b) rows below the sub-panel inside the block: [kbu+wu, oend) x [oend, M)
           int64_t m = oend - kbu - wu;
           if (m > 0) {
@@ -683,6 +779,7 @@ static int build_schedule(smlu_handle* h) {
         L.cnt = cnt;
         L.nwg = wg;
         if (wg > 0) h->fac.push_back(L);
+        add_gemm_launch(ctri, 0.0, (int)t, K_TRSML, 0, &tp);
         add_gemm_launch(cand, fl, (int)t, K_GEMMU);
       }
       // (c) trailing update, k = oend - ostart <= 256.  With look-ahead the columns of the next
@@ -879,6 +976,14 @@ static int build_schedule(smlu_handle* h) {
   HIPCHK(h->ilist.upload(ilist.data(), ilist.size(), st));
   HIPCHK(h->xtasks.upload(xt.data(), xt.size(), st));
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
+  if (!tinv_patch.empty()) {   // operands in the tile-inverse slots: patch in the buffer address
+    HIPCHK(h->tinv.alloc((size_t)max_list * 8192));
+    for (auto& pt : tinv_patch) {
+      const double* a = h->tinv.p + pt.second / 2;
+      if (pt.second & 1) gt[pt.first].B = a;
+      else gt[pt.first].A = a;
+    }
+  }
   HIPCHK(h->gtasks.upload(gt.data(), gt.size(), st));
   HIPCHK(h->stasks.upload(st_tasks.data(), st_tasks.size(), st));
   HIPCHK(h->xcols.upload(xc.data(), xc.size(), st));
@@ -1036,6 +1141,12 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
     case K_GEMMO:
     case K_GEMM22:
       return launch_gemm(st, L.nwg, h->gtasks.p + L.off, (int)L.cnt, (int)L.aux, L.side ? h->side_wg : 0);
+    case K_TRSML:
+      return launch_gemm_g(st, L.nwg, h->gtasks.p + L.off, (int)L.cnt, (int)L.aux, 0, h->info.p,
+                           h->growth.p, piv_tol);
+    case K_TRIINV:
+      return launch_tri_inv(st, (int)L.cnt, L.step, h->ilist.p + L.off, h->sn.p, h->store.p, h->scratch.p,
+                            h->tinv.p);
   }
   return hipErrorInvalidValue;
 }
