@@ -57,6 +57,9 @@ __device__ __forceinline__ void tile_growth(const GrowthArgs& ga, int sid, doubl
 #define GBM 64
 #define GBN 64
 #define GBK 16
+// TRSM = true: the GEMM-form triangular-solve launches (growth epilogue; a separate symbol so
+// that profiles tell them apart from the Schur-complement updates)
+template <bool TRSM>
 __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks, int ntask, GrowthArgs ga) {
   __shared__ double As[2][GBK][GBM + 2];
   __shared__ double Bs[2][GBK][GBN + 2];
@@ -140,7 +143,7 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
       }
     }
   }
-  if (t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
+  if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
 }
 
 // ------------------------------------------------------------------------------------
@@ -270,6 +273,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__
 // C[row = 16 bi + (l & 15)][col = 16 bj + (l >> 4) + 4 r], r = 0..3.
 // ------------------------------------------------------------------------------------
 typedef double v4d __attribute__((ext_vector_type(4)));
+template <bool TRSM>
 __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restrict__ tasks, int ntask,
                                                          GrowthArgs ga) {
   __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
@@ -361,7 +365,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
         }
       }
   }
-  if (t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
+  if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
 }
 
 
@@ -453,11 +457,14 @@ hipError_t launch_gemm_g(hipStream_t st, int64_t ntiles, const GemmTask* tasks, 
                          int64_t maxwg, int32_t* info, double* growth, double piv_tol) {
   if (ntiles <= 0) return hipSuccess;
   const GrowthArgs ga{info, growth, piv_tol};
-  if (tile == 129) k_gemm128_mfma<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 128)   // VALU 128 tile (SMLU_VALU_GEMM only): no growth epilogue
+  const bool trsm = info != nullptr;
+  if (tile == 129 && trsm) k_gemm128_mfma<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  else if (tile == 129) k_gemm128_mfma<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  else if (tile == 128)   // VALU 128 tile (SMLU_VALU_GEMM only; never used for the TRSM form)
     k_gemm128<<<(unsigned)(maxwg > 0 ? std::min<int64_t>(ntiles, maxwg) : ntiles), 256, 0, st>>>(
         tasks, ntask, ntiles);
-  else k_gemm<<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  else if (trsm) k_gemm<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  else k_gemm<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   return hipGetLastError();
 }
 hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask, int tile,

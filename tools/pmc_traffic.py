@@ -17,10 +17,14 @@ base = "gpurun_out"
 
 
 def load(counter):
+    """Per-kernel totals of the Schur-update GEMMs (the <false> instantiations; the <true> ones
+    are the GEMM-form triangular solves, accounted as "trsm")."""
     path = os.path.join(base, f"pmc_{counter}_{N}", "pmc_counter_collection.csv")
     per = {}
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"].split("(")[0]
+        if "<true>" in name:
+            continue
         d = per.setdefault(name, [0, 0.0])
         d[0] += 1
         d[1] += float(r["Counter_Value"])
