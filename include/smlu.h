@@ -126,6 +126,18 @@ int smlu_lsolve(smlu_handle* h, double* x);
 /* rsolve!(F, x) — src/SharedMemSparseLU.jl:374-392: in place U \ x. */
 int smlu_rsolve(smlu_handle* h, double* x);
 
+/* The reference's own dense-chunk solve layout on the GPU, a parity mode for
+ * small banded systems: chunk geometry, negated rectangles and back-to-front U chunks as
+ * get_chunking_parameters / allocate_chunks / fill_chunks! (src/SharedMemSparseLU.jl:101-243)
+ * build them from the current factors (chunk_size <= 0: 8, as :67-70; clamped to n, :72).
+ * smlu_chunked_ldiv is ldiv! (:286-342) with lsolve!/rsolve! (:349-392) done chunk by chunk
+ * (trsv on the diagonal block, then x[rows] += Rect*x[cols]); x may alias b.  The chunks are
+ * refilled automatically after a refactor (as lu! does, :265-276).  Refuses (SMLU_ERR_ALLOC)
+ * layouts above 32 GB -- the reference's layout is dense and infeasible for large fill. */
+int smlu_chunked_setup(smlu_handle* h, int64_t chunk_size);
+int smlu_chunked_ldiv(smlu_handle* h, const double* b, double* x);
+int smlu_chunked_ldiv_device(smlu_handle* h, const double* d_b, double* d_x);
+
 /* Sizes for smlu_get_factors: n, nnz(L) (incl. unit diagonal), nnz(U). */
 int smlu_get_sizes(smlu_handle* h, int64_t* n, int64_t* nnz_L, int64_t* nnz_U);
 

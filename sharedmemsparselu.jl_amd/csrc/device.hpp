@@ -62,4 +62,11 @@ struct SwapTask {
   int64_t wg0;
 };
 
+// One dense chunk of the reference's solve layout (src/SharedMemSparseLU.jl:101-243), 0-based:
+// the s x s diagonal block over x[c0, c0+s) at data[tri] (column-major, ld s) and the negated
+// nr x s rectangle over rows x[r0, r0+nr) at data[rect] (column-major, ld nr).
+struct ChunkDesc {
+  int64_t c0, s, r0, nr, tri, rect;
+};
+
 }  // namespace smlu

@@ -369,6 +369,55 @@ hipError_t launch_perm_out_masked(hipStream_t st, int64_t n, const int64_t* q, c
   k_perm_out_masked<<<nblk(n, 256), 256, 0, st>>>(n, q, own, wrk, x);
   return hipGetLastError();
 }
+// ------------------------------------------------------------------------------------
+// The reference's chunked triangular solves: lsolve! (src/SharedMemSparseLU.jl:
+// 349-367) and rsolve! (:374-392) chunk by chunk in the reference's order -- trsv! on the
+// diagonal block (dtrsv 'L','N','U' / 'U','N','N', column sweep), then x[rows] += Rect*x[cols]
+// with the negated rectangle (gemm! with alpha = beta = 1, quirk Q3).  One workgroup walks the
+// chunks in sequence (each chunk depends on the previous); rectangle rows are spread over its
+// 256 threads.  A parity mode for small banded systems, not the fast path.
+// ------------------------------------------------------------------------------------
+template <bool UPPER>
+__global__ __launch_bounds__(256) void k_chunked_solve(int64_t nchunk, const ChunkDesc* __restrict__ desc,
+                                                       const double* __restrict__ data,
+                                                       double* __restrict__ x) {
+  for (int64_t c = 0; c < nchunk; ++c) {
+    const ChunkDesc d = desc[c];
+    const double* T = data + d.tri;
+    double* xs = x + d.c0;
+    if (threadIdx.x == 0) {
+      if (!UPPER) {
+        for (int64_t j = 0; j < d.s; ++j) {
+          const double xj = xs[j];
+          for (int64_t i = j + 1; i < d.s; ++i) xs[i] = fma(-T[j * d.s + i], xj, xs[i]);
+        }
+      } else {
+        for (int64_t j = d.s - 1; j >= 0; --j) {
+          xs[j] = xs[j] / T[j * d.s + j];
+          const double xj = xs[j];
+          for (int64_t i = 0; i < j; ++i) xs[i] = fma(-T[j * d.s + i], xj, xs[i]);
+        }
+      }
+    }
+    __syncthreads();
+    const double* Rc = data + d.rect;
+    for (int64_t r = threadIdx.x; r < d.nr; r += 256) {
+      double acc = x[d.r0 + r];
+      for (int64_t j = 0; j < d.s; ++j) acc = fma(Rc[j * d.nr + r], xs[j], acc);
+      x[d.r0 + r] = acc;
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_chunked_solve(hipStream_t st, bool upper, int64_t nchunk, const ChunkDesc* desc,
+                                const double* data, double* x) {
+  if (nchunk <= 0) return hipSuccess;
+  if (upper) k_chunked_solve<true><<<1, 256, 0, st>>>(nchunk, desc, data, x);
+  else k_chunked_solve<false><<<1, 256, 0, st>>>(nchunk, desc, data, x);
+  return hipGetLastError();
+}
+
 hipError_t launch_perm_out(hipStream_t st, int64_t n, const int64_t* q, const double* wrk, double* x) {
   k_perm_out<<<nblk(n, 256), 256, 0, st>>>(n, q, wrk, x);
   return hipGetLastError();

@@ -63,6 +63,7 @@ hipError_t launch_residual(hipStream_t, int64_t, const int64_t*, const int32_t*,
 hipError_t launch_axpy1(hipStream_t, int64_t, const double*, double*);
 hipError_t launch_perm_in(hipStream_t, int64_t, const int64_t*, const double*, const double*, double*);
 hipError_t launch_perm_out(hipStream_t, int64_t, const int64_t*, const double*, double*);
+hipError_t launch_chunked_solve(hipStream_t, bool, int64_t, const ChunkDesc*, const double*, double*);
 hipError_t launch_perm_out_masked(hipStream_t, int64_t, const int64_t*, const int8_t*, const double*, double*);
 hipError_t launch_unswap(hipStream_t, int64_t, const int64_t*, const int32_t*, const double*, double*);
 }  // namespace smlu
@@ -140,6 +141,12 @@ struct smlu_handle {
   // device buffers
   DBuf<double> A, Rs, store, scratch, wrk, wrk2, vbuf, growth;
   DBuf<double> tinv;   // per (front, sub-panel) slot: I - L_kk^-1 and I - U_kk^-1 (GEMM-form TRSM)
+  // the reference's dense-chunk solve layout, rebuilt after each factorization
+  DBuf<double> ch_data;
+  DBuf<ChunkDesc> ch_desc;   // L chunks [0, ch_T), U chunks [ch_T, 2 ch_T)
+  DBuf<int64_t> ch_p, ch_q;
+  int64_t ch_T = 0, ch_size = 0, ch_version = -1;
+  int64_t nfactor = 0;       // completed numeric factorizations
   DBuf<double> ref_b, ref_r, ref_d, ref_nrm;   // iterative refinement (allocated on first use)
   DBuf<int32_t> Acol;                          // column of each A entry (residuals)
   int refine_steps = 0;
@@ -190,7 +197,11 @@ struct smlu_handle {
     if (stream) (void)hipSetDevice(device);
     release_graphs();
     DBuf<double>* d[] = {&A, &Rs, &store, &scratch, &wrk, &wrk2, &vbuf, &growth, &ref_b, &ref_r, &ref_d, &ref_nrm,
-                         &tinv};
+                         &tinv, &ch_data};
+    ch_desc.free();
+    ch_p.free();
+    ch_q.free();
+    ch_version = -1;
     Acol.free();
     for (auto* b : d) b->free();
     DBuf<int64_t>* l[] = {&Arowptr, &Adest, &p0, &q, &posfirst};
@@ -1245,6 +1256,7 @@ static int finish_factor(smlu_handle* h, Timer& tm, std::chrono::steady_clock::t
   h->refactor_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   h->growth_max = g;
   h->have_numeric = true;
+  ++h->nfactor;
   h->weak = 0;
   h->errcol = -1;
   int rc = SMLU_OK;
@@ -1738,6 +1750,127 @@ int smlu_get_factors(smlu_handle* h, int64_t* Lcolptr, int64_t* Lrowval, double*
   return SMLU_OK;
 }
 
+// ---- the reference's dense-chunk solve layout on the GPU -------------------
+// Chunk geometry, negated rectangles and back-to-front U chunks exactly as
+// get_chunking_parameters / allocate_chunks / fill_chunks! (src/SharedMemSparseLU.jl:101-243)
+// lay them out (quirks Q1-Q4 of SURVEY appendix B), built from the current factors.
+int smlu_chunked_setup(smlu_handle* h, int64_t chunk_size) {
+  if (!h) return fail(h, SMLU_ERR_ARG, "NULL handle");
+  if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  Exported X;
+  int rc = export_factors(h, X, true);
+  if (rc != SMLU_OK) return rc;
+  const int64_t n = h->plan.n, m = n;
+  int64_t cs = chunk_size > 0 ? chunk_size : 8;   // :67-70
+  cs = std::min(cs, n);                           // :72 (clamped with A.n)
+  const int64_t T = (m + cs - 1) / cs;            // :108 (with m, quirk Q1)
+  {   // the layout is dense per chunk (the reference's): refuse what cannot fit
+    double total = 0;
+    for (int64_t c = 0; c < T; ++c) {
+      const int64_t cmin = c * cs, cmax = std::min(m, (c + 1) * cs), s = cmax - cmin;
+      int64_t rmax = cmax, rmin = cmin;
+      for (int64_t j = cmin; j < cmax; ++j) {
+        if (X.Lp[j + 1] > X.Lp[j]) rmax = std::max(rmax, X.Li[X.Lp[j + 1] - 1] + 1);
+        if (X.Up[j + 1] > X.Up[j]) rmin = std::min(rmin, X.Ui[X.Up[j]]);
+      }
+      total += 2.0 * s * s + (double)(rmax - cmax) * s + (double)(cmin - rmin) * s;
+    }
+    if (total > 4.0e9)
+      return fail(h, SMLU_ERR_ALLOC, "chunked layout needs " + std::to_string(8.0 * total / 1e9) +
+                                         " GB (dense chunks, as in the reference); use smlu_solve");
+  }
+  std::vector<ChunkDesc> desc;
+  std::vector<double> data;
+  // one chunk: columns [c0, c1), rectangle rows [r0, r1) (0-based)
+  auto add = [&](int64_t c0, int64_t c1, int64_t r0, int64_t r1, bool upper) {
+    ChunkDesc d;
+    d.c0 = c0;
+    d.s = c1 - c0;
+    d.r0 = r0;
+    d.nr = std::max<int64_t>(r1 - r0, 0);
+    d.tri = (int64_t)data.size();
+    data.resize(data.size() + d.s * d.s, 0.0);
+    d.rect = (int64_t)data.size();
+    data.resize(data.size() + d.nr * d.s, 0.0);
+    const auto& Cp = upper ? X.Up : X.Lp;
+    const auto& Ci = upper ? X.Ui : X.Li;
+    const auto& Cx = upper ? X.Ux : X.Lx;
+    for (int64_t j = c0; j < c1; ++j)
+      for (int64_t e = Cp[j]; e < Cp[j + 1]; ++e) {
+        const int64_t i = Ci[e];
+        const bool in_tri = upper ? i >= c0 : i < c1;
+        if (in_tri) data[d.tri + (j - c0) * d.s + (i - c0)] = Cx[e];
+        else if (i >= r0 && i < r1) data[d.rect + (j - c0) * d.nr + (i - r0)] = -Cx[e];   // :207, :238
+      }
+    desc.push_back(d);
+  };
+  for (int64_t c = 1; c <= T; ++c) {              // L chunks, :111-123
+    const int64_t cmin = (c - 1) * cs, cmax = std::min(m, c * cs);
+    int64_t rmax = cmax;                          // one past the max row of the chunk's columns
+    for (int64_t j = cmin; j < cmax; ++j)
+      if (X.Lp[j + 1] > X.Lp[j]) rmax = std::max(rmax, X.Li[X.Lp[j + 1] - 1] + 1);
+    add(cmin, cmax, cmax, rmax, false);
+  }
+  for (int64_t c = 1; c <= T; ++c) {              // U chunks from the back, :132-144 (Q2)
+    const int64_t cmin = (T - c) * cs, cmax = std::min(m, (T - c + 1) * cs);
+    int64_t rmin = cmin;                          // min row of the chunk's columns
+    for (int64_t j = cmin; j < cmax; ++j)
+      if (X.Up[j + 1] > X.Up[j]) rmin = std::min(rmin, X.Ui[X.Up[j]]);
+    add(cmin, cmax, rmin, cmin, true);
+  }
+  hipStream_t st = h->stream;
+  h->ch_data.free();
+  h->ch_desc.free();
+  h->ch_p.free();
+  h->ch_q.free();
+  HIPCHK(h->ch_data.upload(data.data(), data.size(), st));
+  HIPCHK(h->ch_desc.upload(desc.data(), desc.size(), st));
+  HIPCHK(h->ch_p.upload(X.p.data(), X.p.size(), st));
+  HIPCHK(h->ch_q.upload(X.q.data(), X.q.size(), st));
+  HIPCHK(hipStreamSynchronize(st));
+  h->ch_T = T;
+  h->ch_size = cs;
+  h->ch_version = h->nfactor;
+  return SMLU_OK;
+}
+
+// ldiv! (:286-342) through the chunked layout: wrk = (Rs.*b)[p]; lsolve!; rsolve!; x[q] = wrk.
+// Device pointers; x may alias b.  Refills the chunks when the factors changed since the setup
+// (the reference refills them in lu!, :265-276).
+int smlu_chunked_ldiv_device(smlu_handle* h, const double* d_b, double* d_x) {
+  if (!h || !d_b || !d_x) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
+  if (h->ch_version != h->nfactor) {
+    int rc = smlu_chunked_setup(h, h->ch_size);
+    if (rc != SMLU_OK) return rc;
+  }
+  HIPCHK(hipSetDevice(h->device));
+  hipStream_t st = h->stream;
+  const int64_t n = h->plan.n;
+  double* w = h->wrk.p;
+  HIPCHK(launch_perm_in(st, n, h->ch_p.p, h->Rs.p, d_b, w));
+  HIPCHK(launch_chunked_solve(st, false, h->ch_T, h->ch_desc.p, h->ch_data.p, w));
+  HIPCHK(launch_chunked_solve(st, true, h->ch_T, h->ch_desc.p + h->ch_T, h->ch_data.p, w));
+  HIPCHK(launch_perm_out(st, n, h->ch_q.p, w, d_x));
+  HIPCHK(hipStreamSynchronize(st));
+  return SMLU_OK;
+}
+
+int smlu_chunked_ldiv(smlu_handle* h, const double* b, double* x) {
+  if (!h || !b || !x) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
+  HIPCHK(hipSetDevice(h->device));
+  const int64_t n = h->plan.n;
+  HIPCHK(hipMemcpyAsync(h->wrk2.p, b, sizeof(double) * n, hipMemcpyHostToDevice, h->stream));
+  int rc = smlu_chunked_ldiv_device(h, h->wrk2.p, h->wrk2.p);
+  if (rc != SMLU_OK) return rc;
+  HIPCHK(hipMemcpyAsync(x, h->wrk2.p, sizeof(double) * n, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return SMLU_OK;
+}
+
 void smlu_destroy(smlu_handle* h) { delete h; }
 
 const char* smlu_last_error_string(const smlu_handle* h) {
@@ -1765,6 +1898,12 @@ static double plan_stat(const Plan& P, const std::string& k) {
   if (k == "factor_bytes") return 8.0 * (double)P.factor_size;
   if (k == "scratch_bytes") return 8.0 * (double)P.scratch_size;
   if (k == "analysis_ms") return P.analysis_ms;
+  if (k == "extadd_entries") {   // child F22 entries moved by the extend-add per factorization
+    double t = 0;
+    for (int64_t s = 0; s < P.nsup; ++s)
+      if (P.s_parent[s] >= 0) t += (double)P.nu(s) * (double)P.nu(s);
+    return t;
+  }
   return std::numeric_limits<double>::quiet_NaN();
 }
 

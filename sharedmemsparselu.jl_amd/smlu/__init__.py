@@ -3,11 +3,12 @@ SharedMemSparseLU.jl (ParallelSparseLU / lu! / ldiv!).  Host symbolic analysis +
 in libsmlu.so (C-ABI: include/smlu.h); this package is the Python mirror of the Julia API."""
 from ._lib import build, lib, default_opts, LIB_PATH  # noqa: F401
 from .api import (ParallelSparseLU, lu_, ldiv_, lsolve_, rsolve_,  # noqa: F401
-                  cleanup_ParallelSparseLU_, allocate_shared, DimensionMismatch,
+                  chunked_setup, chunked_ldiv_, cleanup_ParallelSparseLU_, allocate_shared, DimensionMismatch,
                   SingularException, SmluError)
 from .plan import Plan  # noqa: F401
 from .dist import DistributedSparseLU  # noqa: F401
 
-__all__ = ["ParallelSparseLU", "lu_", "ldiv_", "lsolve_", "rsolve_", "cleanup_ParallelSparseLU_",
+__all__ = ["ParallelSparseLU", "lu_", "ldiv_", "lsolve_", "rsolve_", "chunked_setup", "chunked_ldiv_",
+           "cleanup_ParallelSparseLU_",
            "allocate_shared", "DimensionMismatch", "SingularException", "SmluError", "Plan", "DistributedSparseLU", "build",
            "lib"]

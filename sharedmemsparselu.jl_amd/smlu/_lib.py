@@ -68,6 +68,9 @@ SIGNATURES = {
     "smlu_create_i32": (i32, [i64, vp, vp, vp, ctypes.POINTER(SmluOpts), ctypes.POINTER(vp)]),
     "smlu_lsolve": (i32, [vp, vp]),
     "smlu_rsolve": (i32, [vp, vp]),
+    "smlu_chunked_setup": (i32, [vp, i64]),
+    "smlu_chunked_ldiv": (i32, [vp, vp, vp]),
+    "smlu_chunked_ldiv_device": (i32, [vp, vp, vp]),
     "smlu_get_sizes": (i32, [vp, i64p, i64p, i64p]),
     "smlu_get_factors": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "smlu_destroy": (None, [vp]),

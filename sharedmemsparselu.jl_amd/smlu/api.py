@@ -269,6 +269,25 @@ def rsolve_(F: ParallelSparseLU, x):
     return _tri(F, x, "U")
 
 
+def chunked_setup(F: ParallelSparseLU, chunk_size=None):
+    """Build the reference's dense-chunk solve layout on the GPU from F's current factors
+    (get_chunking_parameters / allocate_chunks / fill_chunks!, src/SharedMemSparseLU.jl:101-243;
+    chunk_size defaults to 8 as :67-70).  SURVEY §8f-3 parity mode for small banded systems."""
+    _check(C.lib().smlu_chunked_setup(F._h, 0 if chunk_size is None else int(chunk_size)), F._h)
+
+
+def chunked_ldiv_(x, F: ParallelSparseLU, b):
+    """ldiv!(x, F, b) (:286-342) through the chunked layout: lsolve!/rsolve! (:349-392) chunk by
+    chunk on the GPU.  Same DimensionMismatch checks as ldiv_; x may be b."""
+    if len(x) != F.n or len(b) != F.n:
+        raise DimensionMismatch(f"x and b must have length F.n={F.n}: {len(x)}, {len(b)}")
+    bb = np.ascontiguousarray(b, dtype=np.float64)
+    xx = np.empty(F.n)
+    _check(C.lib().smlu_chunked_ldiv(F._h, C.ptr(bb), C.ptr(xx)), F._h)
+    x[:] = xx
+    return x
+
+
 def cleanup_ParallelSparseLU_(F: ParallelSparseLU):
     """cleanup_ParallelSparseLU!(F) — exported but undefined in the reference (:31); here it
     releases the device memory, stream and host plan of F."""

@@ -246,3 +246,48 @@ def test_int32_indices(gpu):
     F32 = smlu.ParallelSparseLU(A, int32_indices=True)
     assert np.array_equal(F64.p, F32.p) and np.array_equal(F64.q, F32.q)
     assert abs(F64.L - F32.L).max() == 0 and abs(F64.U - F32.U).max() == 0
+
+
+@pytest.mark.parametrize("nel,cs", [(1, None), (7, None), (57, None), (57, 3), (200, 16)])
+def test_chunked_layout_ldiv(gpu, nel, cs):
+    # the reference's dense-chunk layout on the GPU.  Same factors as ldiv_, so
+    # the solutions agree to rounding; against the oracle's verbatim CPU restatement of the
+    # chunked lsolve!/rsolve! on the exported factors at the reference's tolerance.
+    rng = np.random.default_rng(100 + nel)
+    A = O.test_matrix(rng, nel, 5)
+    n = A.shape[0]
+    F = smlu.ParallelSparseLU(A)
+    smlu.chunked_setup(F, cs)
+    b = rng.random(n)
+    x = np.empty(n)
+    smlu.chunked_ldiv_(x, F, b)
+    xr = np.empty(n)
+    smlu.ldiv_(xr, F, b)
+    assert isapprox(x, xr, TOL, TOL)
+    CS = O.ChunkedSolve(F.L, F.U, cs)
+    w = (F.Rs * b)[F.p]
+    CS.lsolve(w)
+    CS.rsolve(w)
+    xo = np.empty(n)
+    xo[F.q] = w
+    assert isapprox(x, xo, TOL, TOL)
+    assert isapprox(x, spla.spsolve(A, b), TOL, TOL)
+    # after lu! the chunks are refilled (src/SharedMemSparseLU.jl:265-276)
+    A2 = O.test_matrix(np.random.default_rng(7 + nel), nel, 5)
+    smlu.lu_(F, A2)
+    smlu.chunked_ldiv_(x, F, b)
+    assert isapprox(x, spla.spsolve(A2, b), TOL, TOL)
+
+
+def test_chunked_layout_dense_and_refusal(gpu):
+    rng = np.random.default_rng(9)
+    D = rng.random((64, 64))
+    A = sp.csc_matrix(D)
+    F = smlu.ParallelSparseLU(A)
+    smlu.chunked_setup(F)
+    b = rng.random(64)
+    x = b.copy()
+    smlu.chunked_ldiv_(x, F, x)   # x === b allowed
+    assert isapprox(x, np.linalg.solve(D, b), DENSE_TOL, DENSE_TOL)
+    with pytest.raises(smlu.DimensionMismatch):
+        smlu.chunked_ldiv_(np.empty(63), F, b)
