@@ -146,6 +146,79 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
   if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
 }
 
+// Small-k variant of k_gemm (every task of the launch has k <= 64: the in-block updates and the
+// GEMM-form triangular solves): the whole K extent of the A and B tiles is staged in one shot
+// (32 loads per thread in flight together with the 16 C loads), so a launch pays one memory
+// round trip instead of one per 16-deep slice.  Same per-element arithmetic as k_gemm.
+template <bool TRSM>
+__global__ __launch_bounds__(256) void k_gemm_k64(const GemmTask* __restrict__ tasks, int ntask, GrowthArgs ga) {
+  __shared__ double As[64][GBM + 2];   // [k][row]
+  __shared__ double Bs[64][GBN + 2];   // [k][col], negated
+  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+  const gdbl* gA = gbl(t.A);
+  const gdbl* gB = gbl(t.B);
+  gdbl* gC = gbl(t.C);
+  int tm, tn;
+  tile_rc<GBM>(t, b - t.tile0, tm, tn);
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int tid = threadIdx.x;
+  const int tx = tid & 15, ty = tid >> 4;
+  const int K = t.k;
+  double acc[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + ty + 16 * j;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + tx + 16 * i;
+      acc[i][j] = (col < t.n && row < t.m) ? gC[(int64_t)col * t.ldc + row] : 0.0;
+    }
+  }
+  // A: row = tid & 63, k = (tid >> 6) + 4r;  B: k = tid & 63, col = (tid >> 6) + 4r
+  const int ar = tid & 63, ak = tid >> 6;
+  double ra[16], rb[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int kk = ak + 4 * r, row = m0 + ar;
+    ra[r] = (row < t.m && kk < K) ? gA[(int64_t)kk * t.lda + row] : 0.0;
+    const int col = n0 + ak + 4 * r;
+    rb[r] = (col < t.n && ar < K) ? gB[(int64_t)col * t.ldb + ar] : 0.0;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    As[ak + 4 * r][ar] = ra[r];
+    Bs[ar][ak + 4 * r] = -rb[r];
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int kk = 0; kk < K; ++kk) {
+    double a[4], bb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = As[kk][tx + 16 * i];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bb[j] = Bs[kk][ty + 16 * j];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], bb[j], acc[i][j]);
+  }
+  double gmax = 0.0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int col = n0 + ty + 16 * j;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = m0 + tx + 16 * i;
+      if (col < t.n && row < t.m) {
+        gC[(int64_t)col * t.ldc + row] = acc[i][j];
+        gmax = fmax(gmax, fabs(acc[i][j]));
+      }
+    }
+  }
+  if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
+}
+
 // ------------------------------------------------------------------------------------
 // Dense update C -= A*B, large tiles: 128x128 output tile per 256-thread workgroup, 8x8
 // accumulators per thread (128 VGPRs), K staged through double-buffered LDS in slices of 16
@@ -463,6 +536,8 @@ hipError_t launch_gemm_g(hipStream_t st, int64_t ntiles, const GemmTask* tasks, 
   else if (tile == 128)   // VALU 128 tile (SMLU_VALU_GEMM only; never used for the TRSM form)
     k_gemm128<<<(unsigned)(maxwg > 0 ? std::min<int64_t>(ntiles, maxwg) : ntiles), 256, 0, st>>>(
         tasks, ntask, ntiles);
+  else if (tile == 65 && trsm) k_gemm_k64<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  else if (tile == 65) k_gemm_k64<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (trsm) k_gemm<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else k_gemm<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   return hipGetLastError();

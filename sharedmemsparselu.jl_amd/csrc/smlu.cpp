@@ -189,6 +189,7 @@ struct smlu_handle {
   bool lookahead = false;     // SMLU_LOOKAHEAD=1: trailing updates beyond the next block on a side stream
   int ob = kOBDefault;        // outer block width (SMLU_OB overrides; multiple of 64)
   int64_t t128_min = 512;     // 128x128 GEMM tiles when a launch has at least this many
+  bool small_k = true;        // k <= 64 launches use k_gemm_k64 (SMLU_SMALLK=0: off)
   bool trsm_gemm = true;      // GEMM-form triangular solves of the blocked fronts
   bool trsm_gemm64_only = false;   // SMLU_TRSM_GEMM=2: only for diagonal-tile (nb = 64) fronts
   int64_t side_wg = 0;        // grid cap of look-ahead GEMMs (SMLU_SIDE_WG; 0 = uncapped)
@@ -357,6 +358,7 @@ static int build_schedule(smlu_handle* h) {
   if (const char* e = std::getenv("SMLU_SIDE_WG")) h->side_wg = std::atoll(e);
   if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
   if (const char* e = std::getenv("SMLU_T128MIN")) h->t128_min = std::atoll(e);
+  h->small_k = !(std::getenv("SMLU_SMALLK") && std::atoi(std::getenv("SMLU_SMALLK")) == 0);
   // GEMM-form TRSM (k_tri_inv + GEMM tasks) needs the growth epilogue of the MFMA/64 tiles
   {
     const char* e = std::getenv("SMLU_TRSM_GEMM");
@@ -382,6 +384,11 @@ static int build_schedule(smlu_handle* h) {
     for (auto& g : cand) t128 += (int64_t)((g.m + 127) / 128) * ((g.n + 127) / 128);
     int tile = t128 >= h->t128_min ? 128 : 64;
     if (tile == 128 && h->opts.use_mfma) tile = 129;   // fp64 MFMA variant of the 128 tile
+    if (tile == 64 && h->small_k) {                    // every k <= 64: one-shot K staging
+      int kmax = 0;
+      for (auto& g : cand) kmax = std::max(kmax, g.k);
+      if (kmax <= 64) tile = 65;
+    }
     Launch L;
     L.kind = step < 0 ? K_GEMM22 : kind;
     L.side = side;
@@ -389,7 +396,7 @@ static int build_schedule(smlu_handle* h) {
     L.off = (int64_t)gt.size();
     L.aux = tile;
     int64_t tiles = 0;
-    const int ts = tile == 129 ? 128 : tile;
+    const int ts = tile >= 128 ? 128 : 64;
     for (size_t i = 0; i < cand.size(); ++i) {
       GemmTask& g = cand[i];
       if (count) h->gemm_bytes += 8.0 * ((double)g.m * g.k + (double)g.k * g.n + 2.0 * g.m * g.n);
@@ -406,7 +413,7 @@ static int build_schedule(smlu_handle* h) {
     if (!count) return;
     h->gemm_flops += fl;
     ++h->gemm_launches;
-    if (tile != 64) ++h->gemm128_launches;
+    if (tile >= 128) ++h->gemm128_launches;
     if (step < 0) h->gemm22_flops += fl;
   };
   // tinv operand encoding in tpatch: offset * 2 + (1 if the operand is B, 0 if A)
