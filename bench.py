@@ -193,6 +193,9 @@ def main():
                 pm = json.load(fh)
             traffic = pm.get("hbm_bytes_per_launch")
             traffic_src = os.path.relpath(pmc, ROOT)
+        hbm_refactor = None
+        if os.path.exists(pmc):
+            hbm_refactor = pm.get("refactor_all_kernels", {}).get("hbm_bytes")
         nnzA = A.nnz
         # SURVEY §8(d) algorithmic bytes of the scatter/gather formulation, for reference
         bytes_sg = 12 * upd + 12 * nnzA + 12 * nnzLU + 16 * (n + 1)
@@ -235,6 +238,10 @@ def main():
                            "f22_gflop": F.stat("gemm22_flops") / 1e9},
             "refactor_tflops": dense_flops / (ms_per_step * 1e-3) / 1e12,
             "scatter_gather_equiv_GBs": bytes_sg / (ms_per_step * 1e-3) / 1e9,
+            # measured HBM traffic of a whole refactor (PMC FETCH_SIZE x2 + WRITE_SIZE over every
+            # kernel, profiles/) over this run's time per refactor
+            "achieved_hbm_GBs": (hbm_refactor / (ms_per_step * 1e-3) / 1e9) if hbm_refactor else None,
+            "achieved_hbm_frac": (hbm_refactor / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS) if hbm_refactor else None,
             "solve_ms": solve_ms,
             "solve_residual": solve_residual,
             "create_s": t_create,

@@ -55,6 +55,23 @@ res = {
     "gemm_flops": flops,
     "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), KiB -> bytes; WRITE_SIZE as is",
 }
+# whole factorization (every kernel, incl. the memset fills): HBM bytes per refactor
+if os.path.exists(os.path.join(base, f"pmcall_FETCH_SIZE_{N}", "pmc_counter_collection.csv")):
+    def load_all(counter):
+        per = {}
+        path = os.path.join(base, f"pmcall_{counter}_{N}", "pmc_counter_collection.csv")
+        for r in csv.DictReader(open(path)):
+            name = r["Kernel_Name"].split("(")[0]
+            per[name] = per.get(name, 0.0) + float(r["Counter_Value"])
+        return per
+    fa, wa = load_all("FETCH_SIZE"), load_all("WRITE_SIZE")
+    tot = {k: 2.0 * fa.get(k, 0.0) * 1024 + wa.get(k, 0.0) * 1024 for k in set(fa) | set(wa)}
+    res["refactor_all_kernels"] = {
+        "hbm_bytes": sum(tot.values()),
+        "fetch_bytes": 2.0 * sum(fa.values()) * 1024, "write_bytes": sum(wa.values()) * 1024,
+        "by_kernel_top": dict(sorted(tot.items(), key=lambda kv: -kv[1])[:12]),
+        "note": "one eager factorization (first factorization incl. k_rowscale), every kernel",
+    }
 os.makedirs(out_dir, exist_ok=True)
 with open(os.path.join(out_dir, f"pmc_gemm_{N}.json"), "w") as fh:
     json.dump(res, fh, indent=1)

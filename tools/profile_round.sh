@@ -12,3 +12,8 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex "k_gemm" -d gpurun_out/pmc_${c}_$N -o pmc \
     --output-format csv -- python3 tools/pmc_factor.py $N > gpurun_out/pmc_${c}_$N.log 2>&1 || exit 1
 done
+# the same two counters over every kernel of the factorization: whole-refactor HBM bytes
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $c -d gpurun_out/pmcall_${c}_$N -o pmc \
+    --output-format csv -- python3 tools/pmc_factor.py $N > gpurun_out/pmcall_${c}_$N.log 2>&1 || exit 1
+done
