@@ -185,7 +185,7 @@ def main():
         dense_flops = F.stat("dense_flops")
         achieved = gemm_flops / (ms_gemm * 1e-3) / 1e12 if ms_gemm > 0 else None
         n_gemm = F.stat("gemm_launches")
-        avg_us = ms_gemm * 1e3 / n_gemm if n_gemm else None
+        avg_us = ms_gemm * 1e3 / n_gemm if (n_gemm and ms_gemm > 0) else None
         traffic, traffic_src = None, "not collected"
         pmc = os.path.join(ROOT, "profiles", "r01", f"pmc_gemm_{N}.json")
         if os.path.exists(pmc):
@@ -232,10 +232,12 @@ def main():
                                  "stream); traffic = HBM bytes per launch from rocprofv3 PMC "
                                  "(FETCH_SIZE x2 + WRITE_SIZE, " + traffic_src + ")"},
             "kernel_ms_per_step": {k: v / K for k, v in kind_ms.items()},
-            "gemm_split": {"panel_tflops": (gemm_flops - F.stat("gemm22_flops")) / max((kind_ms["gemm"] + kind_ms["gemmu"] + kind_ms["gemmo"]) / K, 1e-9) / 1e9,
-                           "f22_tflops": F.stat("gemm22_flops") / max(kind_ms["gemm22"] / K, 1e-9) / 1e9,
-                           "panel_gflop": (gemm_flops - F.stat("gemm22_flops")) / 1e9,
-                           "f22_gflop": F.stat("gemm22_flops") / 1e9},
+            # per-kind HIP-event times exist for the single-GPU path only (partitioned: None)
+            "gemm_split": ({"panel_tflops": (gemm_flops - F.stat("gemm22_flops")) / ((kind_ms["gemm"] + kind_ms["gemmu"] + kind_ms["gemmo"]) / K) / 1e9,
+                            "f22_tflops": F.stat("gemm22_flops") / (kind_ms["gemm22"] / K) / 1e9,
+                            "panel_gflop": (gemm_flops - F.stat("gemm22_flops")) / 1e9,
+                            "f22_gflop": F.stat("gemm22_flops") / 1e9}
+                           if ms_gemm > 0 and kind_ms["gemm22"] > 0 else None),
             "refactor_tflops": dense_flops / (ms_per_step * 1e-3) / 1e12,
             "scatter_gather_equiv_GBs": bytes_sg / (ms_per_step * 1e-3) / 1e9,
             # measured HBM traffic of a whole refactor (PMC FETCH_SIZE x2 + WRITE_SIZE over every
