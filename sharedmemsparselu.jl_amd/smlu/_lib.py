@@ -11,7 +11,7 @@ import os
 import subprocess
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # sharedmemsparselu.jl_amd/
-LIB_PATH = os.path.join(_PKG, "libsmlu.so")
+LIB_PATH = os.environ.get("SMLU_LIB") or os.path.join(_PKG, "libsmlu.so")   # SMLU_LIB: dev variants
 
 i64 = ctypes.c_int64
 i32 = ctypes.c_int32
