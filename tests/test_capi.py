@@ -81,6 +81,9 @@ def test_null_handle_calls_are_safe():
     L = smlu.lib()
     assert L.smlu_refactor(None, None) == C.SMLU_ERR_ARG
     assert L.smlu_solve(None, None, None) == C.SMLU_ERR_ARG
+    assert L.smlu_chunked_setup(None, 8) == C.SMLU_ERR_ARG
+    assert L.smlu_chunked_ldiv(None, None, None) == C.SMLU_ERR_ARG
+    assert L.smlu_chunked_ldiv_device(None, None, None) == C.SMLU_ERR_ARG
     assert L.smlu_last_error_col(None) == -1
     L.smlu_destroy(None)
     assert np.isnan(L.smlu_stat(None, b"n"))
