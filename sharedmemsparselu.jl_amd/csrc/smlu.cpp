@@ -190,6 +190,7 @@ struct smlu_handle {
   int ob = kOBDefault;        // outer block width (SMLU_OB overrides; multiple of 64)
   int64_t t128_min = 512;     // 128x128 GEMM tiles when a launch has at least this many
   bool small_k = true;        // k <= 64 launches use k_gemm_k64 (SMLU_SMALLK=0: off)
+  bool dominant = false;      // A diagonally dominant (by rows or columns) at analysis time
   bool trsm_gemm = true;      // GEMM-form triangular solves of the blocked fronts
   bool trsm_gemm64_only = false;   // SMLU_TRSM_GEMM=2: only for diagonal-tile (nb = 64) fronts
   int64_t side_wg = 0;        // grid cap of look-ahead GEMMs (SMLU_SIDE_WG; 0 = uncapped)
@@ -307,6 +308,13 @@ static int build_schedule(smlu_handle* h) {
   // supernode records
   h->hsn.resize(nsup);
   int64_t voff = 0;
+  // Largest ns factored with full-candidate pivoting.  A diagonally dominant matrix needs no
+  // row exchanges (partial pivoting keeps the diagonal and the Schur complements stay
+  // dominant), so there the mid-size fronts take the faster diagonal-tile path too; its growth
+  // check still flags weak pivots if a refactor's new values lose dominance (refinement then
+  // runs in the solves).  SMLU_FULLPIV_NS overrides (dev).
+  const int64_t full_piv_ns = std::getenv("SMLU_FULLPIV_NS") ? std::atoll(std::getenv("SMLU_FULLPIV_NS"))
+                              : h->dominant ? (int64_t)kSmallM : (int64_t)kFullPivNs;
   for (int64_t s = 0; s < nsup; ++s) {
     SNode r{};
     r.first = P.s_first[s];
@@ -321,7 +329,7 @@ static int build_schedule(smlu_handle* h) {
     r.parent = (int32_t)P.s_parent[s];
     int64_t M = P.M(s);
     if (M <= kSmallM) { r.mode = 0; r.nb = 0; }
-    else if (r.ns <= kFullPivNs) { r.mode = 1; r.nb = kNbFull; }
+    else if (r.ns <= full_piv_ns) { r.mode = 1; r.nb = kNbFull; }
     else { r.mode = 2; r.nb = kNbTile; }
     if (h->opts.pivot_tol <= 0) { /* no pivoting requested: tile mode never searches far */ }
     r.chbeg = (int32_t)P.ch_ptr[s];
@@ -1344,6 +1352,27 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode)
 
 static bool valid_opts(const smlu_opts* o) { return o && (o->index_base == 0 || o->index_base == 1); }
 
+// Diagonal dominance of A by columns or by rows (|a_jj| >= sum of the other |a_ij|, a_jj != 0).
+static bool diagonally_dominant(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* a,
+                                int64_t base) {
+  std::vector<double> rdiag(n, 0.0), roff(n, 0.0);
+  bool col_dom = true;
+  for (int64_t j = 0; j < n; ++j) {
+    double d = 0.0, off = 0.0;
+    for (int64_t e = colptr[j] - base; e < colptr[j + 1] - base; ++e) {
+      const int64_t i = rowval[e] - base;
+      const double v = std::fabs(a[e]);
+      if (i == j) { d += v; rdiag[i] += v; }
+      else { off += v; roff[i] += v; }
+    }
+    if (!(d > 0.0 && d >= off)) col_dom = false;
+  }
+  if (col_dom) return true;
+  for (int64_t i = 0; i < n; ++i)
+    if (!(rdiag[i] > 0.0 && rdiag[i] >= roff[i])) return false;
+  return true;
+}
+
 static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
                        const int64_t* p, const int64_t* q, const double* Rs, const smlu_opts* opts,
                        smlu_handle** out, int rank = 0, int nranks = 1) {
@@ -1368,6 +1397,7 @@ static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, 
   if (!e.empty()) return fail(nullptr, SMLU_ERR_ARG, e);
   h->rank = rank;
   h->nranks = nranks;
+  if (!p) h->dominant = diagonally_dominant(n, colptr, rowval, nzval, h->opts.index_base);
   if (nranks > 1) {
     h->plan.compute_owners(nranks);
     h->opts.profile = 0;   // per-kind event timing is single-GPU only
@@ -1475,6 +1505,7 @@ int smlu_refactor_csc(smlu_handle* h, int64_t n, const int64_t* colptr, const in
     return fail(h, SMLU_ERR_ALLOC, "host allocation failed during analysis");
   }
   if (!e.empty()) return fail(h, SMLU_ERR_ARG, e);
+  h->dominant = diagonally_dominant(n, colptr, rowval, nzval, base);
   int rc = setup_device(h);
   if (rc != SMLU_OK) return rc;
   HIPCHK(hipMemcpyAsync(h->A.p, nzval, sizeof(double) * h->plan.nnzA, hipMemcpyHostToDevice, h->stream));
@@ -1922,6 +1953,7 @@ double smlu_stat(const smlu_handle* h, const char* key) {
   if (k == "solve_ms_last") return h->solve_ms;
   if (k == "growth_max") return h->growth_max;
   if (k == "weak") return (double)h->weak;
+  if (k == "dominant") return h->dominant ? 1.0 : 0.0;
   if (k == "refine_steps") return (double)h->refine_steps;
   if (k == "refine_residual") return h->refine_resid;
   if (k == "gemm_flops") return h->gemm_flops;

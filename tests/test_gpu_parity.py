@@ -291,3 +291,21 @@ def test_chunked_layout_dense_and_refusal(gpu):
     assert isapprox(x, np.linalg.solve(D, b), DENSE_TOL, DENSE_TOL)
     with pytest.raises(smlu.DimensionMismatch):
         smlu.chunked_ldiv_(np.empty(63), F, b)
+
+
+def test_dominance_selects_tile_pivoting(gpu):
+    # diagonally dominant input: mid-size fronts take the diagonal-tile path (no row exchanges
+    # are needed); a random dense matrix keeps full-candidate pivoting.  Both solve correctly.
+    A = mats.poisson3d(12)
+    F = smlu.ParallelSparseLU(A)
+    assert F.stat("dominant") == 1.0
+    b = np.random.default_rng(3).random(A.shape[0])
+    x = np.empty_like(b)
+    smlu.ldiv_(x, F, b)
+    assert isapprox(x, spla.spsolve(A, b), TOL, TOL)
+    D = np.random.default_rng(4).random((200, 200))
+    G = smlu.ParallelSparseLU(sp.csc_matrix(D))
+    assert G.stat("dominant") == 0.0
+    y = np.empty(200)
+    smlu.ldiv_(y, G, b[:200])
+    assert isapprox(y, np.linalg.solve(D, b[:200]), DENSE_TOL, DENSE_TOL)
