@@ -6,8 +6,9 @@ Poisson matrix (default 128^3, BASELINE config C3/C5), values already resident i
 Prints ONE JSON line (rank 0).  Launch: ``python bench.py`` (1 GPU) or, for N GPUs,
 ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``.
 
-Multi-GPU in this round: independent replicas (each rank refactors its own copy; no
-data-path collective) — see DESIGN.md §Multi-GPU for the subtree partition that replaces it.
+Multi-GPU (N > 1): ONE factorization split over the ranks — subtrees of the assembly tree per
+rank, update blocks moved at exchange points over RCCL point-to-point ("scaling": "strong";
+`--replicas` runs independent copies instead).  DESIGN.md §7.
 """
 from __future__ import annotations
 
