@@ -975,13 +975,14 @@ hipError_t launch_panel1(hipStream_t st, int cnt, int lds_doubles, int rmax, int
 #define PANEL1_ARGS list, step, sn, store, scratch, rowperm, swaps, swap_stride, info, growth, diag_tol
   (void)lds;
   static const bool lds_panel = std::getenv("SMLU_LDS_PANEL") != nullptr;
-  // 64-wide panels: column-split kernel (8 waves by default, SMLU_PANEL_COLS=4 for 4);
-  // SMLU_PANEL_COLS=1 selects the single-wave kernel
+  // 64-wide panels: column-split kernel (16 waves by default -- 16/8/4 waves: 27/30/35 ms per
+  // 128^3 refactor; SMLU_PANEL_COLS=8 or 4 selects those); SMLU_PANEL_COLS=1: single-wave kernel
   static const int cols_waves = [] {
     const char* e = std::getenv("SMLU_PANEL_COLS");
-    return e ? std::atoi(e) : 8;
+    return e ? std::atoi(e) : 16;
   }();
-  if (wmax > 32 && !lds_panel && cols_waves == 8) k_panel_cols<8><<<cnt, 512, 0, st>>>(PANEL1_ARGS);
+  if (wmax > 32 && !lds_panel && cols_waves == 16) k_panel_cols<16><<<cnt, 1024, 0, st>>>(PANEL1_ARGS);
+  else if (wmax > 32 && !lds_panel && cols_waves == 8) k_panel_cols<8><<<cnt, 512, 0, st>>>(PANEL1_ARGS);
   else if (wmax > 32 && !lds_panel && cols_waves == 4) k_panel_cols<4><<<cnt, 256, 0, st>>>(PANEL1_ARGS);
   else if (wmax > 32 && !lds_panel) k_panel_wave<64><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
   else if (wmax > 32) k_panel_reg<64, 1><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
