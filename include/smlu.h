@@ -105,6 +105,11 @@ int smlu_solve(smlu_handle* h, const double* b, double* x);
 /* Same with device pointers (x == b allowed). */
 int smlu_solve_device(smlu_handle* h, const double* d_b, double* d_x);
 
+/* r = b - A x with the handle's current A values (device pointers, length n; r may not alias
+ * x or b) and its max-norm in *nrm (may be NULL).  The residual step of iterative refinement,
+ * exported for callers that drive the partitioned solve (smlu_dist_*). */
+int smlu_residual_device(smlu_handle* h, const double* d_x, const double* d_b, double* d_r, double* nrm);
+
 /* ldiv! with nrhs right-hand sides: column j of B (ldb >= n) -> column j of X (ldx >= n),
  * host memory, X == B allowed.  The reference's ldiv! is generic over the vector type
  * (src/SharedMemSparseLU.jl:286); multiple RHS are SURVEY §8f-4. */

@@ -689,6 +689,136 @@ __device__ __forceinline__ int find_swap_task(const SwapTask* __restrict__ t, in
   return lo;
 }
 
+// ------------------------------------------------------------------------------------
+// Full-candidate panel for tall candidate sets (mode 1, R > 512 rows: the re-pivoting
+// refactor puts every blocked front in mode 1).  One 1024-thread workgroup per front works on
+// the panel in place in HBM/L2 (the candidates do not fit in registers): per column the same
+// diagonal-preference test and argmax (ties to the lowest position) as k_panel_reg, a
+// physical swap of the two rows across the w panel columns, then scaling and the rank-1
+// update of the remaining panel columns by rows.  The transpositions are turned into the
+// (final position, original offset) swap list and the rowperm update the other kernels use.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_panel_tall(const int32_t* __restrict__ list, int step,
+                                                     const SNode* __restrict__ sn,
+                                                     double* __restrict__ store,
+                                                     double* __restrict__ scratch,
+                                                     int32_t* __restrict__ rowperm,
+                                                     int32_t* __restrict__ swaps,
+                                                     int64_t swap_stride,
+                                                     int32_t* __restrict__ info,
+                                                     double* __restrict__ growth, double diag_tol) {
+  constexpr int NT = 1024, NWV = NT / 64;
+  __shared__ double s_val[NWV];
+  __shared__ int s_idx[NWV];
+  __shared__ int s_any[NWV];
+  __shared__ int s_tp[64];          // transposition partner of each panel column
+  __shared__ int s_key[128], s_org[128];
+  __shared__ int32_t s_rp[128];
+  const int sid = list[2 * blockIdx.x];
+  const SNode s = sn[sid];
+  FrontPtrs f = front_ptrs(s, store, scratch);
+  const int64_t M = f.M;
+  const int ns = (int)f.ns;
+  const int kb = step * s.nb;
+  const int w = min(s.nb, ns - kb);
+  const int R = (s.mode == 1) ? ns - kb : w;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  gdbl* P = f.L + (int64_t)kb * M + kb;
+  int flag = 0, err = -1;
+  double lmax = 0.0;
+  for (int k = 0; k < w; ++k) {
+    gdbl* col = P + (int64_t)k * M;
+    const double akk = col[k];
+    bool beats = false;
+    for (int r = k + 1 + tid; r < R; r += NT) beats |= fabs(col[r]) * diag_tol > fabs(akk);
+    const bool any_w = __ballot(beats) != 0ull;
+    if (lane == 0) s_any[wv] = any_w ? 1 : 0;
+    __syncthreads();
+    bool any = false;
+    for (int v = 0; v < NWV; ++v) any |= s_any[v] != 0;
+    int p = k;
+    if (any || akk == 0.0) {
+      double am = -1.0;
+      int ai = 0x7fffffff;
+      for (int r = k + tid; r < R; r += NT) {
+        const double v = fabs(col[r]);
+        if (v > am) { am = v; ai = r; }   // rows visited in increasing order: ties keep the lowest
+      }
+      am = wave_max_idx(am, ai);
+      if (lane == 0) { s_val[wv] = am; s_idx[wv] = ai; }
+      __syncthreads();
+      am = s_val[0];
+      ai = s_idx[0];
+      for (int v = 1; v < NWV; ++v)
+        if (s_val[v] > am || (s_val[v] == am && s_idx[v] < ai)) { am = s_val[v]; ai = s_idx[v]; }
+      if (am <= 0.0) {
+        flag |= 1;
+        if (err < 0) err = kb + k;
+      } else {
+        p = ai;
+      }
+    }
+    if (tid == 0) s_tp[k] = p;
+    if (p != k) {   // physical interchange of rows k and p across the panel columns
+      for (int j = tid; j < w; j += NT) {
+        const double a = P[(int64_t)j * M + k];
+        P[(int64_t)j * M + k] = P[(int64_t)j * M + p];
+        P[(int64_t)j * M + p] = a;
+      }
+    }
+    __syncthreads();
+    const double pinv = recip(col[k]);
+    for (int r = k + 1 + tid; r < R; r += NT) {
+      const double l = col[r] * pinv;
+      col[r] = l;
+      lmax = fmax(lmax, fabs(l));
+      if (l != 0.0)
+        for (int j = k + 1; j < w; ++j) P[(int64_t)j * M + r] = fma(-l, P[(int64_t)j * M + k], P[(int64_t)j * M + r]);
+    }
+    __syncthreads();
+  }
+  // net permutation of the touched positions: position -> original offset
+  if (tid == 0) {
+    int nk = 0;
+    auto slot = [&](int x) {
+      for (int i = 0; i < nk; ++i)
+        if (s_key[i] == x) return i;
+      s_key[nk] = x;
+      s_org[nk] = x;
+      return nk++;
+    };
+    for (int k = 0; k < w; ++k) {
+      const int p = s_tp[k];
+      if (p == k) continue;
+      const int a = slot(k), b = slot(p);
+      const int t = s_org[a];
+      s_org[a] = s_org[b];
+      s_org[b] = t;
+    }
+    int32_t* rp = rowperm + s.first + kb;
+    for (int i = 0; i < nk; ++i) s_rp[i] = rp[s_org[i]];
+    int32_t* sw = swaps + (int64_t)list[2 * blockIdx.x + 1] * swap_stride;
+    int m = 0;
+    for (int i = 0; i < nk; ++i) {
+      if (s_key[i] == s_org[i]) continue;
+      rp[s_key[i]] = s_rp[i];
+      sw[1 + 2 * m] = s_key[i];
+      sw[2 + 2 * m] = s_org[i];
+      ++m;
+    }
+    sw[0] = m;
+  }
+  lmax = wave_max(lmax);
+  if (lane == 0) s_val[wv] = lmax;
+  __syncthreads();
+  if (tid == 0) {
+    double g = 0.0;
+    for (int v = 0; v < NWV; ++v) g = fmax(g, s_val[v]);
+    if (g > 0.0) atomic_max_pos(&growth[0], g);
+    if (flag) publish_info(info + sid, flag, err);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_laswp(const SwapTask* __restrict__ tasks, int ntask,
                                                const SNode* __restrict__ sn,
                                                double* __restrict__ store,
@@ -990,7 +1120,8 @@ hipError_t launch_panel1(hipStream_t st, int cnt, int lds_doubles, int rmax, int
   else if (rmax <= 64) k_panel_reg<32, 1><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
   else if (rmax <= 128) k_panel_reg<32, 2><<<cnt, 128, 0, st>>>(PANEL1_ARGS);
   else if (rmax <= 256) k_panel_reg<32, 4><<<cnt, 256, 0, st>>>(PANEL1_ARGS);
-  else k_panel_reg<32, 8><<<cnt, 512, 0, st>>>(PANEL1_ARGS);
+  else if (rmax <= 512) k_panel_reg<32, 8><<<cnt, 512, 0, st>>>(PANEL1_ARGS);
+  else k_panel_tall<<<cnt, 1024, 0, st>>>(PANEL1_ARGS);   // full-candidate panels of the re-pivoting refactor
 #undef PANEL1_ARGS
   return hipGetLastError();
 }

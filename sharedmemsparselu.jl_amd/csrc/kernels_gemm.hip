@@ -339,8 +339,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__
 }
 
 // ------------------------------------------------------------------------------------
-// Optional fp64 MFMA variant of the same 128x128 tile (opts.use_mfma; default off: the north
-// star asks for no MFMA).  v_mfma_f64_16x16x4_f64; each wave owns a 64x64 quadrant = 4x4
+// fp64 MFMA variant of the same 128x128 tile (opts.use_mfma = 1, the default; opts.use_mfma = 0
+// or SMLU_VALU_GEMM selects the VALU tiles).  v_mfma_f64_16x16x4_f64; each wave owns a 64x64 quadrant = 4x4
 // blocks.  The product is formed as C^T = B^T A^T so that the accumulator's lane index runs
 // along C's rows (column-major C stays coalesced): lane l of block (bi,bj) holds
 // C[row = 16 bi + (l & 15)][col = 16 bj + (l >> 4) + 4 r], r = 0..3.

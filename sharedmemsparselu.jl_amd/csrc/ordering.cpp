@@ -245,4 +245,76 @@ std::vector<int64_t> order_graph_nd(const Graph& g, int64_t leaf) {
   return st.out;
 }
 
+// Zero-free diagonal by a maximum transversal (Duff's augmenting-path algorithm, with the
+// cheap assignment first).  The fronts pivot only among their fully-summed rows (no delayed
+// pivots), so a structurally zero diagonal -- KKT / saddle-point blocks -- would give a zero
+// pivot in a nonsingular matrix; UMFPACK's unrestricted column pivoting does not need this.
+// Diagonal preference: a column keeps its diagonal when |a_jj| >= 0.1 max_i |a_ij|; the other
+// columns take the largest free entry, then augmenting paths (explicit zeros never match).
+// Returns match[c] = row (0-based), or an empty vector when A is structurally singular.
+std::vector<int64_t> zero_free_diagonal(int64_t n, const int64_t* colptr, const int32_t* rowval,
+                                        const double* a) {
+  std::vector<int64_t> cm(n, -1), rm(n, -1);
+  for (int64_t c = 0; c < n; ++c) {
+    double mx = 0.0, d = 0.0;
+    for (int64_t e = colptr[c]; e < colptr[c + 1]; ++e) {
+      mx = std::max(mx, std::fabs(a[e]));
+      if (rowval[e] == c) d = std::fabs(a[e]);
+    }
+    if (d > 0.0 && d >= 0.1 * mx && rm[c] < 0) { cm[c] = c; rm[c] = c; }
+  }
+  for (int64_t c = 0; c < n; ++c) {   // cheap assignment: the largest free entry
+    if (cm[c] >= 0) continue;
+    int64_t best = -1;
+    double bv = 0.0;
+    for (int64_t e = colptr[c]; e < colptr[c + 1]; ++e) {
+      const double v = std::fabs(a[e]);
+      if (v > bv && rm[rowval[e]] < 0) { bv = v; best = rowval[e]; }
+    }
+    if (best >= 0) { cm[c] = best; rm[best] = c; }
+  }
+  // augmenting paths (iterative DFS over columns; a row is visited once per search)
+  std::vector<int64_t> visited(n, -1), stack_c, stack_e;
+  for (int64_t c0 = 0; c0 < n; ++c0) {
+    if (cm[c0] >= 0) continue;
+    stack_c.assign(1, c0);
+    stack_e.assign(1, colptr[c0]);
+    int64_t found = -1;
+    while (!stack_c.empty() && found < 0) {
+      const int64_t c = stack_c.back();
+      int64_t e = stack_e.back();
+      int64_t next = -1;
+      for (; e < colptr[c + 1]; ++e) {
+        const int64_t r = rowval[e];
+        if (a[e] == 0.0 || visited[r] == c0) continue;
+        visited[r] = c0;
+        if (rm[r] < 0) { found = r; break; }
+        next = rm[r];
+        ++e;
+        break;
+      }
+      stack_e.back() = e;
+      if (found >= 0) break;
+      if (next >= 0) {
+        stack_c.push_back(next);
+        stack_e.push_back(colptr[next]);
+        continue;
+      }
+      stack_c.pop_back();
+      stack_e.pop_back();
+    }
+    if (found < 0) return {};
+    // flip the path: each column on the stack takes the row its edge pointer passed last
+    int64_t r = found;
+    for (size_t k = stack_c.size(); k-- > 0;) {
+      const int64_t c = stack_c[k];
+      const int64_t prev = cm[c];
+      cm[c] = r;
+      rm[r] = c;
+      r = prev;
+    }
+  }
+  return cm;
+}
+
 }  // namespace smlu

@@ -83,7 +83,8 @@ std::vector<int64_t> postorder(const std::vector<int64_t>& parent) {
 }  // namespace
 
 std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval, int base,
-                        const PlanOptions& opt, const int64_t* pgiven, const int64_t* qgiven) {
+                        const PlanOptions& opt, const int64_t* pgiven, const int64_t* qgiven,
+                        const int64_t* rowmatch) {
   auto t0 = std::chrono::steady_clock::now();
   n = n_;
   if (n <= 0) return "n must be positive";
@@ -107,7 +108,37 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
       Arow[e] = (int32_t)r;
     }
   }
+  {   // is the pattern of A symmetric?  (the supernodal structure below is that of A+A')
+    std::vector<int64_t> cnt(n + 1, 0);
+    for (int64_t e = 0; e < nnzA; ++e) ++cnt[Arow[e] + 1];
+    for (int64_t i = 0; i < n; ++i) cnt[i + 1] += cnt[i];
+    sym_pattern = true;
+    std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
+    std::vector<int32_t> tr(nnzA);
+    for (int64_t j = 0; j < n; ++j)
+      for (int64_t e = Acolptr[j]; e < Acolptr[j + 1]; ++e) tr[pos[Arow[e]]++] = (int32_t)j;
+    for (int64_t j = 0; j <= n && sym_pattern; ++j) sym_pattern = cnt[j] == Acolptr[j];
+    for (int64_t e = 0; e < nnzA && sym_pattern; ++e) sym_pattern = tr[e] == Arow[e];
+  }
   Graph g = build_sym_graph(n, Acolptr.data(), Arow.data());
+  // Row pre-permutation from a transversal (match[c] = row of A placed at column c's
+  // diagonal): the fronts are built on pattern(B + B') with B = A[match, :], labelled by columns.
+  matched = rowmatch != nullptr && pgiven == nullptr;
+  if (matched) {
+    std::vector<int64_t> minv(n, -1);
+    for (int64_t c = 0; c < n; ++c) {
+      if (rowmatch[c] < 0 || rowmatch[c] >= n || minv[rowmatch[c]] >= 0) return "row match is not a permutation";
+      minv[rowmatch[c]] = c;
+    }
+    std::vector<int64_t> bptr(n + 1, 0);
+    std::vector<int32_t> brow(nnzA);
+    for (int64_t c = 0; c < n; ++c) {
+      for (int64_t e = Acolptr[c]; e < Acolptr[c + 1]; ++e) brow[e] = (int32_t)minv[Arow[e]];
+      std::sort(brow.begin() + Acolptr[c], brow.begin() + Acolptr[c + 1]);
+      bptr[c + 1] = Acolptr[c + 1];
+    }
+    g = build_sym_graph(n, bptr.data(), brow.data());
+  }
 
   // ---- ordering ----
   given_order = (pgiven != nullptr && qgiven != nullptr);
@@ -179,6 +210,8 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
     parent = etree_sym(g, q, qinv);
   }
   if (!given_order) p0 = q;
+  if (matched)
+    for (int64_t k = 0; k < n; ++k) p0[k] = rowmatch[q[k]];
   p0inv.assign(n, 0);
   for (int64_t k = 0; k < n; ++k) p0inv[p0[k]] = k;
 

@@ -34,17 +34,21 @@ Graph build_sym_graph(int64_t n, const int64_t* colptr, const int32_t* rowval);
 // Orderings return perm (new -> old).
 std::vector<int64_t> order_geometric_nd(int64_t nx, int64_t ny, int64_t nz, int64_t leaf);
 std::vector<int64_t> order_graph_nd(const Graph& g, int64_t leaf);
+std::vector<int64_t> zero_free_diagonal(int64_t n, const int64_t* colptr, const int32_t* rowval,
+                                        const double* a);
 
 struct Plan {
   // ---- input pattern (0-based copy) ----
   int64_t n = 0, nnzA = 0;
   std::vector<int64_t> Acolptr;
   std::vector<int32_t> Arow;
+  bool sym_pattern = false;       // pattern(A) == pattern(A'): the plan's structure is exact
 
   // ---- orderings: new -> old and inverses ----
   std::vector<int64_t> q, qinv;   // columns
   std::vector<int64_t> p0, p0inv; // rows (== q unless given)
   bool given_order = false;
+  bool matched = false;           // rows pre-permuted by a zero-free-diagonal transversal
 
   // ---- exact (pre-relaxation) supernodes: structure of L column j in t=col2t[j] is
   //      {j..last(t)} U R_t  (R_t sorted, all > last(t)) ----
@@ -111,7 +115,7 @@ struct Plan {
 
   std::string build(int64_t n, const int64_t* colptr, const int64_t* rowval, int index_base,
                     const PlanOptions& opt, const int64_t* pgiven = nullptr,
-                    const int64_t* qgiven = nullptr);
+                    const int64_t* qgiven = nullptr, const int64_t* rowmatch = nullptr);
 
   int64_t ns(int64_t s) const { return s_first[s + 1] - s_first[s]; }
   int64_t nu(int64_t s) const { return s_rowptr[s + 1] - s_rowptr[s]; }

@@ -190,7 +190,11 @@ struct smlu_handle {
   int ob = kOBDefault;        // outer block width (SMLU_OB overrides; multiple of 64)
   int64_t t128_min = 512;     // 128x128 GEMM tiles when a launch has at least this many
   bool small_k = true;        // k <= 64 launches use k_gemm_k64 (SMLU_SMALLK=0: off)
-  bool dominant = false;      // A diagonally dominant (by rows or columns) at analysis time
+  bool dominant = false;      // A diagonally dominant (by rows or columns): last host values seen
+  int pivmode = 0;            // 0: diagonal-tile pivoting for large (and, if dominant, mid-size)
+                              //    fronts; 1: full-candidate pivoting in every blocked front (the
+                              //    re-pivoting refactor after a zero or weak tile pivot)
+  int64_t repivots = 0;       // re-pivoting refactors run so far
   bool trsm_gemm = true;      // GEMM-form triangular solves of the blocked fronts
   bool trsm_gemm64_only = false;   // SMLU_TRSM_GEMM=2: only for diagonal-tile (nb = 64) fronts
   int64_t side_wg = 0;        // grid cap of look-ahead GEMMs (SMLU_SIDE_WG; 0 = uncapped)
@@ -313,7 +317,8 @@ static int build_schedule(smlu_handle* h) {
   // dominant), so there the mid-size fronts take the faster diagonal-tile path too; its growth
   // check still flags weak pivots if a refactor's new values lose dominance (refinement then
   // runs in the solves).  SMLU_FULLPIV_NS overrides (dev).
-  const int64_t full_piv_ns = std::getenv("SMLU_FULLPIV_NS") ? std::atoll(std::getenv("SMLU_FULLPIV_NS"))
+  const int64_t full_piv_ns = h->pivmode == 1 ? std::numeric_limits<int64_t>::max()
+                              : std::getenv("SMLU_FULLPIV_NS") ? std::atoll(std::getenv("SMLU_FULLPIV_NS"))
                               : h->dominant ? (int64_t)kSmallM : (int64_t)kFullPivNs;
   for (int64_t s = 0; s < nsup; ++s) {
     SNode r{};
@@ -538,12 +543,12 @@ static int build_schedule(smlu_handle* h) {
         int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
         int64_t R = r.mode == 1 ? r.ns - kb : w;
         if (r.nb > 32) return 0;
-        return R <= 64 ? 1 : R <= 128 ? 2 : R <= 256 ? 3 : 4;
+        return R <= 64 ? 1 : R <= 128 ? 2 : R <= 256 ? 3 : R <= 512 ? 4 : 5;
       };
       std::stable_sort(act.begin(), act.end(), [&](int64_t a, int64_t b) { return pclass(a) < pclass(b); });
       {
         size_t pos = 0;
-        for (int c = 0; c < 5 && pos < act.size(); ++c) {
+        for (int c = 0; c < 6 && pos < act.size(); ++c) {
           L = Launch();
           L.kind = K_PANEL;
           L.step = (int)t;
@@ -561,7 +566,8 @@ static int build_schedule(smlu_handle* h) {
           }
           L.cnt = cnt;
           L.aux = 0;
-          L.nwg = rmax | (wmax << 16);
+          L.nwg = rmax;
+          L.aux2 = wmax;
           if (L.cnt > 0) h->fac.push_back(L);
         }
         if (pos != act.size()) return fail(h, SMLU_ERR_ARG, "internal: panel classes");
@@ -1155,7 +1161,7 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
       return launch_laswp(st, L.nwg, h->stasks.p + L.off, (int)L.cnt, h->sn.p, h->store.p, h->scratch.p,
                           h->swaps.p, kSwapStride);
     case K_PANEL:
-      return launch_panel1(st, (int)L.cnt, (int)L.aux, (int)(L.nwg & 0xffff), (int)(L.nwg >> 16), L.step,
+      return launch_panel1(st, (int)L.cnt, (int)L.aux, (int)L.nwg, (int)L.aux2, L.step,
                            h->ilist.p + L.off, h->sn.p,
                           h->store.p, h->scratch.p, h->rowperm.p, h->swaps.p, kSwapStride, h->info.p,
                           h->growth.p, diag_tol);
@@ -1287,7 +1293,7 @@ static int finish_factor(smlu_handle* h, Timer& tm, std::chrono::steady_clock::t
   return rc;
 }
 
-static int run_factor(smlu_handle* h) {
+static int run_factor_once(smlu_handle* h) {
   HIPCHK(hipSetDevice(h->device));
   if (h->nranks > 1) return fail(h, SMLU_ERR_STATE, "partitioned handle: use smlu_dist_factor_segment");
   auto t0 = std::chrono::steady_clock::now();
@@ -1298,6 +1304,56 @@ static int run_factor(smlu_handle* h) {
     if (rc != SMLU_OK) return rc;
   }
   return finish_factor(h, tm, t0);
+}
+
+// Schedule-dependent device buffers and graphs (rebuilt when the pivoting mode changes).
+static void release_schedule(smlu_handle* h) {
+  h->release_graphs();
+  h->sn.free();
+  h->ilist.free();
+  h->xtasks.free();
+  h->ftiles.free();
+  h->gtasks.free();
+  h->stasks.free();
+  h->xcols.free();
+  h->swaps.free();
+  h->vbuf.free();
+  h->tinv.free();
+}
+
+static int rebuild_schedule(smlu_handle* h) {
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  release_schedule(h);
+  return build_schedule(h);
+}
+
+static bool has_tile_fronts(const smlu_handle* h) {
+  for (const SNode& r : h->hsn)
+    if (r.mode == 2) return true;
+  return false;
+}
+
+// One numeric factorization with the re-pivoting fallback (UMFPACK re-pivots in
+// every lu!, src/SharedMemSparseLU.jl:247): the diagonal-tile pivoting of large fronts only
+// searches the 64x64 diagonal tile.  When it meets a zero pivot (the matrix may still be
+// nonsingular: a zero diagonal block) or accepts weak pivots, the same values are factored
+// again with full-candidate pivoting (every fully-summed row of the front) in every blocked
+// front, and the handle keeps that mode until a refactor's host values are diagonally dominant
+// again.  A given (p, q) is never re-pivoted.
+static int run_factor(smlu_handle* h) {
+  int rc = run_factor_once(h);
+  if (rc < 0) return rc;
+  const bool off = std::getenv("SMLU_NO_REPIVOT") != nullptr;   // dev/test knob
+  if ((rc == SMLU_SINGULAR || h->weak > 0) && h->pivmode == 0 && !off && has_tile_fronts(h) &&
+      h->opts.pivot_tol > 0 && !h->plan.given_order) {
+    h->pivmode = 1;
+    int r2 = rebuild_schedule(h);
+    if (r2 != SMLU_OK) return r2;
+    ++h->repivots;
+    rc = run_factor_once(h);
+  }
+  return rc;
 }
 
 static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w) {
@@ -1353,7 +1409,8 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode)
 static bool valid_opts(const smlu_opts* o) { return o && (o->index_base == 0 || o->index_base == 1); }
 
 // Diagonal dominance of A by columns or by rows (|a_jj| >= sum of the other |a_ij|, a_jj != 0).
-static bool diagonally_dominant(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* a,
+template <class RI>
+static bool diagonally_dominant(int64_t n, const int64_t* colptr, const RI* rowval, const double* a,
                                 int64_t base) {
   std::vector<double> rdiag(n, 0.0), roff(n, 0.0);
   bool col_dom = true;
@@ -1373,6 +1430,30 @@ static bool diagonally_dominant(int64_t n, const int64_t* colptr, const int64_t*
   return true;
 }
 
+// Row transversal for a zero-free diagonal (ordering.cpp: zero_free_diagonal), computed only
+// when A has a structurally or exactly zero diagonal entry; empty = not needed / not possible.
+static std::vector<int64_t> diagonal_match(int64_t n, const int64_t* colptr, const int64_t* rowval,
+                                           const double* a, int64_t base) {
+  bool need = false;
+  for (int64_t j = 0; j < n && !need; ++j) {
+    bool has = false;
+    for (int64_t e = colptr[j] - base; e < colptr[j + 1] - base; ++e)
+      if (rowval[e] - base == j) has = a[e] != 0.0;
+    need = !has;
+  }
+  if (!need) return {};
+  const int64_t nnz = colptr[n] - base;
+  std::vector<int64_t> cp(n + 1);
+  std::vector<int32_t> ri((size_t)std::max<int64_t>(nnz, 1));
+  for (int64_t j = 0; j <= n; ++j) cp[j] = colptr[j] - base;
+  for (int64_t e = 0; e < nnz; ++e) ri[e] = (int32_t)(rowval[e] - base);
+  std::vector<int64_t> m = zero_free_diagonal(n, cp.data(), ri.data(), a);
+  bool ident = true;
+  for (int64_t j = 0; j < (int64_t)m.size() && ident; ++j) ident = m[j] == j;
+  if (ident) m.clear();
+  return m;
+}
+
 static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
                        const int64_t* p, const int64_t* q, const double* Rs, const smlu_opts* opts,
                        smlu_handle** out, int rank = 0, int nranks = 1) {
@@ -1390,14 +1471,18 @@ static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, 
   if (rc != SMLU_OK) return rc;
   std::string e;
   try {
-    e = h->plan.build(n, colptr, rowval, h->opts.index_base, plan_opts(h->opts), p, q);
+    std::vector<int64_t> match;
+    if (!p && h->opts.ordering != SMLU_ORDER_GIVEN)
+      match = diagonal_match(n, colptr, rowval, nzval, h->opts.index_base);
+    e = h->plan.build(n, colptr, rowval, h->opts.index_base, plan_opts(h->opts), p, q,
+                      match.empty() ? nullptr : match.data());
   } catch (const std::bad_alloc&) {
     return fail(nullptr, SMLU_ERR_ALLOC, "host allocation failed during analysis");
   }
   if (!e.empty()) return fail(nullptr, SMLU_ERR_ARG, e);
   h->rank = rank;
   h->nranks = nranks;
-  if (!p) h->dominant = diagonally_dominant(n, colptr, rowval, nzval, h->opts.index_base);
+  if (!p && !h->plan.matched) h->dominant = diagonally_dominant(n, colptr, rowval, nzval, h->opts.index_base);
   if (nranks > 1) {
     h->plan.compute_owners(nranks);
     h->opts.profile = 0;   // per-kind event timing is single-GPU only
@@ -1470,8 +1555,26 @@ int smlu_create_with_pivots(int64_t n, const int64_t* colptr, const int64_t* row
 
 int smlu_refactor(smlu_handle* h, const double* nzval) {
   if (!h || !nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  if (h->nranks > 1) return fail(h, SMLU_ERR_STATE, "partitioned handle: use smlu_dist_set_values");
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipMemcpyAsync(h->A.p, nzval, sizeof(double) * h->plan.nnzA, hipMemcpyHostToDevice, h->stream));
+  if (!h->plan.given_order && !h->plan.matched) {   // pivoting mode per refactor: re-check dominance
+    const Plan& P = h->plan;
+    const bool dom = diagonally_dominant(P.n, P.Acolptr.data(), P.Arow.data(), nzval, 0);
+    bool changed = false;
+    if (dom != h->dominant) {
+      h->dominant = dom;
+      changed = h->pivmode == 0;
+    }
+    if (dom && h->pivmode == 1) {
+      h->pivmode = 0;
+      changed = true;
+    }
+    if (changed) {
+      int rc = rebuild_schedule(h);
+      if (rc != SMLU_OK) return rc;
+    }
+  }
   return run_factor(h);
 }
 
@@ -1486,6 +1589,7 @@ int smlu_refactor_device(smlu_handle* h, const double* d_nzval) {
 int smlu_refactor_csc(smlu_handle* h, int64_t n, const int64_t* colptr, const int64_t* rowval,
                       const double* nzval) {
   if (!h || !colptr || !rowval || !nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  if (h->nranks > 1) return fail(h, SMLU_ERR_STATE, "partitioned handle: create a new one for a new pattern");
   const Plan& P = h->plan;
   int base = h->opts.index_base;
   bool same = (n == P.n);
@@ -1500,12 +1604,15 @@ int smlu_refactor_csc(smlu_handle* h, int64_t n, const int64_t* colptr, const in
   h->plan = Plan();
   std::string e;
   try {
-    e = h->plan.build(n, colptr, rowval, base, plan_opts(h->opts));
+    std::vector<int64_t> match = diagonal_match(n, colptr, rowval, nzval, base);
+    e = h->plan.build(n, colptr, rowval, base, plan_opts(h->opts), nullptr, nullptr,
+                      match.empty() ? nullptr : match.data());
   } catch (const std::bad_alloc&) {
     return fail(h, SMLU_ERR_ALLOC, "host allocation failed during analysis");
   }
   if (!e.empty()) return fail(h, SMLU_ERR_ARG, e);
-  h->dominant = diagonally_dominant(n, colptr, rowval, nzval, base);
+  h->dominant = !h->plan.matched && diagonally_dominant(n, colptr, rowval, nzval, base);
+  h->pivmode = 0;
   int rc = setup_device(h);
   if (rc != SMLU_OK) return rc;
   HIPCHK(hipMemcpyAsync(h->A.p, nzval, sizeof(double) * h->plan.nnzA, hipMemcpyHostToDevice, h->stream));
@@ -1516,11 +1623,8 @@ int smlu_refactor_csc(smlu_handle* h, int64_t n, const int64_t* colptr, const in
 // diagonal-tile pivoting of large fronts cannot always keep growth below 1/pivot_tol; when a
 // refactor flags such weak pivots (h->weak), refine = -1 applies up to 3 steps (the pivot-
 // failure fallback).  Stops when the residual max-norm stops halving.
-static int solve_refined(smlu_handle* h, const double* db, double* dx) {
-  const int steps = h->opts.refine < 0 ? (h->weak > 0 ? 3 : 0) : h->opts.refine;
-  h->refine_steps = 0;
-  h->refine_resid = -1;
-  if (steps == 0) return run_solve_dev(h, db, dx, 0);
+// Residual buffers and the column of every A entry (allocated on first use).
+static int ensure_residual(smlu_handle* h) {
   Plan& P = h->plan;
   const int64_t n = P.n;
   hipStream_t st = h->stream;
@@ -1536,6 +1640,19 @@ static int solve_refined(smlu_handle* h, const double* db, double* dx) {
       for (int64_t e = P.Acolptr[c]; e < P.Acolptr[c + 1]; ++e) ac[e] = (int32_t)c;
     HIPCHK(h->Acol.upload(ac.data(), ac.size(), st));
   }
+  return SMLU_OK;
+}
+
+static int solve_refined(smlu_handle* h, const double* db, double* dx) {
+  const int steps = h->opts.refine < 0 ? (h->weak > 0 ? 3 : 0) : h->opts.refine;
+  h->refine_steps = 0;
+  h->refine_resid = -1;
+  if (steps == 0) return run_solve_dev(h, db, dx, 0);
+  Plan& P = h->plan;
+  const int64_t n = P.n;
+  hipStream_t st = h->stream;
+  int rc0 = ensure_residual(h);
+  if (rc0 != SMLU_OK) return rc0;
   HIPCHK(hipMemcpyAsync(h->ref_b.p, db, sizeof(double) * n, hipMemcpyDeviceToDevice, st));   // db may alias dx
   int rc = run_solve_dev(h, h->ref_b.p, dx, 0);
   if (rc != SMLU_OK) return rc;
@@ -1558,6 +1675,22 @@ static int solve_refined(smlu_handle* h, const double* db, double* dx) {
   }
   HIPCHK(hipStreamSynchronize(st));
   h->solve_ms = ms;   // the plain solve's time (refinement steps reported separately)
+  return SMLU_OK;
+}
+
+int smlu_residual_device(smlu_handle* h, const double* d_x, const double* d_b, double* d_r, double* nrm) {
+  if (!h || !d_x || !d_b || !d_r) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  HIPCHK(hipSetDevice(h->device));
+  int rc = ensure_residual(h);
+  if (rc != SMLU_OK) return rc;
+  hipStream_t st = h->stream;
+  HIPCHK(hipMemsetAsync(h->ref_nrm.p, 0, sizeof(double), st));
+  HIPCHK(launch_residual(st, h->plan.n, h->Arowptr.p, h->Arow_ent.p, h->Acol.p, h->A.p, d_x, d_b, d_r,
+                         h->ref_nrm.p));
+  double v = 0;
+  HIPCHK(hipMemcpyAsync(&v, h->ref_nrm.p, sizeof(double), hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if (nrm) *nrm = v;
   return SMLU_OK;
 }
 
@@ -1634,6 +1767,107 @@ struct Exported {
   std::vector<double> Lx, Ux;
 };
 
+// Exact structural pattern of L and U for B = (Rs.*A)[p, q] with the pivot sequence fixed
+// (X.p, X.q already set): column k of L+U is the reach of pattern(B(:,k)) in the graph of
+// L(:, 0:k-1) (Gilbert-Peierls symbolic step; the diagonal of U is always stored).  Values
+// come from the fronts: L(i,k) from the L panel of k's front (own rows in their final
+// position, update rows looked up by their pre-interchange position), U(i,k) from the
+// diagonal block or U12 of i's front.  Every structural entry lies in the front
+// (pattern(A+A') contains it), otherwise the export fails.
+static int export_exact(smlu_handle* h, Exported& X, const std::vector<double>* store,
+                        const std::vector<int32_t>& rp) {
+  const Plan& P = h->plan;
+  const int64_t n = P.n;
+  std::vector<int64_t> pinv(n);
+  for (int64_t i = 0; i < n; ++i) pinv[X.p[i]] = i;
+  std::vector<int64_t> Lp(n + 1, 0), Up(n + 1, 0), Li, Ui;
+  std::vector<int64_t> mark(n, -1), stack(n), pstack(n), reach;
+  reach.reserve(1024);
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t c = X.q[k];
+    reach.clear();
+    for (int64_t e = P.Acolptr[c]; e < P.Acolptr[c + 1]; ++e) {
+      const int64_t i0 = pinv[P.Arow[e]];
+      if (mark[i0] == k) continue;
+      int64_t head = 0;
+      stack[0] = i0;
+      mark[i0] = k;
+      pstack[0] = i0 < k ? Lp[i0] : 0;
+      while (head >= 0) {
+        const int64_t j = stack[head];
+        bool pushed = false;
+        if (j < k) {
+          for (int64_t t = pstack[head]; t < Lp[j + 1]; ++t) {
+            const int64_t r = Li[t];
+            if (mark[r] == k) continue;
+            pstack[head] = t + 1;
+            mark[r] = k;
+            stack[++head] = r;
+            pstack[head] = r < k ? Lp[r] : 0;
+            pushed = true;
+            break;
+          }
+        }
+        if (!pushed) {
+          reach.push_back(j);
+          --head;
+        }
+      }
+    }
+    if (mark[k] != k) reach.push_back(k);
+    std::sort(reach.begin(), reach.end());
+    for (int64_t j : reach) (j <= k ? Ui : Li).push_back(j);
+    Lp[k + 1] = (int64_t)Li.size();   // strictly lower rows only (unit diagonal added below)
+    Up[k + 1] = (int64_t)Ui.size();
+  }
+  auto front_row = [&](int64_t s, int64_t g) -> int64_t {   // local index of update row g in s
+    const int32_t* b = P.s_rows.data() + P.s_rowptr[s];
+    const int32_t* e = P.s_rows.data() + P.s_rowptr[s + 1];
+    const int32_t* it = std::lower_bound(b, e, (int32_t)g);
+    return (it == e || *it != g) ? -1 : P.ns(s) + (it - b);
+  };
+  X.Lp.assign(n + 1, 0);
+  for (int64_t k = 0; k < n; ++k) X.Lp[k + 1] = X.Lp[k] + 1 + (Lp[k + 1] - Lp[k]);
+  X.Li.resize(X.Lp[n]);
+  X.Lx.resize(X.Lp[n]);
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t s = P.col2s[k], f = P.s_first[s], ns = P.ns(s), M = P.M(s), jj = k - f;
+    int64_t o = X.Lp[k];
+    X.Li[o] = k;
+    X.Lx[o++] = 1.0;
+    for (int64_t t = Lp[k]; t < Lp[k + 1]; ++t, ++o) {
+      const int64_t i = Li[t];
+      X.Li[o] = i;
+      X.Lx[o] = 0.0;
+      if (!store) continue;
+      int64_t li = i - f;
+      if (i >= f + ns) {
+        const int64_t gpre = P.s_first[P.col2s[i]] + rp[i];   // position before the interchanges
+        li = front_row(s, gpre);
+        if (li < 0) return fail(h, SMLU_ERR_STATE, "internal: structural L entry outside its front");
+      }
+      X.Lx[o] = (*store)[P.Loff[s] + jj * M + li];
+    }
+  }
+  X.Up = Up;
+  X.Ui = Ui;
+  X.Ux.assign(Ui.size(), 0.0);
+  if (store)
+    for (int64_t k = 0; k < n; ++k)
+      for (int64_t t = Up[k]; t < Up[k + 1]; ++t) {
+        const int64_t i = Ui[t];
+        const int64_t s = P.col2s[i], f = P.s_first[s], ns = P.ns(s), M = P.M(s), jj = i - f;
+        if (k < f + ns) {
+          X.Ux[t] = (*store)[P.Loff[s] + (k - f) * M + jj];
+        } else {
+          const int64_t li = front_row(s, k);
+          if (li < 0) return fail(h, SMLU_ERR_STATE, "internal: structural U entry outside its front");
+          X.Ux[t] = (*store)[P.Uoff[s] + (li - ns) * ns + jj];
+        }
+      }
+  return SMLU_OK;
+}
+
 static int export_factors(smlu_handle* h, Exported& X, bool values) {
   const Plan& P = h->plan;
   const int64_t n = P.n;
@@ -1660,6 +1894,12 @@ static int export_factors(smlu_handle* h, Exported& X, bool values) {
     int64_t f = P.s_first[s];
     for (int64_t i = f; i < P.s_first[s + 1]; ++i) X.p[i] = P.p0[f + rp[i]];
   }
+  bool any_swap = false;
+  for (int64_t s = 0; s < P.nsup && !any_swap; ++s) any_swap = swapped[s] != 0;
+  // The fronts are built on pattern(A + A'); when that is not the structure of the factors
+  // (unsymmetric A, row interchanges, a given p != q) the export takes the exact structural
+  // pattern of (Rs.*A)[p, q] for the final (p, q) and reads each entry from its front.
+  if (!P.sym_pattern || any_swap || X.p != X.q) return export_exact(h, X, values ? &store : nullptr, rp);
   // Row lists per column (L) in final positions with values; U by rows then transposed.
   X.Lp.assign(n + 1, 0);
   std::vector<int64_t> Ucnt(n + 1, 0);
@@ -1954,6 +2194,33 @@ double smlu_stat(const smlu_handle* h, const char* key) {
   if (k == "growth_max") return h->growth_max;
   if (k == "weak") return (double)h->weak;
   if (k == "dominant") return h->dominant ? 1.0 : 0.0;
+  if (k == "pivmode") return (double)h->pivmode;
+  if (k == "matched") return h->plan.matched ? 1.0 : 0.0;
+  if (k == "repivots") return (double)h->repivots;
+  if (k.rfind("launches_", 0) == 0) {   // launches per kernel variant in the factor schedule
+    const std::string v = k.substr(9);
+    double c = 0;
+    for (const Launch& L : h->fac) {
+      const bool gemm = L.kind == K_GEMM || L.kind == K_GEMMU || L.kind == K_GEMMO || L.kind == K_GEMM22;
+      const bool trsm = L.kind == K_TRSML;
+      if (v == "mfma128" && gemm && L.aux == 129) ++c;
+      else if (v == "mfma128_trsm" && trsm && L.aux == 129) ++c;
+      else if (v == "valu128" && gemm && L.aux == 128) ++c;
+      else if (v == "k64" && gemm && L.aux == 65) ++c;
+      else if (v == "k64_trsm" && trsm && L.aux == 65) ++c;
+      else if (v == "valu64" && gemm && L.aux == 64) ++c;
+      else if (v == "valu64_trsm" && trsm && L.aux == 64) ++c;
+      else if (v == "tri_inv" && L.kind == K_TRIINV) ++c;
+      else if (v == "panel_tall" && L.kind == K_PANEL && L.nwg > 512) ++c;
+    }
+    return c;
+  }
+  if (k.rfind("fronts_mode", 0) == 0) {
+    const int m = std::atoi(k.c_str() + 11);
+    double c = 0;
+    for (const SNode& r : h->hsn) c += r.mode == m ? 1 : 0;
+    return c;
+  }
   if (k == "refine_steps") return (double)h->refine_steps;
   if (k == "refine_residual") return h->refine_resid;
   if (k == "gemm_flops") return h->gemm_flops;

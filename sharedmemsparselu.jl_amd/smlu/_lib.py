@@ -63,6 +63,7 @@ SIGNATURES = {
     "smlu_refactor_csc": (i32, [vp, i64, vp, vp, vp]),
     "smlu_solve": (i32, [vp, vp, vp]),
     "smlu_solve_device": (i32, [vp, vp, vp]),
+    "smlu_residual_device": (i32, [vp, vp, vp, vp, vp]),
     "smlu_solve_multi": (i32, [vp, i64, vp, i64, vp, i64]),
     "smlu_solve_multi_device": (i32, [vp, i64, vp, i64, vp, i64]),
     "smlu_create_i32": (i32, [i64, vp, vp, vp, ctypes.POINTER(SmluOpts), ctypes.POINTER(vp)]),

@@ -54,6 +54,8 @@ class DistributedSparseLU:
         self._h = h
         self.nseg = int(C.lib().smlu_dist_nsegments(h))
         self.status = None
+        self.weak = 0
+        self.refine_steps = 0
         if factor:
             _check(C.lib().smlu_dist_set_values(h, C.ptr(vals), 0), h)
             self._factor()
@@ -147,14 +149,22 @@ class DistributedSparseLU:
             if seg > 0:
                 self._exchange(0, seg)
             rc = _check(L.smlu_dist_factor_segment(self._h, seg), self._h)
-        # every rank learns whether any rank hit a zero pivot
-        flag = self.torch.tensor([float(rc)], dtype=self.torch.float64)
+        # every rank learns whether any rank hit a zero pivot (and where) and how many weak
+        # pivots the partition accepted: [singular, weak, zero-pivot column] reduced by MAX/SUM
+        torch = self.torch
+        sing = float(rc == C.SMLU_SINGULAR)
+        col = float(L.smlu_last_error_col(self._h)) if sing else -1.0
+        st = torch.tensor([sing, col], dtype=torch.float64)
+        wk = torch.tensor([self.stat("weak")], dtype=torch.float64)
         if self.backend == "nccl":
-            flag = flag.to(self.device)
-        self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX, group=self.group)
-        self.status = int(flag.item())
-        if self.status == C.SMLU_SINGULAR:
-            raise SingularException(L.smlu_last_error_col(self._h))
+            st, wk = st.to(self.device), wk.to(self.device)
+        self.dist.all_reduce(st, op=self.dist.ReduceOp.MAX, group=self.group)
+        self.dist.all_reduce(wk, op=self.dist.ReduceOp.SUM, group=self.group)
+        self.weak = int(wk.item())
+        if st[0].item() > 0:
+            self.status = C.SMLU_SINGULAR
+            raise SingularException(int(st[1].item()))
+        self.status = C.SMLU_PIVOT_WEAK if self.weak > 0 else C.SMLU_OK
         return self.status
 
     def refactor_device(self, d_values):
@@ -162,7 +172,36 @@ class DistributedSparseLU:
         _check(C.lib().smlu_dist_set_values(self._h, ctypes.c_void_p(ptr), 1), self._h)
         return self._factor()
 
-    def solve_device(self, d_x, d_b):
+    def solve_device(self, d_x, d_b, refine=None):
+        """ldiv!(x, F, b) across the ranks; x complete on every rank.  As on one GPU
+        (smlu_solve*), weak pivots anywhere in the partition trigger up to 3 steps of iterative
+        refinement (refine=None), stopping when the residual max-norm stops halving; every rank
+        holds A and the whole x, so each computes the same residual."""
+        steps = (3 if self.weak > 0 else 0) if refine is None else int(refine)
+        if steps == 0:
+            return self._solve_once(d_x, d_b)
+        torch = self.torch
+        b = d_b.clone()                  # d_b may alias d_x
+        self._solve_once(d_x, b)
+        r = torch.empty_like(b)
+        d = torch.empty_like(b)
+        nrm = ctypes.c_double()
+        prev = float("inf")
+        self.refine_steps = 0
+        for _ in range(steps):
+            _check(C.lib().smlu_residual_device(self._h, ctypes.c_void_p(d_x.data_ptr()),
+                                                ctypes.c_void_p(b.data_ptr()),
+                                                ctypes.c_void_p(r.data_ptr()), ctypes.byref(nrm)),
+                   self._h)
+            if nrm.value == 0.0 or nrm.value > 0.5 * prev:
+                break
+            prev = nrm.value
+            self._solve_once(d, r)
+            d_x += d
+            self.refine_steps += 1
+        return d_x
+
+    def _solve_once(self, d_x, d_b):
         L = C.lib()
         pb = ctypes.c_void_p(d_b.data_ptr())
         for seg in range(self.nseg):

@@ -1,0 +1,42 @@
+"""Shared parity helpers of the GPU tests: the oracle comparison of exported factors and the
+reference's isapprox (test/runtests.jl:25-26 tolerances)."""
+import numpy as np
+import scipy.sparse as sp
+
+import oracle as O
+
+TOL = 1.0e-12
+DENSE_TOL = 1.0e-10
+
+
+def isapprox(x, y, rtol, atol):
+    """Julia's isapprox for vectors: norm(x-y) <= max(atol, rtol*max(norm(x), norm(y)))."""
+    return np.linalg.norm(x - y) <= max(atol, rtol * max(np.linalg.norm(x), np.linalg.norm(y)))
+
+
+def assert_same_pattern(G, R):
+    """CSC colptr and rowval identical (stored entries, explicit zeros included)."""
+    assert G.shape == R.shape
+    assert np.array_equal(G.indptr, R.indptr), "colptr differs from the oracle's"
+    assert np.array_equal(G.indices, R.indices), "rowval differs from the oracle's"
+
+
+def factor_parity(A, F, rtol=1e-12):
+    """Exported factors vs the oracle's fixed-pivot LU with the GPU's own (p, q)."""
+    p, q, Rs = F.p, F.q, F.Rs
+    Ro = O.rowscale(A)
+    assert np.array_equal(Rs, Ro), "row scaling must be bitwise identical"
+    ref = O.OracleLU(A, p, q, Ro)
+    assert ref.status == 0
+    L, U = F.L, F.U
+    for G, R in ((L, ref.L), (U, ref.U)):
+        # pattern: bit-identical colptr/rowval to the oracle's structural fill of (Rs.*A)[p,q]
+        assert_same_pattern(G, R)
+        D = (G - R)
+        scale = max(abs(R).max(), 1.0)
+        assert abs(D).max() <= rtol * scale, f"factor mismatch {abs(D).max()} (scale {scale})"
+    # UMFPACK contract L*U == (Rs.*A)[p,q]
+    B = (sp.diags(Rs) @ A).tocsr()[p][:, q]
+    E = L @ U - B
+    assert abs(E).max() <= 1e-10 * max(abs(B).max(), 1.0)
+    return ref

@@ -97,3 +97,75 @@ def test_dist_factor_solve_matches_single_gpu(world, which):
         r1 = np.abs(A @ x1 - b).max() / np.abs(b).max()
         r2 = np.abs(A2 @ x2 - b).max() / np.abs(b).max()
         assert r1 < 1e-12 and r2 < 1e-12, (r1, r2)
+
+
+def _weak_matrix():
+    """Two 600-pivot dense blocks with tiny 64x64 diagonal tiles (weak diagonal-tile pivots),
+    coupled only through a 64-column separator: under the natural order the assembly tree has
+    two 600-column fronts below the separator front, so two ranks each factor one block."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(21)
+    m, k = 600, 64
+    n = 2 * m + k
+    D = np.zeros((n, n))
+    for b in (0, m):
+        blk = rng.random((m, m))
+        for b0 in range(0, m, 64):
+            b1 = min(m, b0 + 64)
+            blk[b0:b1, b0:b1] = 1e-2 * rng.random((b1 - b0, b1 - b0)) + 1e-2 * np.eye(b1 - b0)
+        D[b:b + m, b:b + m] = blk
+    # block 1 couples to separator rows/columns [0, 32), block 2 to [32, 64): the blocks' last
+    # columns then do not nest into the separator (no supernode merge across it)
+    h = k // 2
+    for b, s0 in ((0, 0), (m, h)):
+        D[2 * m + s0:2 * m + s0 + h, b:b + m] = rng.random((h, m))
+        D[b:b + m, 2 * m + s0:2 * m + s0 + h] = rng.random((m, h))
+    D[2 * m:, 2 * m:] = rng.random((k, k)) + k * np.eye(k)
+    return sp.csc_matrix(D), D
+
+
+def _weak_worker(rank, world, port, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        import smlu
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        A, _ = _weak_matrix()
+        n = A.shape[0]
+        F = smlu.DistributedSparseLU(A, device=0, ordering="natural")
+        b = torch.from_numpy(np.random.default_rng(4).random(n)).cuda()
+        x = torch.empty_like(b)
+        F.solve_device(x, b)
+        q.put((rank, x.cpu().numpy(), F.weak, F.refine_steps, F.status, F.nseg, None))
+        F.close()
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((rank, None, 0, 0, 0, 0, traceback.format_exc()))
+
+
+def test_dist_weak_pivots_refine():
+    # weak pivots on any rank are summed over the partition (status SMLU_PIVOT_WEAK on every
+    # rank) and the partitioned solve refines, as the single-GPU solve does
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_weak_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=600) for _ in ps]
+    for p in ps:
+        p.join(timeout=120)
+    errs = [r[6] for r in res if r[6]]
+    assert not errs, errs[0]
+    _, D = _weak_matrix()
+    b = np.random.default_rng(4).random(D.shape[0])
+    xr = np.linalg.solve(D, b)
+    ctol = max(1e-10, 8 * np.finfo(float).eps * np.linalg.cond(D))
+    for rank, x, weak, steps, status, nseg, _ in res:
+        assert nseg > 1
+        assert weak > 0 and status == 2 and steps >= 1, (rank, weak, status, steps)
+        assert np.linalg.norm(x - xr) <= ctol * np.linalg.norm(xr), rank

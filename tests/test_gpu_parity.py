@@ -12,40 +12,7 @@ from smlu import matrices as mats
 
 pytestmark = pytest.mark.gpu
 
-TOL = 1.0e-12
-DENSE_TOL = 1.0e-10
-
-
-def isapprox(x, y, rtol, atol):
-    """Julia's isapprox for vectors: norm(x-y) <= max(atol, rtol*max(norm(x), norm(y)))."""
-    return np.linalg.norm(x - y) <= max(atol, rtol * max(np.linalg.norm(x), np.linalg.norm(y)))
-
-
-def factor_parity(A, F, rtol=1e-12):
-    """Exported factors vs the oracle's fixed-pivot LU with the GPU's own (p, q)."""
-    p, q, Rs = F.p, F.q, F.Rs
-    Ro = O.rowscale(A)
-    assert np.array_equal(Rs, Ro), "row scaling must be bitwise identical"
-    ref = O.OracleLU(A, p, q, Ro)
-    assert ref.status == 0
-    L, U = F.L, F.U
-    for G, R in ((L, ref.L), (U, ref.U)):
-        G = sp.csc_matrix(G); R = sp.csc_matrix(R)
-        # pattern: oracle's structural fill must be contained; extras hold exact zeros
-        Gp = G.copy(); Gp.data[:] = 1
-        Rp = R.copy(); Rp.data[:] = 1
-        missing = (Rp - Gp.multiply(Rp))
-        assert missing.count_nonzero() == 0, "GPU pattern misses structural entries"
-        extra = G - G.multiply(Rp)
-        assert extra.count_nonzero() == 0, "entries outside the structural pattern must be 0"
-        D = (G - R)
-        scale = max(abs(R).max(), 1.0)
-        assert abs(D).max() <= rtol * scale, f"factor mismatch {abs(D).max()} (scale {scale})"
-    # UMFPACK contract L*U == (Rs.*A)[p,q]
-    B = (sp.diags(Rs) @ A).tocsr()[p][:, q]
-    E = L @ U - B
-    assert abs(E).max() <= 1e-10 * max(abs(B).max(), 1.0)
-    return ref
+from _parity import DENSE_TOL, TOL, assert_same_pattern, factor_parity, isapprox  # noqa: F401
 
 
 @pytest.mark.parametrize("N", [4, 10, 23])
@@ -188,9 +155,11 @@ def _weak_tile_matrix(n, seed):
     return D
 
 
-def test_weak_pivots_trigger_refinement(gpu):
-    # pivot-failure fallback.  refine=-1 (default) refines only when the
-    # factorization flagged weak pivots; the refined solution meets the dense tolerance.
+def test_weak_pivots_trigger_refinement(gpu, monkeypatch):
+    # with the re-pivoting refactor switched off (SMLU_NO_REPIVOT), weak tile
+    # pivots are left to the solves: refine=-1 (default) refines only when the factorization
+    # flagged weak pivots; the refined solution meets the dense tolerance.
+    monkeypatch.setenv("SMLU_NO_REPIVOT", "1")
     n = 700
     D = _weak_tile_matrix(n, 21)
     A = sp.csc_matrix(D)

@@ -132,6 +132,8 @@ def test_golden_with_given_pivots(gpu, path):
     L = sp.csc_matrix((z["L_data"], z["L_indices"], z["L_indptr"]), shape=(n, n))
     U = sp.csc_matrix((z["U_data"], z["U_indices"], z["U_indptr"]), shape=(n, n))
     for G, R in ((F.L, L), (F.U, U)):
+        assert np.array_equal(G.indptr, R.indptr), "colptr differs from the fixture"
+        assert np.array_equal(G.indices, R.indices), "rowval differs from the fixture"
         D = (G - R)
         assert abs(D).max() <= 1e-11 * max(1.0, abs(R).max())
     x = np.empty(n)
