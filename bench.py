@@ -31,36 +31,100 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(N_cpu, ordering, grid_hint):
-    """Oracle (scalar C port of the reference's fixed-pivot LU) on a bounded sample: the same
-    workload family at N_cpu^3 with the same ordering algorithm, 1 core."""
+def _fit_power(xs, ts):
+    """Least-squares fit of log t = log a + alpha log x; returns (a, alpha)."""
+    lx, lt = np.log(np.asarray(xs, float)), np.log(np.asarray(ts, float))
+    alpha, la = np.polyfit(lx, lt, 1)
+    return float(np.exp(la)), float(alpha)
+
+
+def cpu_baseline(N_head, upd_head, nnz_head, ordering, grid_hint, samples=(24, 32, 40)):
+    """CPU baselines on the GPU box's host, reported beside the GPU number:
+
+    * value: the oracle (scalar C port of the reference's numeric LU, fixed pivots, 1 core as
+      the reference's UMFPACK path runs) timed on 3D Poisson 24^3, 32^3 and 40^3 with the same
+      ordering algorithm; log(time) fitted linearly in log(upd) (upd = sum_k |L_k||U_k|, exact
+      from each plan) and EXTRAPOLATED to the headline config's upd -> seconds and nnz(L+U)/s
+      of one headline refactor on one core.  A full C3 run would take hours.
+    * superlu: scipy's SuperLU (splu, MMD on A'+A, diag_pivot_thresh 0.1: UMFPACK-like symmetric
+      strategy) as the third-party anchor: timed at C2 (2D Poisson 512^2) and at the same 3D
+      samples, extrapolated to the headline n with its own fitted exponent.
+    * throughput_16_independent: 16 concurrent oracle factorizations of the 32^3 sample (one
+      per core of the box's CPU share; NOT a parallel factorization of one matrix)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
+    import scipy.sparse.linalg as spla
     import smlu
     from smlu import matrices as mats
-    A = mats.poisson3d(N_cpu)
-    P = smlu.Plan(A, grid=(N_cpu,) * 3 if grid_hint else None)
-    q = P.q()
-    Rs = O.rowscale(A)
+    rows, lu_t, lu_n = [], [], []
+    keep = None
+    for N in samples:
+        A = mats.poisson3d(N)
+        P = smlu.Plan(A, grid=(N,) * 3 if grid_hint else None)
+        q = P.q()
+        Rs = O.rowscale(A)
+        t0 = time.perf_counter()
+        F = O.OracleLU(A, q, q, Rs)
+        dt = time.perf_counter() - t0
+        nnz = F.L.nnz + F.U.nnz - A.shape[0]
+        rows.append({"N": N, "seconds": dt, "upd": P.stat("upd"), "nnzLU": nnz,
+                     "nnzLU_per_s": nnz / dt, "gflops": 2 * P.stat("upd") / dt / 1e9})
+        t0 = time.perf_counter()
+        lu = spla.splu(A.tocsc(), permc_spec="MMD_AT_PLUS_A", diag_pivot_thresh=0.1)
+        lu_t.append(time.perf_counter() - t0)
+        lu_n.append({"N": N, "seconds": lu_t[-1], "nnzLU": int(lu.L.nnz + lu.U.nnz - A.shape[0])})
+        if N == 32:
+            keep = (A, q, Rs, nnz)
+        log(f"cpu baseline sample {N}^3: oracle {dt:.2f} s, superlu {lu_t[-1]:.2f} s")
+    a, alpha = _fit_power([r["upd"] for r in rows], [r["seconds"] for r in rows])
+    t_head = a * upd_head ** alpha
+    res = {"value": nnz_head / t_head, "unit": "nnz(L+U)/s", "cores": 1, "kind": "port",
+           "sample": (f"oracle (fixed-pivot Gilbert-Peierls LU, scalar C, 1 core) on 3D Poisson "
+                      f"{'/'.join(f'{N}^3' for N in samples)} ({ordering} order); time fitted as "
+                      f"{a:.3g} * upd^{alpha:.3f} and extrapolated to {N_head}^3 (upd={upd_head:.4g}): "
+                      f"{t_head:.0f} s per refactor"),
+           "extrapolated": True, "headline_seconds": t_head, "fit": {"a": a, "alpha": alpha},
+           "samples": rows}
+    # SuperLU anchor: C2 measured; headline n extrapolated from the 3D samples (t ~ n^beta)
+    A2 = mats.poisson2d(512)
     t0 = time.perf_counter()
-    F = O.OracleLU(A, q, q, Rs)
-    dt = time.perf_counter() - t0
-    nnz = F.L.nnz + F.U.nnz - A.shape[0]
-    one = {"value": nnz / dt, "unit": "nnz(L+U)/s", "cores": 1, "kind": "port",
-           "sample": f"oracle fixed-pivot Gilbert-Peierls LU of 3D Poisson {N_cpu}^3 "
-                     f"({ordering} order, nnz(L+U)={nnz}, upd={P.stat('upd'):.3g}) in {dt:.2f} s",
-           "seconds": dt, "gflops": 2 * P.stat("upd") / dt / 1e9}
-    # all host cores (SURVEY §8d-i): the same factorization on C threads at once (the C oracle
-    # runs without the GIL), aggregate throughput; C = the box's CPU share (16) or fewer
+    lu = spla.splu(A2.tocsc(), permc_spec="MMD_AT_PLUS_A", diag_pivot_thresh=0.1)
+    t_c2 = time.perf_counter() - t0
+    b, beta = _fit_power([N ** 3 for N in samples], lu_t)
+    t_sl = b * float(N_head ** 3) ** beta
+    res["superlu"] = {"kind": "third-party", "cores": 1,
+                      "c2_poisson2d_512_seconds": t_c2, "c2_nnzLU": int(lu.L.nnz + lu.U.nnz - A2.shape[0]),
+                      "c2_nnzLU_per_s": (lu.L.nnz + lu.U.nnz - A2.shape[0]) / t_c2,
+                      "samples_3d": lu_n, "fit": {"b": b, "beta": beta},
+                      "headline_seconds_extrapolated": t_sl,
+                      "note": "scipy.sparse.linalg.splu (SuperLU), MMD on A'+A, diag_pivot_thresh 0.1; "
+                              "its own ordering and fill, so nnz(L+U) differs from the GPU plan's"}
+    # 16 independent copies of the 32^3 sample at once (the C oracle releases the GIL)
     from concurrent.futures import ThreadPoolExecutor
+    A, q, Rs, nnz = keep
     C = max(1, min(16, os.cpu_count() or 1))
     t0 = time.perf_counter()
     with ThreadPoolExecutor(C) as ex:
         list(ex.map(lambda _: O.OracleLU(A, q, q, Rs), range(C)))
     dtc = time.perf_counter() - t0
-    one["all_cores"] = {"value": C * nnz / dtc, "unit": "nnz(L+U)/s", "cores": C, "kind": "port",
-                        "sample": f"{C} concurrent copies of the same factorization in {dtc:.2f} s"}
-    return one
+    res["throughput_16_independent"] = {
+        "value": C * nnz / dtc, "unit": "nnz(L+U)/s", "cores": C, "kind": "port",
+        "sample": f"{C} independent oracle factorizations of the 32^3 sample running concurrently "
+                  f"({dtc:.2f} s): aggregate throughput over {C} problems, not one parallel factorization"}
+    return res
+
+
+def kernel_source_sha():
+    """Hash of the library sources: a committed PMC profile applies to this build only if its
+    recorded hash matches (otherwise its traffic numbers are stale and are not reported)."""
+    import hashlib
+    hs = hashlib.sha1()
+    d = os.path.join(ROOT, "sharedmemsparselu.jl_amd", "csrc")
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".cpp", ".hpp")):
+            with open(os.path.join(d, f), "rb") as fh:
+                hs.update(f.encode() + fh.read())
+    return hs.hexdigest()[:12]
 
 
 def max_over_ranks(x, device=None):
@@ -101,7 +165,6 @@ def main():
     ap.add_argument("--side", "--n", dest="n", type=int, default=128,
                     help="grid side of the 3D Poisson workload")
     ap.add_argument("--ordering", default="nd", choices=["nd", "geometric"])
-    ap.add_argument("--cpu-n", type=int, default=32, help="grid side of the CPU baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--test-one-gpu", action="store_true",
@@ -198,19 +261,22 @@ def main():
         achieved = gemm_flops / (ms_gemm * 1e-3) / 1e12 if ms_gemm > 0 else None
         n_gemm = F.stat("gemm_launches")
         avg_us = ms_gemm * 1e3 / n_gemm if (n_gemm and ms_gemm > 0) else None
-        traffic, traffic_src = None, "not collected"
-        pmc = os.path.join(ROOT, "profiles", "r01", f"pmc_gemm_{N}.json")
-        if os.path.exists(pmc):
+        # PMC traffic comes from a committed rocprofv3 profile (profiles/<round>/pmc_gemm_N.json);
+        # it is reported only when that profile was taken from this exact library source
+        # (kernels_sha) on the single-GPU path, otherwise null.
+        sha = kernel_source_sha()
+        traffic, traffic_src, hbm_refactor, pm = None, "no profile of this build", None, None
+        import glob
+        for pmc in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"pmc_gemm_{N}.json")), reverse=True):
             with open(pmc) as fh:
-                pm = json.load(fh)
+                cand = json.load(fh)
+            if cand.get("kernels_sha") == sha:
+                pm, traffic_src = cand, os.path.relpath(pmc, ROOT)
+                break
+        if pm is not None and not partitioned:
             traffic = pm.get("hbm_bytes_per_launch")
-            traffic_src = os.path.relpath(pmc, ROOT)
-        hbm_refactor = None
-        if os.path.exists(pmc):
             hbm_refactor = pm.get("refactor_all_kernels", {}).get("hbm_bytes")
         nnzA = A.nnz
-        # SURVEY §8(d) algorithmic bytes of the scatter/gather formulation, for reference
-        bytes_sg = 12 * upd + 12 * nnzA + 12 * nnzLU + 16 * (n + 1)
         res = {
             "metric": "nnz(L+U)/s + achieved HBM GB/s, 3D Poisson 128³ numeric LU, 1/2/4/8 GPU",
             "value": nnzLU * (1 if partitioned else world) / (ms_per_step * 1e-3),
@@ -234,9 +300,11 @@ def main():
                          "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic,
-                         "launches_per_step": n_gemm, "avg_launch_us": avg_us,
-                         "flops_per_launch": gemm_flops / n_gemm if n_gemm else None,
-                         "algorithmic_bytes_per_launch": F.stat("gemm_bytes") / n_gemm if n_gemm else None,
+                         "launches_per_step": n_gemm if not partitioned else None,
+                         "avg_launch_us": avg_us,
+                         "flops_per_launch": gemm_flops / n_gemm if (n_gemm and not partitioned) else None,
+                         "algorithmic_bytes_per_launch": F.stat("gemm_bytes") / n_gemm if (n_gemm and not partitioned) else None,
+                         "traffic_source": traffic_src, "kernels_sha": sha,
                          "note": "fp64 MFMA (v_mfma_f64_16x16x4) 128x128 tiles for large launches, fp64 VALU "
                                  "64x64 tiles for small ones; peak = MI355X fp64 dense peak; "
                                  "achieved = GEMM flops per refactor / HIP-event time of the GEMM "
@@ -251,7 +319,6 @@ def main():
                             "f22_gflop": F.stat("gemm22_flops") / 1e9}
                            if ms_gemm > 0 and kind_ms["gemm22"] > 0 else None),
             "refactor_tflops": dense_flops / (ms_per_step * 1e-3) / 1e12,
-            "scatter_gather_equiv_GBs": bytes_sg / (ms_per_step * 1e-3) / 1e9,
             # measured HBM traffic of a whole refactor (PMC FETCH_SIZE x2 + WRITE_SIZE over every
             # kernel, profiles/) over this run's time per refactor
             "achieved_hbm_GBs": (hbm_refactor / (ms_per_step * 1e-3) / 1e9) if hbm_refactor else None,
@@ -262,7 +329,7 @@ def main():
         }
         if not args.no_cpu and world == 1:
             log("cpu baseline ...")
-            res["cpu_baseline"] = cpu_baseline(args.cpu_n, args.ordering, args.ordering == "geometric")
+            res["cpu_baseline"] = cpu_baseline(N, upd, nnzLU, args.ordering, args.ordering == "geometric")
         print(json.dumps(res), flush=True)
     F.close()
     if world > 1:

@@ -11,6 +11,9 @@ import os
 import re
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import kernel_source_sha  # noqa: E402
+
 N = int(sys.argv[1])
 out_dir = sys.argv[2]
 base = "gpurun_out"
@@ -54,6 +57,7 @@ res = {
     "traffic_over_algorithmic": hbm / alg_bytes,
     "gemm_flops": flops,
     "correction": "FETCH_SIZE x2 (gfx950 wide-read tally), KiB -> bytes; WRITE_SIZE as is",
+    "kernels_sha": kernel_source_sha(),
 }
 # whole factorization (every kernel, incl. the memset fills): HBM bytes per refactor
 if os.path.exists(os.path.join(base, f"pmcall_FETCH_SIZE_{N}", "pmc_counter_collection.csv")):
