@@ -47,10 +47,14 @@ struct FrontTile {
 
 // Extend-add task: parent front p's column tj receives cnt child columns, listed as (child,
 // child column) pairs at contrib[off, off+cnt) in child order.
+// Assembly task: column tj of front p.  Child contributions xtasks[off, off+cnt) (child, child
+// F22 column) in child order; A entries aents[aoff, aoff+acnt) as (entry id, local row), rows
+// ascending.
 struct XCol {
   int32_t p, tj;
   int64_t off;
-  int32_t cnt, pad;
+  int32_t cnt, acnt;
+  int64_t aoff;
 };
 
 // Row swaps of one or more consecutive panels (sub-panels kb0 + u*nb, swap-list slots slot0 + u,

@@ -5,8 +5,8 @@
 //
 // Reference mapping (SharedMemSparseLU.jl):
 //   k_rowscale            UMFPACK SUM scaling behind lu(A) (src/SharedMemSparseLU.jl:74, Rs at :51)
-//   k_scatterA            gather A's values into fronts (the "active columns")
-//   k_extend_add          scatter of Schur-complement updates into ancestor fronts
+//   k_assemble            gather A's values into fronts (the "active columns") and the children's
+//                         Schur-complement updates (extend-add), one pass per front column
 //   k_front_lds           whole small fronts in LDS: pivot search, pivot scaling, rank-1 updates
 //   k_panel_reg, k_laswp, the same column-elimination loop of lu(A)/lu!(F,A) (:74, :247) for
 //   k_step_trsm, k_trsm_u, large fronts, blocked: panel, row swaps, triangular solves and
@@ -36,87 +36,101 @@ __global__ void k_fill(int64_t n, double* __restrict__ x, double v) {
 }
 
 // ------------------------------------------------------------------------------------
-// Front assembly, part 1: A entries of this level's fronts -> their slots (plain stores into
-// freshly zeroed fronts; every A entry owns a unique slot).
+// Front assembly (one wave per front column, one launch per level): the column is built in
+// 256-row chunks in LDS -- zeros, then the scaled A entries (plain stores: every entry owns
+// its slot), then each contributing child's F22 column added in child order -- and written
+// once, coalesced.  No memset of the fronts and no read-modify-write of the parent: every
+// front element is written exactly once per factorization, every child F22 element and its
+// row map read once.  The order of the additions per element is that of a zeroed front with
+// A stored and the children added in child order (deterministic, no atomics).
+// Lane q < 64 keeps the running position of contribution q in its child column (row maps are
+// ascending, chunks are visited in ascending row order); contributions beyond the 64th find
+// their start by binary search.
 // ------------------------------------------------------------------------------------
-__global__ void k_scatterA(int64_t cnt, const int32_t* __restrict__ ents,
-                           const int64_t* __restrict__ dest, const int32_t* __restrict__ arow,
-                           const double* __restrict__ a, const double* __restrict__ Rs,
-                           double* __restrict__ store, double* __restrict__ scratch) {
-  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= cnt) return;
-  int32_t e = ents[t];
-  double v = Rs[arow[e]] * a[e];
-  int64_t d = dest[e];
-  if (d >= 0) store[d] = v;
-  else scratch[-1 - d] = v;
-}
-
-// ------------------------------------------------------------------------------------
-// Front assembly, part 2 (extend-add): one wave per parent column; it adds the contributing
-// child F22 columns one after the other in child order (deterministic, no atomics, one
-// launch per level).  4 independent elements per lane in flight.
-// ------------------------------------------------------------------------------------
-__global__ void k_extend_add(int64_t ntasks, const XCol* __restrict__ cols,
-                             const int2* __restrict__ contrib, const SNode* __restrict__ sn,
-                             const int32_t* __restrict__ relmap, double* __restrict__ store,
-                             double* __restrict__ scratch) {
+__global__ __launch_bounds__(256) void k_assemble(int64_t ntasks, const XCol* __restrict__ cols,
+                                                  const int2* __restrict__ contrib,
+                                                  const int2* __restrict__ aents,
+                                                  const SNode* __restrict__ sn,
+                                                  const int32_t* __restrict__ relmap,
+                                                  const double* __restrict__ a,
+                                                  const int32_t* __restrict__ arow,
+                                                  const double* __restrict__ Rs,
+                                                  double* __restrict__ store, double* __restrict__ scratch) {
+  __shared__ double sbuf[4][256];
   const int64_t w = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (w >= ntasks) return;
+  double* b = sbuf[threadIdx.x >> 6];
   const XCol t = cols[w];
   const SNode p = sn[t.p];
   FrontPtrs P = front_ptrs(p, store, scratch);
+  const int64_t len = P.M;
   const int64_t tj = t.tj;
-  for (int q = 0; q < t.cnt; ++q) {
-    if (q > 0) __threadfence_block();   // the previous child's stores before this child's loads
-    const int2 ck = contrib[t.off + q];
-    const SNode c = sn[ck.x];
-    const int64_t nuc = c.nu;
-    const double* src = scratch + c.Foff + (int64_t)ck.y * nuc;
-    const int32_t* rm = relmap + c.rowptr;
-    if (tj < P.ns) {
-      gdbl* col = P.L + tj * P.M;
-      for (int64_t i0 = lane; i0 < nuc; i0 += 256) {
-        double v[4];
-        int32_t r[4];
+  // destination of local row r of this column
+  gdbl* colL = tj < P.ns ? P.L + tj * P.M : nullptr;
+  gdbl* colU = tj < P.ns ? nullptr : P.U + (tj - P.ns) * P.ns;
+  gdbl* colF = (tj < P.ns || P.nu == 0) ? nullptr : P.F + (tj - P.ns) * P.nu - P.ns;
+  int cur = 0;                  // lane q: position in contribution q's child column
+  int64_t ap = 0;               // next A entry
+  for (int64_t r0 = 0; r0 < len; r0 += 256) {
+    const int64_t r1 = min<int64_t>(len, r0 + 256);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int64_t i = i0 + 64 * u;
-          v[u] = i < nuc ? src[i] : 0.0;
-          r[u] = i < nuc ? rm[i] : -1;
+    for (int u = 0; u < 4; ++u) b[lane + 64 * u] = 0.0;
+    wave_lds_sync();
+    while (ap < t.acnt) {       // A entries with rows in [r0, r1): a prefix of the rest
+      const int64_t i = ap + lane;
+      int2 en = make_int2(0, 0x7fffffff);
+      if (i < t.acnt) en = aents[t.aoff + i];
+      const bool take = en.y < r1;
+      const unsigned long long m = __ballot(take);
+      if (take) b[en.y - r0] = Rs[arow[en.x]] * a[en.x];
+      const int c = __popcll(m);
+      ap += c;
+      if (c < 64) break;
+    }
+    wave_lds_sync();
+    for (int q = 0; q < t.cnt; ++q) {
+      const int2 ck = contrib[t.off + q];
+      const SNode c = sn[ck.x];
+      const int64_t nuc = c.nu;
+      const double* src = scratch + c.Foff + (int64_t)ck.y * nuc;
+      const int32_t* rm = relmap + c.rowptr;
+      int64_t pos;
+      if (q < 64) {
+        pos = __builtin_amdgcn_readlane(cur, q);
+      } else {                  // binary search for the first row >= r0
+        int64_t lo = 0, hi = nuc;
+        while (lo < hi) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (rm[mid] < r0) lo = mid + 1;
+          else hi = mid;
         }
-        double cv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) cv[u] = r[u] >= 0 ? col[r[u]] : 0.0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (r[u] >= 0) col[r[u]] = cv[u] + v[u];
+        pos = lo;
       }
-    } else {
-      gdbl* colU = P.U + (tj - P.ns) * P.ns;
-      gdbl* colF = P.F + (tj - P.ns) * P.nu - P.ns;
-      for (int64_t i0 = lane; i0 < nuc; i0 += 256) {
-        double v[4];
-        int32_t r[4];
+      while (pos < nuc) {
+        const int64_t i = pos + lane;
+        const int32_t r = i < nuc ? rm[i] : 0x7fffffff;
+        const bool take = r < r1;
+        const unsigned long long m = __ballot(take);
+        if (take) b[r - r0] += src[i];
+        const int cn = __popcll(m);
+        pos += cn;
+        if (cn < 64) break;
+      }
+      if (q < 64 && lane == q) cur = (int)pos;
+      wave_lds_sync();
+    }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int64_t i = i0 + 64 * u;
-          v[u] = i < nuc ? src[i] : 0.0;
-          r[u] = i < nuc ? rm[i] : -1;
-        }
-        gdbl* dst[4];
-        double cv[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          dst[u] = r[u] < 0 ? nullptr : (r[u] < P.ns ? colU + r[u] : colF + r[u]);
-          cv[u] = dst[u] ? *dst[u] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (dst[u]) *dst[u] = cv[u] + v[u];
+    for (int u = 0; u < 4; ++u) {
+      const int64_t r = r0 + lane + 64 * u;
+      if (r < r1) {
+        const double v = b[lane + 64 * u];
+        if (colL) colL[r] = v;
+        else if (r < P.ns) colU[r] = v;
+        else colF[r] = v;
       }
     }
+    wave_lds_sync();
   }
 }
 
@@ -1074,17 +1088,12 @@ hipError_t launch_fill(hipStream_t st, int64_t n, double* x, double v) {
   k_fill<<<nblk(n, 256), 256, 0, st>>>(n, x, v);
   return hipGetLastError();
 }
-hipError_t launch_scatterA(hipStream_t st, int64_t cnt, const int32_t* ents, const int64_t* dest,
-                           const int32_t* arow, const double* a, const double* Rs, double* store,
-                           double* scratch) {
-  if (cnt <= 0) return hipSuccess;
-  k_scatterA<<<nblk(cnt, 256), 256, 0, st>>>(cnt, ents, dest, arow, a, Rs, store, scratch);
-  return hipGetLastError();
-}
-hipError_t launch_extend_add(hipStream_t st, int64_t ntasks, const XCol* cols, const int2* contrib,
-                             const SNode* sn, const int32_t* relmap, double* store, double* scratch) {
+hipError_t launch_assemble(hipStream_t st, int64_t ntasks, const XCol* cols, const int2* contrib,
+                           const int2* aents, const SNode* sn, const int32_t* relmap, const double* a,
+                           const int32_t* arow, const double* Rs, double* store, double* scratch) {
   if (ntasks <= 0) return hipSuccess;
-  k_extend_add<<<nblk(ntasks * 64, 256), 256, 0, st>>>(ntasks, cols, contrib, sn, relmap, store, scratch);
+  k_assemble<<<(unsigned)((ntasks + 3) / 4), 256, 0, st>>>(ntasks, cols, contrib, aents, sn, relmap, a, arow,
+                                                            Rs, store, scratch);
   return hipGetLastError();
 }
 hipError_t launch_front_lds(hipStream_t st, int cnt, int Mmax, const int32_t* list, const SNode* sn,

@@ -575,6 +575,9 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
 
   // ---- A map ----
   Adest.assign(nnzA, 0);
+  A_s.assign(nnzA, 0);
+  A_li.assign(nnzA, 0);
+  A_lj.assign(nnzA, 0);
   std::vector<int> ent_level(nnzA, 0);
   for (int64_t c = 0; c < n; ++c) {
     int64_t pc = qinv[c];
@@ -590,6 +593,9 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
       else if (li < a) dest = Uoff[s] + (lj - a) * a + li;
       else dest = -1 - (Foff[s] + (lj - a) * (m - a) + (li - a));
       Adest[e] = dest;
+      A_s[e] = (int32_t)s;
+      A_li[e] = (int32_t)li;
+      A_lj[e] = (int32_t)lj;
       ent_level[e] = s_level[s];
     }
   }

@@ -88,6 +88,7 @@ struct Plan {
   // ---- A entry -> front slot ----
   // dest >= 0: factor store offset;  dest < 0: scratch offset (-1 - dest)
   std::vector<int64_t> Adest;
+  std::vector<int32_t> A_s, A_li, A_lj;       // front, local row, local column of each entry
   std::vector<int64_t> Alev_ptr;              // nlevels+1
   std::vector<int32_t> Alev_ent;              // A entry ids grouped by level, sorted by dest
   // row-scaling support: A entries grouped by row (CSR order of A)

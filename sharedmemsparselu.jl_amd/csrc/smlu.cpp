@@ -30,10 +30,8 @@
 namespace smlu {
 hipError_t launch_rowscale(hipStream_t, int64_t, const int64_t*, const int32_t*, const double*, double*);
 hipError_t launch_fill(hipStream_t, int64_t, double*, double);
-hipError_t launch_scatterA(hipStream_t, int64_t, const int32_t*, const int64_t*, const int32_t*,
-                           const double*, const double*, double*, double*);
-hipError_t launch_extend_add(hipStream_t, int64_t, const XCol*, const int2*, const SNode*, const int32_t*,
-                             double*, double*);
+hipError_t launch_assemble(hipStream_t, int64_t, const XCol*, const int2*, const int2*, const SNode*,
+                           const int32_t*, const double*, const int32_t*, const double*, double*, double*);
 hipError_t launch_front_lds(hipStream_t, int, int, const int32_t*, const SNode*, double*, double*,
                             int32_t*, int32_t*, double*, double, double);
 hipError_t init_kernel_attributes();
@@ -151,10 +149,10 @@ struct smlu_handle {
   DBuf<int32_t> Acol;                          // column of each A entry (residuals)
   int refine_steps = 0;
   double refine_resid = -1;
-  DBuf<int64_t> Arowptr, Adest, p0, q, posfirst;
-  DBuf<int32_t> Arow_ent, Arow, Alev_ent, rows, relmap, chlist, ilist, rowperm, rowperm0, info, swaps;
+  DBuf<int64_t> Arowptr, p0, q, posfirst;
+  DBuf<int32_t> Arow_ent, Arow, rows, relmap, chlist, ilist, rowperm, rowperm0, info, swaps;
   DBuf<SNode> sn;
-  DBuf<int2> xtasks;
+  DBuf<int2> xtasks, aents;
   DBuf<FrontTile> ftiles;
   DBuf<GemmTask> gtasks;
   DBuf<SwapTask> stasks;
@@ -210,12 +208,13 @@ struct smlu_handle {
     ch_version = -1;
     Acol.free();
     for (auto* b : d) b->free();
-    DBuf<int64_t>* l[] = {&Arowptr, &Adest, &p0, &q, &posfirst};
+    DBuf<int64_t>* l[] = {&Arowptr, &p0, &q, &posfirst};
     for (auto* b : l) b->free();
-    DBuf<int32_t>* i[] = {&Arow_ent, &Arow, &Alev_ent, &rows, &relmap, &chlist, &ilist, &rowperm, &rowperm0, &info, &swaps};
+    DBuf<int32_t>* i[] = {&Arow_ent, &Arow, &rows, &relmap, &chlist, &ilist, &rowperm, &rowperm0, &info, &swaps};
     for (auto* b : i) b->free();
     sn.free();
     xtasks.free();
+    aents.free();
     ftiles.free();
     gtasks.free();
     stasks.free();
@@ -350,6 +349,20 @@ static int build_schedule(smlu_handle* h) {
   std::vector<GemmTask> gt;
   std::vector<SwapTask> st_tasks;
   std::vector<XCol> xc;
+  std::vector<int2> ae;
+  // A entries grouped by front, sorted by (local column, local row)
+  std::vector<int64_t> fr_ptr(nsup + 1, 0);
+  std::vector<int32_t> fr_ent((size_t)P.nnzA);
+  {
+    for (int64_t e = 0; e < P.nnzA; ++e) ++fr_ptr[P.A_s[e] + 1];
+    for (int64_t s = 0; s < nsup; ++s) fr_ptr[s + 1] += fr_ptr[s];
+    std::vector<int64_t> fp(fr_ptr.begin(), fr_ptr.end() - 1);
+    for (int64_t e = 0; e < P.nnzA; ++e) fr_ent[fp[P.A_s[e]]++] = (int32_t)e;
+    for (int64_t s = 0; s < nsup; ++s)
+      std::sort(fr_ent.begin() + fr_ptr[s], fr_ent.begin() + fr_ptr[s + 1], [&](int32_t a, int32_t b) {
+        return P.A_lj[a] != P.A_lj[b] ? P.A_lj[a] < P.A_lj[b] : P.A_li[a] < P.A_li[b];
+      });
+  }
   double* store = h->store.p;
   double* scratch = h->scratch.p;
   h->fac.clear();
@@ -434,27 +447,8 @@ static int build_schedule(smlu_handle* h) {
   for (int l = 0; l < P.nlevels; ++l) {
     Launch L;
     if (isx[l]) h->fac_seg.push_back(h->fac.size());   // exchange point before this level
-    // zero this level's fronts
-    L = Launch();
-    L.kind = K_MEMSET_STORE;
-    L.off = P.lev_foff[l];
-    L.cnt = P.lev_foff[l + 1] - P.lev_foff[l];
-    if (L.cnt > 0) h->fac.push_back(L);
-    if (P.lev_ssize[l] > 0) {
-      L = Launch();
-      L.kind = K_MEMSET_SCRATCH;
-      L.off = P.lev_soff[l];
-      L.cnt = P.lev_ssize[l];
-      h->fac.push_back(L);
-    }
-    // A entries
-    L = Launch();
-    L.kind = K_SCATTER;
-    L.off = P.Alev_ptr[l];
-    L.cnt = P.Alev_ptr[l + 1] - P.Alev_ptr[l];
-    if (L.cnt > 0) h->fac.push_back(L);
-    // extend-add: one task per (parent, target column) with its contributing child columns
-    // in child order (counting sort by target column per parent)
+    // assembly: every column of this level's fronts built once (zeros, scaled A entries, the
+    // children's F22 columns in child order) -- k_assemble, one wave per column
     {
       L = Launch();
       L.kind = K_EXTADD;
@@ -462,7 +456,6 @@ static int build_schedule(smlu_handle* h) {
       std::vector<int32_t> cnt, pos;
       for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {
         int64_t s = LS[k];
-        if (P.ch_ptr[s] == P.ch_ptr[s + 1]) continue;
         const int64_t M = P.M(s);
         cnt.assign(M + 1, 0);
         for (int64_t ci = P.ch_ptr[s]; ci < P.ch_ptr[s + 1]; ++ci) {
@@ -479,9 +472,18 @@ static int build_schedule(smlu_handle* h) {
           const int32_t* rm = P.relmap.data() + h->hsn[c].rowptr;
           for (int64_t jc = 0; jc < P.nu(c); ++jc) xt[base + pos[rm[jc]]++] = make_int2((int)c, (int)jc);
         }
-        for (int64_t tj = 0; tj < M; ++tj)
-          if (cnt[tj + 1] > cnt[tj])
-            xc.push_back(XCol{(int32_t)s, (int32_t)tj, base + cnt[tj], cnt[tj + 1] - cnt[tj], 0});
+        // A entries of this front by (column, row)
+        int64_t ea = fr_ptr[s];
+        const int64_t eb = fr_ptr[s + 1];
+        for (int64_t tj = 0; tj < M; ++tj) {
+          const int64_t a0 = (int64_t)ae.size();
+          while (ea < eb && P.A_lj[fr_ent[ea]] == tj) {
+            ae.push_back(make_int2(fr_ent[ea], P.A_li[fr_ent[ea]]));
+            ++ea;
+          }
+          xc.push_back(XCol{(int32_t)s, (int32_t)tj, base + cnt[tj], cnt[tj + 1] - cnt[tj],
+                            (int32_t)((int64_t)ae.size() - a0), a0});
+        }
       }
       L.cnt = (int64_t)xc.size() - L.off;
       if (L.cnt > 0) h->fac.push_back(L);
@@ -1003,10 +1005,38 @@ static int build_schedule(smlu_handle* h) {
   }
 
   h->nlaunch = (int64_t)h->fac.size();
+  if (const char* path = std::getenv("SMLU_DUMP_SCHEDULE")) {   // dev: per-launch table for trace joins
+    if (FILE* fp = std::fopen(path, "w")) {
+      std::fprintf(fp, "idx,kind,name,step,tile,nwg,cnt,flops,kmax,mn\n");
+      for (size_t i = 0; i < h->fac.size(); ++i) {
+        const Launch& L = h->fac[i];
+        int kmax = 0;
+        double mn = 0;
+        const bool g = L.kind == K_GEMM || L.kind == K_GEMMU || L.kind == K_GEMMO || L.kind == K_GEMM22 ||
+                       L.kind == K_TRSML;
+        if (g)
+          for (int64_t t = 0; t < L.cnt; ++t) {
+            kmax = std::max(kmax, gt[L.off + t].k);
+            mn += (double)gt[L.off + t].m * gt[L.off + t].n;
+          }
+        double rd = 0;
+        if (L.kind == K_EXTADD)   // mn = front elements written, flops column = child values read
+          for (int64_t t = 0; t < L.cnt; ++t) {
+            const XCol& x = xc[L.off + t];
+            mn += (double)P.M(x.p);
+            for (int64_t q = 0; q < x.cnt; ++q) rd += (double)P.nu(xt[x.off + q].x);
+          }
+        std::fprintf(fp, "%zu,%d,%s,%d,%lld,%lld,%lld,%.0f,%d,%.0f\n", i, L.kind, kKindName[L.kind], L.step,
+                     (long long)L.aux, (long long)L.nwg, (long long)L.cnt, L.kind == K_EXTADD ? rd : L.flops, kmax, mn);
+      }
+      std::fclose(fp);
+    }
+  }
   // upload
   HIPCHK(h->sn.upload(h->hsn.data(), h->hsn.size(), st));
   HIPCHK(h->ilist.upload(ilist.data(), ilist.size(), st));
   HIPCHK(h->xtasks.upload(xt.data(), xt.size(), st));
+  HIPCHK(h->aents.upload(ae.data(), ae.size(), st));
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
   if (!tinv_patch.empty()) {   // operands in the tile-inverse slots: patch in the buffer address
     HIPCHK(h->tinv.alloc((size_t)max_list * 8192));
@@ -1065,8 +1095,6 @@ static int setup_device(smlu_handle* h) {
   HIPCHK(h->Arowptr.upload(P.Arowptr.data(), P.Arowptr.size(), st));
   HIPCHK(h->Arow_ent.upload(P.Arow_ent.data(), P.Arow_ent.size(), st));
   HIPCHK(h->Arow.upload(P.Arow.data(), P.Arow.size(), st));
-  HIPCHK(h->Adest.upload(P.Adest.data(), P.Adest.size(), st));
-  HIPCHK(h->Alev_ent.upload(P.Alev_ent.data(), P.Alev_ent.size(), st));
   HIPCHK(h->p0.upload(P.p0.data(), P.p0.size(), st));
   HIPCHK(h->q.upload(P.q.data(), P.q.size(), st));
   HIPCHK(h->rows.upload(P.s_rows.data(), P.s_rows.size(), st));
@@ -1144,12 +1172,9 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
       return hipMemsetAsync(h->store.p + L.off, 0, (size_t)L.cnt * sizeof(double), st);
     case K_MEMSET_SCRATCH:
       return hipMemsetAsync(h->scratch.p + L.off, 0, (size_t)L.cnt * sizeof(double), st);
-    case K_SCATTER:
-      return launch_scatterA(st, L.cnt, h->Alev_ent.p + L.off, h->Adest.p, h->Arow.p, h->A.p, h->Rs.p,
-                             h->store.p, h->scratch.p);
     case K_EXTADD:
-      return launch_extend_add(st, L.cnt, h->xcols.p + L.off, h->xtasks.p, h->sn.p, h->relmap.p,
-                               h->store.p, h->scratch.p);
+      return launch_assemble(st, L.cnt, h->xcols.p + L.off, h->xtasks.p, h->aents.p, h->sn.p, h->relmap.p,
+                             h->A.p, h->Arow.p, h->Rs.p, h->store.p, h->scratch.p);
     case K_FRONT_LDS:
       return launch_front_lds(st, (int)L.cnt, (int)L.aux, h->ilist.p + L.off, h->sn.p, h->store.p,
                               h->scratch.p, h->rowperm.p, h->info.p, h->growth.p, diag_tol, piv_tol);
@@ -1312,6 +1337,7 @@ static void release_schedule(smlu_handle* h) {
   h->sn.free();
   h->ilist.free();
   h->xtasks.free();
+  h->aents.free();
   h->ftiles.free();
   h->gtasks.free();
   h->stasks.free();
