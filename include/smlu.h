@@ -183,36 +183,66 @@ int  smlu_plan_supernodes(const smlu_plan* plan, int64_t* first, int64_t* parent
 void smlu_plan_destroy(smlu_plan* plan);
 
 /* ---- multi-GPU partition ---------------------------------------------------
- * One process per GPU.  The assembly tree is split by proportional mapping: each rank factors
- * its subtrees with no communication; a front whose child lives on another rank receives that
- * child's update block right before its level ("exchange point").  The library runs the
- * segments between exchange points on its own stream; the caller moves the packed blocks
- * between ranks (RCCL point-to-point over xGMI in the Python mirror, smlu/dist.py).  This
- * replaces the reference's MPI shared-memory column split (src/SharedMemSparseLU.jl:101-160
- * distributes dense chunks over ranks).
+ * One process per GPU; every rank calls the same functions with the same matrix (collective).
+ * The assembly tree is split by proportional mapping: subtrees are bin-packed onto ranks and
+ * factored with no communication; each front above them is shared by the ranks owning its
+ * subtrees as a 1D block-cyclic column partition (blocks of 384 columns): the owner of a pivot
+ * block factors it and broadcasts it (L block, pivots, tile inverses) to the group, every
+ * member updates the column blocks it owns; the children's F22 columns move to the owners of
+ * the parent's columns before its assembly.  Each rank allocates only its own fronts and
+ * blocks.  Solves run the same partition (vector segments passed along the block owners, the
+ * solution rows of each level shared); x comes out complete on every rank.  This replaces the
+ * reference's MPI shared-memory column split (src/SharedMemSparseLU.jl:101-160, the rank split
+ * intended at :107, :128).
  *
- * Factor:  smlu_dist_set_values; for seg in 0..nseg-1: (seg > 0: exchange kind 0 before seg)
- *          smlu_dist_factor_segment(seg).  The last segment returns the pivot status.
- * Solve:   forward  segments (phase 0, exchange kind 1 before seg > 0; seg 0 reads b),
- *          backward segments (phase 1, exchange kind 2 before seg > 0),
- *          phase 2 writes this rank's rows of x (others 0); the caller sums x over ranks.
- * Exchange (kind, seg): smlu_dist_xsizes gives per-peer send/recv counts (doubles);
- *          smlu_dist_pack fills a device buffer with the outgoing blocks in destination-rank
- *          order (kind 2: this rank's rows once, sent to every peer); smlu_dist_unpack takes
- *          the incoming blocks concatenated in source-rank order. */
-int     smlu_dist_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
-                         const smlu_opts* opts, int32_t rank, int32_t nranks, smlu_handle** out);
-int64_t smlu_dist_nsegments(const smlu_handle* h);
-int     smlu_dist_set_values(smlu_handle* h, const double* nzval, int32_t on_device);
-int     smlu_dist_factor_segment(smlu_handle* h, int32_t seg);
-int     smlu_dist_solve_segment(smlu_handle* h, const double* d_b, double* d_x, int32_t phase, int32_t seg);
-int     smlu_dist_xsizes(smlu_handle* h, int32_t kind, int32_t seg, int64_t* send, int64_t* recv);
-int     smlu_dist_pack(smlu_handle* h, int32_t kind, int32_t seg, double* d_buf);
-int     smlu_dist_unpack(smlu_handle* h, int32_t kind, int32_t seg, const double* d_buf);
-/* Host-only: the partition a dist handle of `nparts` ranks would use (owner per supernode,
- * exchange-point levels); NULL outputs are skipped. */
-int     smlu_plan_partition(const smlu_plan* plan, int32_t nparts, int32_t* owner, int32_t* xlevels,
-                            int64_t* nx);
+ * After creation a partitioned handle takes the ordinary entry points (smlu_refactor[_device],
+ * smlu_solve[_device], smlu_solve_multi*, smlu_stat); all ranks must call them together.
+ * smlu_get_factors, the chunked layout and smlu_refactor_csc are single-GPU only. */
+
+/* Transport between the ranks, supplied by the caller (or the built-in RCCL one below).
+ * device_memory = 1: buffers are device pointers ordered on `stream` (a hipStream_t), the
+ * callbacks enqueue and return (RCCL); 0: host buffers, the library has synchronised its stream
+ * and waits for the callback to complete (host-staged transports such as gloo / MPI).
+ * exchange: for each of the npeer peers, send sbytes[i] bytes from sbuf[i] to peer[i] and
+ *   receive rbytes[i] bytes from it into rbuf[i] (either may be 0); all must complete.
+ * bcast: `bytes` from rank `root` to every rank of `group` (sorted, includes root).
+ * allreduce_max: element-wise max of count doubles over all ranks (host memory).
+ * Return 0 on success. */
+typedef struct smlu_transport {
+    void*   ctx;
+    int32_t device_memory;
+    int (*exchange)(void* ctx, int32_t npeer, const int32_t* peer, void* const* sbuf,
+                    const int64_t* sbytes, void* const* rbuf, const int64_t* rbytes, void* stream);
+    int (*bcast)(void* ctx, void* buf, int64_t bytes, int32_t root, int32_t gsize,
+                 const int32_t* group, void* stream);
+    int (*allreduce_max)(void* ctx, double* buf, int32_t count);
+} smlu_transport;
+
+/* ParallelSparseLU(A) on `nranks` GPUs (collective): analysis, this rank's allocation, the
+ * first factorization.  `tr` is copied; its ctx must stay valid for the handle's life. */
+int smlu_dist_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
+                     const smlu_opts* opts, int32_t rank, int32_t nranks, const smlu_transport* tr,
+                     smlu_handle** out);
+
+/* Built-in transport over RCCL (xGMI point-to-point): rank 0 calls smlu_rccl_unique_id and
+ * shares the 128 bytes with the other ranks (MPI_Bcast in the Julia shim, torch.distributed in
+ * the Python mirror); every rank then calls smlu_dist_create_rccl. */
+int smlu_rccl_unique_id(uint8_t id[128]);
+int smlu_dist_create_rccl(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
+                          const smlu_opts* opts, int32_t rank, int32_t nranks, const uint8_t id[128],
+                          smlu_handle** out);
+
+/* Host-only: the partition a handle of `nparts` ranks would use.  owner[s] = rank of front s,
+ * -1 for a front shared by several ranks (its column blocks dealt over its group). */
+int     smlu_plan_partition(const smlu_plan* plan, int32_t nparts, int32_t* owner, int64_t* nshared);
+/* Host-only: device bytes rank `rank` of `nparts` allocates (factor store, scratch arena,
+ * broadcast staging). */
+int     smlu_plan_rank_memory(const smlu_plan* plan, int32_t nparts, int32_t rank, double* store_bytes,
+                              double* scratch_bytes, double* stage_bytes);
+/* Host-only critical-path projection of the partitioned factorization at `tflops` per GPU,
+ * `gbs` GB/s per link and `lat_us` per message: returns the projected seconds, *t1 = one GPU. */
+double  smlu_plan_project(const smlu_plan* plan, int32_t nparts, double tflops, double gbs, double lat_us,
+                          double* t1);
 
 /* Library version string. */
 const char* smlu_version(void);

@@ -47,9 +47,21 @@ struct FrontTile {
 
 // Extend-add task: parent front p's column tj receives cnt child columns, listed as (child,
 // child column) pairs at contrib[off, off+cnt) in child order.
-// Assembly task: column tj of front p.  Child contributions xtasks[off, off+cnt) (child, child
-// F22 column) in child order; A entries aents[aoff, aoff+acnt) as (entry id, local row), rows
-// ascending.
+// Assembly task: column tj of front p.  Child contributions xtasks[off, off+cnt) in child order;
+// A entries aents[aoff, aoff+acnt) as (entry id, local row), rows ascending.
+// One child F22 column contributing to a parent column: the child (its nu and row map) and where
+// the column's nu values are: src >= 0 -> scratch + src, src < 0 -> store + (-1 - src).
+struct XContrib {
+  int32_t child, pad;
+  int64_t src;
+};
+
+// Device-to-device copy of n4 4-byte words (the pack / unpack steps of the multi-GPU exchanges).
+struct SegDesc {
+  uint64_t src, dst;
+  int64_t n4;
+};
+
 struct XCol {
   int32_t p, tj;
   int64_t off;

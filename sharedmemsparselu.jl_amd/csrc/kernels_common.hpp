@@ -76,7 +76,7 @@ __device__ __forceinline__ FrontPtrs front_ptrs(const SNode& s, double* store, d
   f.M = (int64_t)s.ns + s.nu;
   f.L = gbl(store + s.Loff);
   f.U = gbl(store + s.Uoff);
-  f.F = s.Foff >= 0 ? gbl(scratch + s.Foff) : nullptr;
+  f.F = s.nu > 0 ? gbl(scratch + s.Foff) : nullptr;   // Foff may be shifted (block nodes)
   return f;
 }
 

@@ -48,7 +48,7 @@ __global__ void k_fill(int64_t n, double* __restrict__ x, double v) {
 // their start by binary search.
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_assemble(int64_t ntasks, const XCol* __restrict__ cols,
-                                                  const int2* __restrict__ contrib,
+                                                  const XContrib* __restrict__ contrib,
                                                   const int2* __restrict__ aents,
                                                   const SNode* __restrict__ sn,
                                                   const int32_t* __restrict__ relmap,
@@ -90,10 +90,10 @@ __global__ __launch_bounds__(256) void k_assemble(int64_t ntasks, const XCol* __
     }
     wave_lds_sync();
     for (int q = 0; q < t.cnt; ++q) {
-      const int2 ck = contrib[t.off + q];
-      const SNode c = sn[ck.x];
+      const XContrib ck = contrib[t.off + q];
+      const SNode c = sn[ck.child];
       const int64_t nuc = c.nu;
-      const double* src = scratch + c.Foff + (int64_t)ck.y * nuc;
+      const double* src = ck.src >= 0 ? scratch + ck.src : store + (-1 - ck.src);
       const int32_t* rm = relmap + c.rowptr;
       int64_t pos;
       if (q < 64) {
@@ -1088,7 +1088,7 @@ hipError_t launch_fill(hipStream_t st, int64_t n, double* x, double v) {
   k_fill<<<nblk(n, 256), 256, 0, st>>>(n, x, v);
   return hipGetLastError();
 }
-hipError_t launch_assemble(hipStream_t st, int64_t ntasks, const XCol* cols, const int2* contrib,
+hipError_t launch_assemble(hipStream_t st, int64_t ntasks, const XCol* cols, const XContrib* contrib,
                            const int2* aents, const SNode* sn, const int32_t* relmap, const double* a,
                            const int32_t* arow, const double* Rs, double* store, double* scratch) {
   if (ntasks <= 0) return hipSuccess;

@@ -245,6 +245,43 @@ __global__ __launch_bounds__(256) void k_bwd_u12(const FrontTile* __restrict__ f
     vbuf[s.voff + i] = x[s.first + i] - (((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
 }
 
+// ------------------------------------------------------------------------------------
+// Multi-GPU helpers.  k_segcopy: the pack / unpack copies of an exchange, one workgroup per
+// segment (4-byte words).  k_bwd_u12_cols: backward-solve contribution of one update-column
+// block of a shared front, v[i] (-)= sum_{j in [c0, c1)} U[i, j] x[R[j - ns]] for i < ns
+// (U12 rows of the block at U + (j - c0) * ns); init: v[i] = x[first + i] - sum.
+// k_vcopy: v[i] = x[first + i], i < ns (start of the backward chain of a front without U12).
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_segcopy(const SegDesc* __restrict__ d, int64_t nd) {
+  for (int64_t k = blockIdx.x; k < nd; k += gridDim.x) {
+    const SegDesc g = d[k];
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(g.src);
+    uint32_t* t = reinterpret_cast<uint32_t*>(g.dst);
+    for (int64_t i = threadIdx.x; i < g.n4; i += 256) t[i] = s[i];
+  }
+}
+__global__ __launch_bounds__(256) void k_bwd_u12_cols(const SNode* __restrict__ sn, int node, int64_t c0,
+                                                      int64_t c1, int init, const int32_t* __restrict__ rows,
+                                                      const double* __restrict__ store,
+                                                      const double* __restrict__ x, double* __restrict__ vbuf) {
+  const SNode s = sn[node];
+  const int64_t ns = s.ns;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= ns) return;
+  const int32_t* R = rows + s.rowptr;
+  const double* U = store + s.Uoff;
+  double acc = 0.0;
+  for (int64_t j = c0; j < c1; ++j) acc = fma(U[(j - ns) * ns + i], x[R[j - ns]], acc);
+  double* v = vbuf + s.voff;
+  v[i] = (init ? x[s.first + i] : v[i]) - acc;
+}
+__global__ void k_vcopy(const SNode* __restrict__ sn, int node, const double* __restrict__ x,
+                        double* __restrict__ vbuf) {
+  const SNode s = sn[node];
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < s.ns) vbuf[s.voff + i] = x[s.first + i];
+}
+
 // wrk[i] = Rs[p0[i]] * b[p0[i]]
 __global__ void k_perm_in(int64_t n, const int64_t* __restrict__ p0, const double* __restrict__ Rs,
                           const double* __restrict__ b, double* __restrict__ wrk) {
@@ -259,12 +296,6 @@ __global__ void k_perm_out(int64_t n, const int64_t* __restrict__ q, const doubl
                            double* __restrict__ x) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[q[i]] = wrk[i];
-}
-// multi-GPU: x[q[i]] = wrk[i] on the rows this rank owns, 0 elsewhere (summed over ranks)
-__global__ void k_perm_out_masked(int64_t n, const int64_t* __restrict__ q, const int8_t* __restrict__ own,
-                                  const double* __restrict__ wrk, double* __restrict__ x) {
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) x[q[i]] = own[i] ? wrk[i] : 0.0;
 }
 // final order -> pre-swap positions: out[first + rowperm[first+i]] = in[first+i]
 __global__ void k_unswap(int64_t n, const int64_t* __restrict__ pos_first,
@@ -363,10 +394,21 @@ hipError_t launch_perm_in(hipStream_t st, int64_t n, const int64_t* p0, const do
   k_perm_in<<<nblk(n, 256), 256, 0, st>>>(n, p0, Rs, b, wrk);
   return hipGetLastError();
 }
-hipError_t launch_perm_out_masked(hipStream_t st, int64_t n, const int64_t* q, const int8_t* own,
-                                  const double* wrk, double* x) {
-  if (n <= 0) return hipSuccess;
-  k_perm_out_masked<<<nblk(n, 256), 256, 0, st>>>(n, q, own, wrk, x);
+hipError_t launch_segcopy(hipStream_t st, const SegDesc* d, int64_t nd) {
+  if (nd <= 0) return hipSuccess;
+  k_segcopy<<<(unsigned)std::min<int64_t>(nd, 65535), 256, 0, st>>>(d, nd);
+  return hipGetLastError();
+}
+hipError_t launch_bwd_u12_cols(hipStream_t st, const SNode* sn, int node, int64_t ns, int64_t c0, int64_t c1,
+                               int init, const int32_t* rows, const double* store, const double* x,
+                               double* vbuf) {
+  if (ns <= 0) return hipSuccess;
+  k_bwd_u12_cols<<<nblk(ns, 256), 256, 0, st>>>(sn, node, c0, c1, init, rows, store, x, vbuf);
+  return hipGetLastError();
+}
+hipError_t launch_vcopy(hipStream_t st, const SNode* sn, int node, int64_t ns, const double* x, double* vbuf) {
+  if (ns <= 0) return hipSuccess;
+  k_vcopy<<<nblk(ns, 256), 256, 0, st>>>(sn, node, x, vbuf);
   return hipGetLastError();
 }
 // ------------------------------------------------------------------------------------

@@ -631,10 +631,11 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
 // least-loaded rank); a top front goes to the rank of its heaviest child, so the largest
 // update block never crosses GPUs.
 // ---------------------------------------------------------------------------------------
-void Plan::compute_owners(int np) {
+void Plan::compute_owners(int np, int64_t block) {
   nparts = std::max(1, np);
+  dob = std::max<int64_t>(64, (block / 64) * 64);
   owner.assign(nsup, 0);
-  xlevels.clear();
+  group.assign(nsup, std::vector<int32_t>{0});
   if (nparts == 1 || nsup == 0) return;
   std::vector<double> W(front_flops.begin(), front_flops.end());   // subtree work
   for (int64_t s = 0; s < nsup; ++s)
@@ -649,6 +650,7 @@ void Plan::compute_owners(int np) {
       if (W[S[i]] > W[S[bi]]) bi = i;
     return bi;
   };
+  // split the heaviest subtree into its children until every subtree fits the per-rank share
   for (int it = 0; it < 64 * nparts && !S.empty(); ++it) {
     double sub = 0;
     for (auto v : S) sub += W[v];
@@ -660,6 +662,7 @@ void Plan::compute_owners(int np) {
     S.erase(S.begin() + (long)bi);
     for (int64_t e = ch_ptr[v]; e < ch_ptr[v + 1]; ++e) S.push_back(ch_list[e]);
   }
+  // bin-pack the subtrees onto ranks (largest first, least-loaded rank)
   std::sort(S.begin(), S.end(), [&](int64_t a, int64_t b) { return W[a] != W[b] ? W[a] > W[b] : a < b; });
   std::vector<double> load(nparts, 0.0);
   std::vector<int32_t> sub_owner(nsup, -1);
@@ -668,27 +671,181 @@ void Plan::compute_owners(int np) {
     load[r] += W[v];
     sub_owner[v] = r;
   }
-  // subtrees: every front below a subtree root takes the root's rank (parents after children,
-  // so walk from the top down: a front's owner is its parent's unless it is a subtree root)
+  // subtree fronts take their root's rank (parents before children: walk down from the top)
   for (int64_t s = nsup - 1; s >= 0; --s) {
     if (sub_owner[s] >= 0) owner[s] = sub_owner[s];
     else if (!top[s] && s_parent[s] >= 0) owner[s] = owner[s_parent[s]];
   }
-  // top fronts (children before parents): the rank of the heaviest child
+  // top fronts (children before parents): the union of the children's groups
   for (int64_t s = 0; s < nsup; ++s) {
-    if (!top[s]) continue;
-    int64_t best = -1;
+    if (!top[s]) {
+      group[s].assign(1, owner[s]);
+      continue;
+    }
+    std::vector<int32_t> g;
     for (int64_t e = ch_ptr[s]; e < ch_ptr[s + 1]; ++e)
-      if (best < 0 || W[ch_list[e]] > W[best]) best = ch_list[e];
-    owner[s] = best >= 0 ? owner[best] : 0;
+      g.insert(g.end(), group[ch_list[e]].begin(), group[ch_list[e]].end());
+    std::sort(g.begin(), g.end());
+    g.erase(std::unique(g.begin(), g.end()), g.end());
+    group[s] = g;
+    owner[s] = g.size() == 1 ? g[0] : -1;
   }
-  std::vector<char> isx(nlevels, 0);
-  for (int64_t s = 0; s < nsup; ++s) {
-    int64_t pp = s_parent[s];
-    if (pp >= 0 && owner[pp] != owner[s]) isx[s_level[pp]] = 1;
+}
+
+namespace {
+// first-fit allocation of blocks live over level intervals [lo, hi]
+struct LiveAlloc {
+  struct Blk { int64_t off, size; int hi; };
+  std::vector<Blk> live;
+  int64_t peak = 0;
+  void release_before(int l) {
+    live.erase(std::remove_if(live.begin(), live.end(), [&](const Blk& b) { return b.hi < l; }), live.end());
   }
-  for (int l = 0; l < nlevels; ++l)
-    if (isx[l]) xlevels.push_back(l);
+  int64_t take(int64_t size, int hi) {
+    if (size <= 0) return -1;
+    std::sort(live.begin(), live.end(), [](const Blk& a, const Blk& b) { return a.off < b.off; });
+    int64_t pos = 0;
+    for (auto& b : live) {
+      if (b.off - pos >= size) break;
+      pos = std::max(pos, b.off + b.size);
+    }
+    live.push_back({pos, size, hi});
+    peak = std::max(peak, pos + size);
+    return pos;
+  }
+};
+int64_t al16(int64_t x) { return (x + 15) & ~int64_t(15); }
+}  // namespace
+
+void rank_layout(const Plan& P, int r, RankLayout& L) {
+  L = RankLayout();
+  L.rank = r;
+  const int64_t nsup = P.nsup;
+  L.Loff.assign(nsup, -1);
+  L.Uoff.assign(nsup, -1);
+  L.Foff.assign(nsup, -1);
+  L.recv_off.assign(nsup, -1);
+  L.recv_size.assign(nsup, 0);
+  auto member = [&](int64_t s) {
+    return std::binary_search(P.group[s].begin(), P.group[s].end(), (int32_t)r);
+  };
+  // factor store
+  int64_t cur = 0;
+  for (int l = 0; l < P.nlevels; ++l)
+    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+      const int64_t s = P.lev_sup[k];
+      const int64_t a = P.ns(s), m = P.M(s);
+      if (!P.dist(s)) {
+        if (P.owner[s] != r) continue;
+        L.Loff[s] = cur;
+        cur = al16(cur + m * a);
+        L.Uoff[s] = cur;
+        cur = al16(cur + a * P.nu(s));
+        continue;
+      }
+      if (!member(s)) continue;
+      const int64_t nb = P.npblk(s) + P.nublk(s);
+      for (int64_t b = 0; b < nb; ++b) {
+        if (P.blk_owner(s, b) != r) continue;
+        RankLayout::Blk B{(int32_t)s, (int32_t)b, P.blk_c0(s, b), P.blk_c1(s, b), cur, -1};
+        const int64_t w = B.c1 - B.c0;
+        cur = al16(cur + (b < P.npblk(s) ? m : a) * w);
+        L.blocks.push_back(B);
+      }
+      L.stage_size = std::max(L.stage_size, m * P.dob);
+    }
+  L.store_size = cur;
+  // scratch: per level, the F22 rows of this rank's fronts (live until the parents' level) and
+  // the receive areas of its distributed fronts (live at their level)
+  LiveAlloc A;
+  for (int l = 0; l < P.nlevels; ++l) {
+    A.release_before(l);
+    int64_t sz = 0;
+    int hi = -1;
+    std::vector<std::pair<int64_t*, int64_t>> place;   // (slot, offset within the level block)
+    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+      const int64_t s = P.lev_sup[k];
+      const int64_t b = P.nu(s);
+      if (b == 0 || P.s_parent[s] < 0) continue;
+      if (!P.dist(s)) {
+        if (P.owner[s] != r) continue;
+        place.push_back({&L.Foff[s], sz});
+        sz = al16(sz + b * b);
+      } else {
+        if (!member(s)) continue;
+        for (auto& B : L.blocks)
+          if (B.s == s && B.c0 >= P.ns(s)) {
+            place.push_back({&B.foff, sz});
+            sz = al16(sz + b * (B.c1 - B.c0));
+          }
+      }
+      hi = std::max(hi, (int)P.s_level[P.s_parent[s]]);
+    }
+    if (sz > 0) {
+      const int64_t base = A.take(sz, hi);
+      for (auto& pl : place) *pl.first = base + pl.second;
+    }
+    // receive areas of the distributed fronts at this level
+    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+      const int64_t t = P.lev_sup[k];
+      if (!P.dist(t) || !member(t)) continue;
+      int64_t need = 0;
+      for (int64_t e = P.ch_ptr[t]; e < P.ch_ptr[t + 1]; ++e) {
+        const int64_t c = P.ch_list[e];
+        const int64_t nuc = P.nu(c);
+        const int32_t* rm = P.relmap.data() + P.s_rowptr[c];
+        for (int64_t jc = 0; jc < nuc; ++jc)
+          if (P.col_owner(t, rm[jc]) == r && P.col_owner(c, P.ns(c) + jc) != r) need += nuc;
+      }
+      L.recv_size[t] = need;
+      if (need > 0) L.recv_off[t] = A.take(al16(need), l);
+    }
+  }
+  L.scratch_size = A.peak;
+}
+
+double project_partition(const Plan& P, double tflops, double gbs, double lat_us, double* t1_out) {
+  const double rate = tflops * 1e12, bw = gbs * 1e9, lat = lat_us * 1e-6;
+  const double step_lat = 80e-6;   // latency of one 64-column panel step (panel, inverses, TRSM)
+  auto panel_chain = [&](int64_t s) { return P.ns(s) > 128 ? step_lat * (double)((P.ns(s) + 63) / 64) : 0.0; };
+  double t1 = 0;
+  for (int64_t s = 0; s < P.nsup; ++s) t1 += P.front_flops[s] / rate + panel_chain(s);
+  if (t1_out) *t1_out = t1;
+  std::vector<double> clk(P.nparts, 0.0);
+  for (int l = 0; l < P.nlevels; ++l)
+    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+      const int64_t s = P.lev_sup[k];
+      if (!P.dist(s)) {
+        clk[P.owner[s]] += P.front_flops[s] / rate + panel_chain(s);
+        continue;
+      }
+      const auto& G = P.group[s];
+      double t = 0;
+      for (int r : G) t = std::max(t, clk[r]);
+      // children's F22 columns: each column to its owner (about all of them cross ranks)
+      double xbytes = 0;
+      for (int64_t e = P.ch_ptr[s]; e < P.ch_ptr[s + 1]; ++e)
+        xbytes += 8.0 * (double)P.nu(P.ch_list[e]) * (double)P.nu(P.ch_list[e]);
+      t += lat + xbytes / G.size() / bw;
+      const double M = (double)P.M(s), ns = (double)P.ns(s);
+      const int64_t np = P.npblk(s), nb = np + P.nublk(s);
+      for (int64_t b = 0; b < np; ++b) {
+        const double c0 = (double)P.blk_c0(s, b), c1 = (double)P.blk_c1(s, b), w = c1 - c0;
+        double inner = 2.0 * (M - c0) * w * w / rate + step_lat * std::ceil(w / 64.0);
+        double bc = lat + 8.0 * (M - c0) * w / bw;
+        double trail = 0;
+        for (int r : G) {   // trailing update of r's blocks right of this one
+          double cols = 0;
+          for (int64_t bb = b + 1; bb < nb; ++bb)
+            if (P.blk_owner(s, bb) == r) cols += (double)(P.blk_c1(s, bb) - P.blk_c0(s, bb));
+          trail = std::max(trail, 2.0 * (M - c0) * w * cols / rate);
+        }
+        t += inner + bc + trail;
+        (void)ns;
+      }
+      for (int r : G) clk[r] = t;
+    }
+  return *std::max_element(clk.begin(), clk.end());
 }
 
 }  // namespace smlu

@@ -10,6 +10,7 @@
 //   -> HBM layout of factor panels and the scratch arena for update (F22) blocks
 //   -> map of every A entry to its slot in a front.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <string>
 #include <vector>
@@ -104,15 +105,36 @@ struct Plan {
   double analysis_ms = 0;
 
   // ---- multi-GPU partition (compute_owners) ----
-  // owner[s] = rank that factors front s.  Proportional mapping of the assembly tree: a
-  // subtree whose rank set has one member is owned by it entirely; a front above that keeps
-  // the first rank of its set.  Exchange points are the levels of fronts with a child owned
-  // by another rank (the child's update block crosses GPUs right before that level).
+  // Subtrees of the assembly tree are bin-packed onto ranks (each factored with no
+  // communication).  A front above them ("top" front) is shared by the group of ranks that own
+  // its subtrees: its columns are split into blocks of `dob` columns dealt round-robin over the
+  // group (pivot blocks first, then the update-column blocks), a 1D block-cyclic column
+  // partition of the dense front.  A front whose group has one rank is an ordinary front of
+  // that rank.
   int nparts = 1;
-  std::vector<int32_t> owner;
-  std::vector<int32_t> xlevels;               // sorted exchange-point levels
+  int64_t dob = 384;                          // column block of the distributed fronts
+  std::vector<int32_t> owner;                 // rank of an ordinary front, -1 for a distributed one
+  std::vector<std::vector<int32_t>> group;    // per front: sorted ranks (size 1: ordinary)
   std::vector<double> front_flops;            // per front (same formula as `flops`)
-  void compute_owners(int nparts);
+  void compute_owners(int nparts, int64_t block = 384);
+  bool dist(int64_t s) const { return !group.empty() && group[s].size() > 1; }
+  int64_t npblk(int64_t s) const { return (ns(s) + dob - 1) / dob; }
+  int64_t nublk(int64_t s) const { return (nu(s) + dob - 1) / dob; }
+  // owner of column block b of front s (b < npblk: pivot columns [b*dob, ..), else update
+  // columns [ns + (b - npblk)*dob, ..))
+  int32_t blk_owner(int64_t s, int64_t b) const { return group[s][b % group[s].size()]; }
+  int64_t blk_c0(int64_t s, int64_t b) const {
+    const int64_t np = npblk(s);
+    return b < np ? b * dob : ns(s) + (b - np) * dob;
+  }
+  int64_t blk_c1(int64_t s, int64_t b) const {
+    const int64_t np = npblk(s);
+    return b < np ? std::min(ns(s), (b + 1) * dob) : std::min(M(s), ns(s) + (b - np + 1) * dob);
+  }
+  int32_t col_owner(int64_t s, int64_t c) const {
+    if (!dist(s)) return owner[s];
+    return c < ns(s) ? blk_owner(s, c / dob) : blk_owner(s, npblk(s) + (c - ns(s)) / dob);
+  }
 
   std::string build(int64_t n, const int64_t* colptr, const int64_t* rowval, int index_base,
                     const PlanOptions& opt, const int64_t* pgiven = nullptr,
@@ -124,5 +146,32 @@ struct Plan {
   // local index of global (new) position g inside front s, or -1
   int64_t local_index(int64_t s, int64_t g) const;
 };
+
+// Device memory layout of one rank (units: doubles).  Ordinary fronts of the rank: L panel and
+// U12 in the factor store, F22 in the scratch arena (first-fit by liveness, live until the
+// parent's level).  Distributed fronts: per owned column block, pivot blocks as M x w
+// full-height L columns in the store; update blocks as their U12 rows (ns x w) in the store
+// and F22 rows (nu x w) in the scratch arena; plus a receive area per distributed front for
+// the children's F22 columns arriving from other ranks (live at the front's level only).
+struct RankLayout {
+  int rank = 0;
+  std::vector<int64_t> Loff, Uoff, Foff;      // ordinary fronts of this rank (-1 elsewhere)
+  struct Blk {
+    int32_t s;          // front
+    int32_t b;          // block index (pivot blocks first)
+    int64_t c0, c1;     // columns
+    int64_t loff;       // pivot block: L columns (ld M); update block: U12 rows (ld ns)
+    int64_t foff;       // update block: F22 rows (ld nu) in scratch, -1 otherwise
+  };
+  std::vector<Blk> blocks;                    // owned blocks of distributed fronts
+  std::vector<int64_t> recv_off, recv_size;   // per front: receive area for child F22 columns
+  int64_t store_size = 0, scratch_size = 0;
+  int64_t stage_size = 0;                     // largest block broadcast (doubles)
+};
+void rank_layout(const Plan& P, int rank, RankLayout& out);
+// Critical-path projection of the partitioned factorization (host model): per front, the
+// flops of its work per rank at `tflops`, the block broadcasts and child F22 exchanges at
+// `gbs` GB/s and `lat_us` per message; returns the projected time (s) and the one-GPU time.
+double project_partition(const Plan& P, double tflops, double gbs, double lat_us, double* t1);
 
 }  // namespace smlu

@@ -8,7 +8,9 @@
 //   lsolve!(F, x) / rsolve!(F, x)    :349-392 -> smlu_lsolve / smlu_rsolve
 //   F.L, F.U, F.p, F.q, F.Rs         :45-52   -> smlu_get_factors
 //   cleanup_ParallelSparseLU!        :31      -> smlu_destroy
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
@@ -30,7 +32,7 @@
 namespace smlu {
 hipError_t launch_rowscale(hipStream_t, int64_t, const int64_t*, const int32_t*, const double*, double*);
 hipError_t launch_fill(hipStream_t, int64_t, double*, double);
-hipError_t launch_assemble(hipStream_t, int64_t, const XCol*, const int2*, const int2*, const SNode*,
+hipError_t launch_assemble(hipStream_t, int64_t, const XCol*, const XContrib*, const int2*, const SNode*,
                            const int32_t*, const double*, const int32_t*, const double*, double*, double*);
 hipError_t launch_front_lds(hipStream_t, int, int, const int32_t*, const SNode*, double*, double*,
                             int32_t*, int32_t*, double*, double, double);
@@ -62,7 +64,10 @@ hipError_t launch_axpy1(hipStream_t, int64_t, const double*, double*);
 hipError_t launch_perm_in(hipStream_t, int64_t, const int64_t*, const double*, const double*, double*);
 hipError_t launch_perm_out(hipStream_t, int64_t, const int64_t*, const double*, double*);
 hipError_t launch_chunked_solve(hipStream_t, bool, int64_t, const ChunkDesc*, const double*, double*);
-hipError_t launch_perm_out_masked(hipStream_t, int64_t, const int64_t*, const int8_t*, const double*, double*);
+hipError_t launch_segcopy(hipStream_t, const SegDesc*, int64_t);
+hipError_t launch_bwd_u12_cols(hipStream_t, const SNode*, int, int64_t, int64_t, int64_t, int, const int32_t*,
+                               const double*, const double*, double*);
+hipError_t launch_vcopy(hipStream_t, const SNode*, int, int64_t, const double*, double*);
 hipError_t launch_unswap(hipStream_t, int64_t, const int64_t*, const int32_t*, const double*, double*);
 }  // namespace smlu
 
@@ -82,15 +87,16 @@ thread_local std::string g_last_error;
 enum Kind : int {
   K_MEMSET_STORE, K_MEMSET_SCRATCH, K_SCATTER, K_EXTADD, K_FRONT_LDS, K_PANEL, K_TRSMU, K_TRSML,
   K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_GEMM22, K_LASWP, K_STEPTRSM, K_GEMMU,
-  K_GEMMO, K_FORK, K_JOIN, K_TRIINV, K_NKIND
+  K_GEMMO, K_FORK, K_JOIN, K_TRIINV, K_BWDU12C, K_VCOPY, K_NKIND
 };
 const char* kKindName[K_NKIND] = {"memset", "memset", "assemble", "assemble", "small", "panel",
                                   "trsm", "trsm", "gemm", "solve", "solve", "solve", "solve",
-                                  "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "sync", "sync", "trsm"};
+                                  "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "sync", "sync", "trsm", "solve", "solve"};
 constexpr int kSolveBigNs = 256;  // fronts with more pivots use the multi-workgroup solve
 
 struct Launch {
   int kind = 0;
+  int node = 0;                           // K_BWDU12C / K_VCOPY: front or block node
   int step = 0;
   int64_t off = 0, cnt = 0, nwg = 0, aux = 0, aux2 = 0;
   int64_t off2 = 0, cnt2 = 0, nwg2 = 0;   // second work list (merged launches)
@@ -118,6 +124,132 @@ struct DBuf {
     n = 0;
   }
 };
+
+// Host description of one copy of a pack / unpack step, resolved to device addresses once the
+// buffers exist: base 0 store, 1 scratch, 2 vbuf, 3 wrk (x), 4 send staging, 5 receive staging,
+// 6 broadcast block buffer, 7 tile inverses, 8 swap lists, 9 rowperm; offsets in bytes.
+struct HSeg {
+  int sb;
+  int64_t so;
+  int db;
+  int64_t dof;
+  int64_t bytes;
+};
+
+// One communication step between segments of the schedule.
+struct CommOp {
+  int type = 0;                          // 0: exchange with peers, 1: broadcast within a group
+  std::vector<int32_t> peer;             // exchange: peers (ascending)
+  std::vector<int> sbase, rbase;         // per peer: buffer (HSeg base ids) and byte offsets
+  std::vector<int64_t> soff, roff, sbytes, rbytes;
+  int32_t root = -1;                     // broadcast: root and group (ascending, includes root)
+  std::vector<int32_t> grp;
+  int bbase = 4;                         // broadcast buffer: send staging on the root, the
+  int64_t bytes = 0;                     //   block buffer elsewhere
+  std::vector<HSeg> pack, unpack;        // copies before / after the transfer
+  int64_t pack0 = 0, unpack0 = 0;        // ranges in the device descriptor array
+  // per-peer helpers used while the schedule is built
+  int at(int32_t p) {
+    for (size_t i = 0; i < peer.size(); ++i)
+      if (peer[i] == p) return (int)i;
+    peer.push_back(p);
+    sbase.push_back(4);
+    rbase.push_back(5);
+    soff.push_back(0);
+    roff.push_back(0);
+    sbytes.push_back(0);
+    rbytes.push_back(0);
+    return (int)peer.size() - 1;
+  }
+};
+
+// ---- built-in RCCL transport (librccl loaded at run time: the library itself needs RCCL only
+// when a caller asks for it) ------------------------------------------------------------------
+struct RcclApi {
+  void* lib = nullptr;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*);
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int);
+  ncclResult_t (*CommDestroy)(ncclComm_t);
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+  ncclResult_t (*GroupStart)();
+  ncclResult_t (*GroupEnd)();
+  ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+};
+
+RcclApi* rccl_api() {
+  static RcclApi api;
+  static bool tried = false;
+  if (tried) return api.lib ? &api : nullptr;
+  tried = true;
+  void* l = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!l) l = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+  if (!l) return nullptr;
+  bool ok = true;
+  auto sym = [&](const char* n) {
+    void* f = dlsym(l, n);
+    ok = ok && f != nullptr;
+    return f;
+  };
+  api.GetUniqueId = (decltype(api.GetUniqueId))sym("ncclGetUniqueId");
+  api.CommInitRank = (decltype(api.CommInitRank))sym("ncclCommInitRank");
+  api.CommDestroy = (decltype(api.CommDestroy))sym("ncclCommDestroy");
+  api.Send = (decltype(api.Send))sym("ncclSend");
+  api.Recv = (decltype(api.Recv))sym("ncclRecv");
+  api.GroupStart = (decltype(api.GroupStart))sym("ncclGroupStart");
+  api.GroupEnd = (decltype(api.GroupEnd))sym("ncclGroupEnd");
+  api.AllReduce = (decltype(api.AllReduce))sym("ncclAllReduce");
+  if (!ok) return nullptr;
+  api.lib = l;
+  return &api;
+}
+
+struct RcclState {
+  ncclComm_t comm = nullptr;
+  int rank = 0;
+  hipStream_t stream = nullptr;   // the handle's stream (allreduce)
+  double* dbuf = nullptr;         // device scratch for the allreduce
+};
+
+// point-to-point batch over xGMI: sends and receives of all peers in one group
+int rccl_exchange(void* ctx, int32_t npeer, const int32_t* peer, void* const* sbuf, const int64_t* sbytes,
+                  void* const* rbuf, const int64_t* rbytes, void* stream) {
+  RcclApi* R = rccl_api();
+  auto* S = static_cast<RcclState*>(ctx);
+  hipStream_t st = (hipStream_t)stream;
+  if (R->GroupStart() != ncclSuccess) return 1;
+  for (int32_t i = 0; i < npeer; ++i) {
+    if (sbytes[i] > 0 && R->Send(sbuf[i], (size_t)sbytes[i], ncclUint8, peer[i], S->comm, st) != ncclSuccess) return 2;
+    if (rbytes[i] > 0 && R->Recv(rbuf[i], (size_t)rbytes[i], ncclUint8, peer[i], S->comm, st) != ncclSuccess) return 3;
+  }
+  return R->GroupEnd() == ncclSuccess ? 0 : 4;
+}
+
+// broadcast inside a rank group as root -> member sends (the group is a subset of the ranks)
+int rccl_bcast(void* ctx, void* buf, int64_t bytes, int32_t root, int32_t gsize, const int32_t* group, void* stream) {
+  RcclApi* R = rccl_api();
+  auto* S = static_cast<RcclState*>(ctx);
+  hipStream_t st = (hipStream_t)stream;
+  if (bytes <= 0) return 0;
+  if (R->GroupStart() != ncclSuccess) return 1;
+  if (S->rank == root) {
+    for (int32_t i = 0; i < gsize; ++i)
+      if (group[i] != root && R->Send(buf, (size_t)bytes, ncclUint8, group[i], S->comm, st) != ncclSuccess) return 2;
+  } else if (R->Recv(buf, (size_t)bytes, ncclUint8, root, S->comm, st) != ncclSuccess) {
+    return 3;
+  }
+  return R->GroupEnd() == ncclSuccess ? 0 : 4;
+}
+
+int rccl_allreduce_max(void* ctx, double* buf, int32_t count) {
+  RcclApi* R = rccl_api();
+  auto* S = static_cast<RcclState*>(ctx);
+  if (count > 8) return 1;
+  if (hipMemcpyAsync(S->dbuf, buf, sizeof(double) * count, hipMemcpyHostToDevice, S->stream) != hipSuccess) return 2;
+  if (R->AllReduce(S->dbuf, S->dbuf, (size_t)count, ncclFloat64, ncclMax, S->comm, S->stream) != ncclSuccess) return 3;
+  if (hipMemcpyAsync(buf, S->dbuf, sizeof(double) * count, hipMemcpyDeviceToHost, S->stream) != hipSuccess) return 4;
+  return hipStreamSynchronize(S->stream) == hipSuccess ? 0 : 5;
+}
 
 }  // namespace
 
@@ -152,7 +284,8 @@ struct smlu_handle {
   DBuf<int64_t> Arowptr, p0, q, posfirst;
   DBuf<int32_t> Arow_ent, Arow, rows, relmap, chlist, ilist, rowperm, rowperm0, info, swaps;
   DBuf<SNode> sn;
-  DBuf<int2> xtasks, aents;
+  DBuf<XContrib> xtasks;
+  DBuf<int2> aents;
   DBuf<FrontTile> ftiles;
   DBuf<GemmTask> gtasks;
   DBuf<SwapTask> stasks;
@@ -175,13 +308,22 @@ struct smlu_handle {
   std::vector<hipGraphExec_t> fac_execs;   // one captured graph per factor segment
   int fac_exec_profile = -1;
   std::vector<std::pair<size_t, size_t>> seg_events;   // profile events of each captured segment
-  // multi-GPU partition (smlu_dist_*): this rank's fronts, segments between exchange points
+  // multi-GPU partition (smlu_dist_*): this rank's fronts and column blocks (RankLayout), the
+  // schedule cut into segments at the communication steps
   int rank = 0, nranks = 1;
+  RankLayout lay;
+  int64_t nnodes = 0;                              // fronts + block nodes of shared fronts
+  std::vector<int32_t> node_front;                 // node -> front
   std::vector<size_t> fac_seg, fwd_seg, bwd_seg;   // launch index where each segment starts
-  struct XBlk { int32_t src, dst; int64_t off, cnt; };
-  std::vector<std::vector<XBlk>> xfac, xfwd;       // per exchange point: child F22 / vbuf blocks
-  std::vector<std::vector<std::vector<std::pair<int64_t, int64_t>>>> xbwd;   // [point][rank] x rows
-  DBuf<int8_t> rowown;
+  std::vector<int> fac_comm, fwd_comm, bwd_comm;   // comm op run before segment k >= 1
+  std::vector<CommOp> comm;
+  smlu_transport tr{};
+  void* rccl = nullptr;                            // built-in RCCL transport state
+  DBuf<double> stage_s, stage_r, bcbuf, d_red;
+  DBuf<SegDesc> segdesc;
+  char* hstage_s = nullptr;                        // pinned host staging (host-memory transports)
+  char* hstage_r = nullptr;
+  int64_t stage_bytes_s = 0, stage_bytes_r = 0;
   size_t fac_graph_events = 0;
   bool graph_failed = false;
   bool lookahead = false;     // SMLU_LOOKAHEAD=1: trailing updates beyond the next block on a side stream
@@ -219,7 +361,14 @@ struct smlu_handle {
     gtasks.free();
     stasks.free();
     xcols.free();
-    rowown.free();
+    stage_s.free();
+    stage_r.free();
+    bcbuf.free();
+    segdesc.free();
+    d_red.free();
+    if (hstage_s) (void)hipHostFree(hstage_s);
+    if (hstage_r) (void)hipHostFree(hstage_r);
+    hstage_s = hstage_r = nullptr;
   }
   void release_graphs() {
     for (auto& g : fac_execs)
@@ -232,6 +381,11 @@ struct smlu_handle {
   void release_all() {
     release_graphs();
     release_buffers();
+    if (rccl) {
+      if (RcclApi* R = rccl_api()) (void)R->CommDestroy(static_cast<RcclState*>(rccl)->comm);
+      delete static_cast<RcclState*>(rccl);
+      rccl = nullptr;
+    }
     for (auto& e : ev_pool) {
       (void)hipEventDestroy(e.first);
       (void)hipEventDestroy(e.second);
@@ -308,7 +462,11 @@ static int build_schedule(smlu_handle* h) {
   Plan& P = h->plan;
   const int64_t nsup = P.nsup;
   hipStream_t st = h->stream;
-  // supernode records
+  // supernode records: fronts [0, nsup) with this rank's offsets (RankLayout); a shared front
+  // (multi-GPU) keeps a front node for its solves and the row maps, plus one block node per
+  // owned column block whose offsets are shifted so that the front's column c of the block sits
+  // at the usual place (pivot block: L + c*M; update block: U + (c-ns)*ns, F + (c-ns)*nu)
+  const RankLayout& Y = h->lay;
   h->hsn.resize(nsup);
   int64_t voff = 0;
   // Largest ns factored with full-candidate pivoting.  A diagonally dominant matrix needs no
@@ -322,9 +480,9 @@ static int build_schedule(smlu_handle* h) {
   for (int64_t s = 0; s < nsup; ++s) {
     SNode r{};
     r.first = P.s_first[s];
-    r.Loff = P.Loff[s];
-    r.Uoff = P.Uoff[s];
-    r.Foff = P.Foff[s];
+    r.Loff = Y.Loff[s] >= 0 ? Y.Loff[s] : 0;
+    r.Uoff = Y.Uoff[s] >= 0 ? Y.Uoff[s] : 0;
+    r.Foff = Y.Foff[s];
     r.rowptr = P.s_rowptr[s];
     r.voff = voff;
     r.ns = (int32_t)P.ns(s);
@@ -339,12 +497,33 @@ static int build_schedule(smlu_handle* h) {
     r.chbeg = (int32_t)P.ch_ptr[s];
     r.chend = (int32_t)P.ch_ptr[s + 1];
     r.level = P.s_level[s];
+    if (h->nranks > 1 && P.dist(s)) { r.mode = 2; r.nb = kNbTile; }   // shared fronts: diagonal-tile pivoting
     h->hsn[s] = r;
   }
+  h->node_front.resize(nsup);
+  for (int64_t s = 0; s < nsup; ++s) h->node_front[s] = (int32_t)s;
+  std::vector<int32_t> blknode(Y.blocks.size());
+  std::unordered_map<int64_t, int32_t> blkmap;   // (front, block) -> index in Y.blocks
+  for (size_t i = 0; i < Y.blocks.size(); ++i) {
+    const RankLayout::Blk& B = Y.blocks[i];
+    SNode r = h->hsn[B.s];
+    const int64_t ns = r.ns, nu = r.nu, M = ns + nu;
+    if (B.c0 < ns) {
+      r.Loff = B.loff - B.c0 * M;
+    } else {
+      r.Uoff = B.loff - (B.c0 - ns) * ns;
+      r.Foff = B.foff - (B.c0 - ns) * nu;
+    }
+    blknode[i] = (int32_t)h->hsn.size();
+    blkmap[(int64_t)B.s * 1048576 + B.b] = (int32_t)i;
+    h->hsn.push_back(r);
+    h->node_front.push_back(B.s);
+  }
+  h->nnodes = (int64_t)h->hsn.size();
   // given (p,q): no pivoting on top of the caller's order -> tile mode pivots only if the
   // diagonal is exactly zero; we force diag preference by a tiny diag tolerance at launch.
   std::vector<int32_t> ilist;
-  std::vector<int2> xt;
+  std::vector<XContrib> xt;
   std::vector<FrontTile> ft;
   std::vector<GemmTask> gt;
   std::vector<SwapTask> st_tasks;
@@ -369,17 +548,50 @@ static int build_schedule(smlu_handle* h) {
   // this rank's fronts by level (every front when nranks == 1)
   std::vector<int64_t> LP(P.nlevels + 1, 0);
   std::vector<int32_t> LS;
+  std::vector<std::vector<int32_t>> dfront(P.nlevels);   // shared fronts this rank works on, per level
+  std::vector<char> dlevel(P.nlevels, 0);          // a level holding any shared front (any rank)
   for (int l = 0; l < P.nlevels; ++l) {
-    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k)
-      if (h->nranks == 1 || P.owner[P.lev_sup[k]] == h->rank) LS.push_back(P.lev_sup[k]);
+    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+      const int64_t s = P.lev_sup[k];
+      if (h->nranks == 1) { LS.push_back((int32_t)s); continue; }
+      if (!P.dist(s)) {
+        if (P.owner[s] == h->rank) LS.push_back((int32_t)s);
+        continue;
+      }
+      dlevel[l] = 1;
+      if (std::binary_search(P.group[s].begin(), P.group[s].end(), h->rank)) dfront[l].push_back((int32_t)s);
+    }
     LP[l + 1] = (int64_t)LS.size();
   }
-  std::vector<char> isx(P.nlevels, 0);
-  if (h->nranks > 1)
-    for (auto l : P.xlevels) isx[l] = 1;
   h->fac_seg.assign(1, 0);
   h->fwd_seg.assign(1, 0);
   h->bwd_seg.assign(1, 0);
+  h->fac_comm.clear();
+  h->fwd_comm.clear();
+  h->bwd_comm.clear();
+  h->comm.clear();
+  // a communication step ends the current segment of `seq`
+  auto add_comm = [&](std::vector<Launch>& seq, std::vector<size_t>& seg, std::vector<int>& cm, CommOp&& op) {
+    seg.push_back(seq.size());
+    cm.push_back((int)h->comm.size());
+    h->comm.push_back(std::move(op));
+  };
+  const int dist_slots = h->nranks > 1 ? h->ob / 32 : 0;   // swap / tile-inverse slots of the shared front
+  // where child column jc of c lives: (rank, scratch offset on that rank if it is this rank)
+  auto child_col = [&](int64_t c, int64_t jc, int64_t* src) -> int32_t {
+    const int64_t nuc = P.nu(c);
+    if (!P.dist(c)) {
+      if (src && P.owner[c] == h->rank) *src = Y.Foff[c] + jc * nuc;
+      return P.owner[c];
+    }
+    const int64_t b = P.npblk(c) + jc / P.dob;
+    const int32_t o = P.blk_owner(c, b);
+    if (src && o == h->rank) {
+      const RankLayout::Blk& B = Y.blocks[blkmap.at((int64_t)c * 1048576 + b)];
+      *src = B.foff + (P.ns(c) + jc - B.c0) * nuc;
+    }
+    return o;
+  };
   h->lookahead = std::getenv("SMLU_LOOKAHEAD") != nullptr;
   if (const char* e = std::getenv("SMLU_SIDE_WG")) h->side_wg = std::atoll(e);
   if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
@@ -446,7 +658,62 @@ static int build_schedule(smlu_handle* h) {
   auto tinv_slot_off = [](int64_t slot, bool upper) { return slot * 8192 + (upper ? 4096 : 0); };
   for (int l = 0; l < P.nlevels; ++l) {
     Launch L;
-    if (isx[l]) h->fac_seg.push_back(h->fac.size());   // exchange point before this level
+    // (shared fronts of this level, in front order on every rank)
+    // shared front: the children's F22 columns move to the owners of the target columns; a
+    // rank receives them into its receive area ordered by (source rank, child, column)
+    std::unordered_map<int64_t, int64_t> recv_at;   // (child, column) -> scratch offset
+    for (const int32_t t : dfront[l]) {
+      CommOp op;
+      std::vector<std::vector<std::pair<int64_t, int64_t>>> from(h->nranks);   // per source: (c, jc)
+      for (int64_t e = P.ch_ptr[t]; e < P.ch_ptr[t + 1]; ++e) {
+        const int64_t c = P.ch_list[e];
+        const int32_t* rm = P.relmap.data() + P.s_rowptr[c];
+        const int64_t nuc = P.nu(c);
+        for (int64_t jc = 0; jc < nuc; ++jc) {
+          const int32_t dst = P.col_owner(t, rm[jc]);
+          int64_t src = -1;
+          const int32_t o = child_col(c, jc, &src);
+          if (o == dst) continue;
+          if (o == h->rank) {            // send: pack into the staging buffer
+            const int pi = op.at(dst);
+            op.pack.push_back(HSeg{1, 8 * src, 4, 0, 8 * nuc});   // staging offset fixed below
+            op.pack.back().db = 1000 + pi;                           // peer marker
+            op.sbytes[pi] += 8 * nuc;
+          } else if (dst == h->rank) {
+            from[o].push_back({c, jc});
+          }
+        }
+      }
+      int64_t ro = Y.recv_off[t];
+      for (int32_t o = 0; o < h->nranks; ++o) {
+        if (from[o].empty()) continue;
+        const int pi = op.at(o);
+        op.rbase[pi] = 1;
+        op.roff[pi] = 8 * ro;
+        for (auto& cj : from[o]) {
+          recv_at[cj.first * 1048576 + cj.second] = ro;
+          ro += P.nu(cj.first);
+          op.rbytes[pi] += 8 * P.nu(cj.first);
+        }
+      }
+      // send staging offsets: per peer contiguous, in (child, column) order
+      {
+        std::vector<int64_t> base(op.peer.size(), 0);
+        int64_t acc = 0;
+        for (size_t i = 0; i < op.peer.size(); ++i) {
+          op.soff[i] = acc;
+          base[i] = acc;
+          acc += op.sbytes[i];
+        }
+        for (auto& g : op.pack) {
+          const int pi = g.db - 1000;
+          g.db = 4;
+          g.dof = base[pi];
+          base[pi] += g.bytes;
+        }
+      }
+      add_comm(h->fac, h->fac_seg, h->fac_comm, std::move(op));
+    }
     // assembly: every column of this level's fronts built once (zeros, scaled A entries, the
     // children's F22 columns in child order) -- k_assemble, one wave per column
     {
@@ -454,8 +721,8 @@ static int build_schedule(smlu_handle* h) {
       L.kind = K_EXTADD;
       L.off = (int64_t)xc.size();
       std::vector<int32_t> cnt, pos;
-      for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {
-        int64_t s = LS[k];
+      auto front_columns = [&](int64_t s, const std::vector<std::pair<int64_t, int64_t>>& ranges,
+                               const std::vector<int32_t>& nodes) {
         const int64_t M = P.M(s);
         cnt.assign(M + 1, 0);
         for (int64_t ci = P.ch_ptr[s]; ci < P.ch_ptr[s + 1]; ++ci) {
@@ -470,20 +737,43 @@ static int build_schedule(smlu_handle* h) {
         for (int64_t ci = P.ch_ptr[s]; ci < P.ch_ptr[s + 1]; ++ci) {
           const int64_t c = P.ch_list[ci];
           const int32_t* rm = P.relmap.data() + h->hsn[c].rowptr;
-          for (int64_t jc = 0; jc < P.nu(c); ++jc) xt[base + pos[rm[jc]]++] = make_int2((int)c, (int)jc);
+          for (int64_t jc = 0; jc < P.nu(c); ++jc) {
+            int64_t src = -1;
+            if (h->nranks == 1) src = h->hsn[c].Foff + jc * P.nu(c);
+            else if (P.col_owner(s, rm[jc]) == h->rank) {
+              if (child_col(c, jc, &src) != h->rank) src = recv_at.at(c * 1048576 + jc);
+            }
+            xt[base + pos[rm[jc]]++] = XContrib{(int32_t)c, 0, src};
+          }
         }
-        // A entries of this front by (column, row)
+        // A entries of this front by (column, row); one task per column of the given ranges
         int64_t ea = fr_ptr[s];
         const int64_t eb = fr_ptr[s + 1];
-        for (int64_t tj = 0; tj < M; ++tj) {
-          const int64_t a0 = (int64_t)ae.size();
-          while (ea < eb && P.A_lj[fr_ent[ea]] == tj) {
-            ae.push_back(make_int2(fr_ent[ea], P.A_li[fr_ent[ea]]));
-            ++ea;
+        for (size_t ri = 0; ri < ranges.size(); ++ri)
+          for (int64_t tj = ranges[ri].first; tj < ranges[ri].second; ++tj) {
+            while (ea < eb && P.A_lj[fr_ent[ea]] < tj) ++ea;
+            const int64_t a0 = (int64_t)ae.size();
+            while (ea < eb && P.A_lj[fr_ent[ea]] == tj) {
+              ae.push_back(make_int2(fr_ent[ea], P.A_li[fr_ent[ea]]));
+              ++ea;
+            }
+            xc.push_back(XCol{nodes[ri], (int32_t)tj, base + cnt[tj], cnt[tj + 1] - cnt[tj],
+                              (int32_t)((int64_t)ae.size() - a0), a0});
           }
-          xc.push_back(XCol{(int32_t)s, (int32_t)tj, base + cnt[tj], cnt[tj + 1] - cnt[tj],
-                            (int32_t)((int64_t)ae.size() - a0), a0});
-        }
+      };
+      for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {
+        const int64_t s = LS[k];
+        front_columns(s, {{0, P.M(s)}}, {(int32_t)s});
+      }
+      for (const int32_t t : dfront[l]) {   // the shared front: this rank's column blocks
+        std::vector<std::pair<int64_t, int64_t>> ranges;
+        std::vector<int32_t> nodes;
+        for (size_t i = 0; i < Y.blocks.size(); ++i)
+          if (Y.blocks[i].s == t) {
+            ranges.push_back({Y.blocks[i].c0, Y.blocks[i].c1});
+            nodes.push_back(blknode[i]);
+          }
+        front_columns(t, ranges, nodes);
       }
       L.cnt = (int64_t)xc.size() - L.off;
       if (L.cnt > 0) h->fac.push_back(L);
@@ -521,9 +811,9 @@ static int build_schedule(smlu_handle* h) {
       big.push_back(s);
       maxsteps = std::max<int64_t>(maxsteps, (r.ns + r.nb - 1) / r.nb);
     }
-    max_list = std::max<int64_t>(max_list, (int64_t)big.size() * (h->ob / 32));
+    max_list = std::max<int64_t>(max_list, dist_slots + (int64_t)big.size() * (h->ob / 32));
     // swap-list slot of sub-panel u of a front's current outer block
-    auto slot_of = [&](int64_t s, int64_t u) { return bidx[s] * (h->ob / 32) + u; };
+    auto slot_of = [&](int64_t s, int64_t u) { return dist_slots + bidx[s] * (h->ob / 32) + u; };
     bool side_busy = false;
     auto join = [&]() {
       if (!side_busy) return;
@@ -882,14 +1172,260 @@ static int build_schedule(smlu_handle* h) {
       }
       add_gemm_launch(cand, fl, -1);
     }
+    // the shared front of this level (multi-GPU): for each pivot block, its owner runs the inner
+    // steps (64-column panels with diagonal-tile pivoting, tile inverses, in-block swaps, GEMM-form
+    // triangular solves, in-block updates) on its copy, broadcasts the factored block (L rows
+    // [ob, M), tile inverses, swap lists, rowperm) to the group, and every member applies it to
+    // the column blocks it owns: deferred swaps, U rows (GEMM-form TRSM per sub-panel), the rows
+    // below each sub-panel, and the trailing update (k = block width) down to the F22 rows
+    for (const int32_t t : dfront[l]) {
+      const SNode& fr = h->hsn[t];
+      const int64_t ns = fr.ns, nu = fr.nu, M = ns + nu;
+      const int64_t np = P.npblk(t);
+      std::vector<size_t> mine;
+      for (size_t i = 0; i < Y.blocks.size(); ++i)
+        if (Y.blocks[i].s == t) mine.push_back(i);
+      for (int64_t b = 0; b < np; ++b) {
+        const int64_t ob = P.blk_c0(t, b), oe = P.blk_c1(t, b), w = oe - ob;
+        const int64_t nsub = (w + 63) / 64;
+        const int32_t o = P.blk_owner(t, b);
+        const bool own = o == h->rank;
+        int32_t bn = -1;
+        double* Lb = nullptr;
+        if (own) {
+          bn = blknode[blkmap.at((int64_t)t * 1048576 + b)];
+          Lb = store + h->hsn[bn].Loff;
+          for (int64_t kb = ob; kb < oe; kb += 64) {
+            const int64_t wk = std::min<int64_t>(64, oe - kb);
+            const int step = (int)(kb / 64);
+            const int32_t u = (int32_t)((kb - ob) / 64);
+            Launch Q;
+            Q.kind = K_PANEL;
+            Q.step = step;
+            Q.off = (int64_t)ilist.size();
+            ilist.push_back(bn);
+            ilist.push_back(u);
+            Q.cnt = 1;
+            Q.nwg = wk;
+            Q.aux2 = 64;
+            h->fac.push_back(Q);
+            Q = Launch();
+            Q.kind = K_TRIINV;
+            Q.step = step;
+            Q.off = (int64_t)ilist.size();
+            ilist.push_back(bn);
+            ilist.push_back(u);
+            Q.cnt = 1;
+            h->fac.push_back(Q);
+            if (oe - ob - wk > 0) {
+              Q = Launch();
+              Q.kind = K_LASWP;
+              Q.step = step;
+              Q.off = (int64_t)st_tasks.size();
+              st_tasks.push_back(SwapTask{bn, (int32_t)kb, 1, u, (int32_t)ob, (int32_t)oe, (int32_t)kb,
+                                          (int32_t)(kb + wk), 0});
+              Q.cnt = 1;
+              Q.nwg = (oe - ob - wk + 63) / 64;
+              h->fac.push_back(Q);
+            }
+            std::vector<GemmTask> cand;
+            std::vector<int64_t> tp;
+            if (oe - kb - wk > 0) {
+              GemmTask g{};
+              g.B = g.C = Lb + (kb + wk) * M + kb;
+              g.m = (int)wk; g.n = (int)(oe - kb - wk); g.k = (int)wk;
+              g.lda = 64; g.ldb = (int)M; g.ldc = (int)M;
+              cand.push_back(g);
+              tp.push_back(tinv_slot_off(u, false) * 2);
+            }
+            if (M - kb - wk > 0) {
+              GemmTask g{};
+              g.A = g.C = Lb + kb * M + kb + wk;
+              g.m = (int)(M - kb - wk); g.n = (int)wk; g.k = (int)wk;
+              g.lda = (int)M; g.ldb = 64; g.ldc = (int)M;
+              g.gsid = bn;
+              cand.push_back(g);
+              tp.push_back(tinv_slot_off(u, true) * 2 + 1);
+            }
+            add_gemm_launch(cand, 0.0, step, K_TRSML, 0, &tp);
+            if (M - kb - wk > 0 && oe - kb - wk > 0) {
+              GemmTask g{};
+              g.A = Lb + kb * M + kb + wk;
+              g.B = Lb + (kb + wk) * M + kb;
+              g.C = Lb + (kb + wk) * M + kb + wk;
+              g.m = (int)(M - kb - wk); g.n = (int)(oe - kb - wk); g.k = (int)wk;
+              g.lda = (int)M; g.ldb = (int)M; g.ldc = (int)M;
+              std::vector<GemmTask> c1{g};
+              add_gemm_launch(c1, 2.0 * g.m * (double)g.n * wk, step);
+            }
+          }
+        }
+        // broadcast: [L rows [ob, M) x w, ld M-ob | tile inverses | swap lists | rowperm]
+        const int64_t lbytes = 8 * (M - ob) * w, tbytes = 8 * nsub * 8192;
+        const int64_t swbytes = 4 * nsub * kSwapStride, rpbytes = 4 * w;
+        {
+          CommOp op;
+          op.type = 1;
+          op.root = o;
+          op.grp = P.group[t];
+          op.bytes = lbytes + tbytes + swbytes + rpbytes;
+          if (own) {
+            op.bbase = 4;
+            for (int64_t c = ob; c < oe; ++c)
+              op.pack.push_back(HSeg{0, 8 * (h->hsn[bn].Loff + c * M + ob), 4, 8 * (c - ob) * (M - ob), 8 * (M - ob)});
+            op.pack.push_back(HSeg{7, 0, 4, lbytes, tbytes});
+            op.pack.push_back(HSeg{8, 0, 4, lbytes + tbytes, swbytes});
+            op.pack.push_back(HSeg{9, 4 * (fr.first + ob), 4, lbytes + tbytes + swbytes, rpbytes});
+          } else {
+            op.bbase = 6;
+            op.unpack.push_back(HSeg{6, lbytes + tbytes, 8, 0, swbytes});
+            op.unpack.push_back(HSeg{6, lbytes + tbytes + swbytes, 9, 4 * (fr.first + ob), rpbytes});
+          }
+          add_comm(h->fac, h->fac_seg, h->fac_comm, std::move(op));
+        }
+        const double* bc = h->bcbuf.p;
+        const int64_t ldL = own ? M : M - ob;
+        auto Lsrc = [&](int64_t row, int64_t col) -> const double* {
+          return own ? Lb + col * M + row : bc + (col - ob) * (M - ob) + (row - ob);
+        };
+        // deferred row swaps on this rank's other blocks (left and right)
+        {
+          Launch Q;
+          Q.kind = K_LASWP;
+          Q.off = (int64_t)st_tasks.size();
+          int64_t wg = 0;
+          for (size_t i : mine) {
+            const RankLayout::Blk& T = Y.blocks[i];
+            if (T.b == b) continue;
+            st_tasks.push_back(SwapTask{blknode[i], (int32_t)ob, (int32_t)nsub, 0, (int32_t)T.c0, (int32_t)T.c1,
+                                        (int32_t)T.c1, (int32_t)T.c1, wg});
+            wg += (T.c1 - T.c0 + 63) / 64;
+          }
+          Q.cnt = (int64_t)st_tasks.size() - Q.off;
+          Q.nwg = wg;
+          if (wg > 0) h->fac.push_back(Q);
+        }
+        // target blocks right of this one: (node, columns, pivot block?) and their row pointers
+        struct Tgt { int32_t node; int64_t c0, c1; bool piv; };
+        std::vector<Tgt> right;
+        for (size_t i : mine) {
+          const RankLayout::Blk& T = Y.blocks[i];
+          if (T.c0 >= oe) right.push_back({blknode[i], T.c0, T.c1, T.c0 < ns});
+        }
+        auto trow = [&](const Tgt& T, int64_t row) -> double* {   // rows < ns of the target's first column
+          const SNode& q = h->hsn[T.node];
+          return T.piv ? store + q.Loff + T.c0 * M + row : store + q.Uoff + (T.c0 - ns) * ns + row;
+        };
+        for (int64_t u = 0; u < nsub; ++u) {
+          const int64_t kbu = ob + 64 * u, wu = std::min<int64_t>(64, oe - kbu);
+          std::vector<GemmTask> ctri, cand;
+          std::vector<int64_t> tp;
+          double fl = 0;
+          for (const Tgt& T : right) {
+            const int ldt = (int)(T.piv ? M : ns);
+            GemmTask g{};
+            g.B = g.C = trow(T, kbu);
+            g.m = (int)wu; g.n = (int)(T.c1 - T.c0); g.k = (int)wu;
+            g.lda = 64; g.ldb = ldt; g.ldc = ldt;
+            if (own) tp.push_back(tinv_slot_off(u, false) * 2);
+            else { g.A = bc + (M - ob) * w + u * 8192; tp.push_back(-1); }
+            ctri.push_back(g);
+            const int64_t m = oe - kbu - wu;
+            if (m > 0) {
+              GemmTask q{};
+              q.A = Lsrc(kbu + wu, kbu);
+              q.B = trow(T, kbu);
+              q.C = trow(T, kbu + wu);
+              q.m = (int)m; q.n = (int)(T.c1 - T.c0); q.k = (int)wu;
+              q.lda = (int)ldL; q.ldb = ldt; q.ldc = ldt;
+              cand.push_back(q);
+              fl += 2.0 * m * (double)(T.c1 - T.c0) * wu;
+            }
+          }
+          add_gemm_launch(ctri, 0.0, (int)(kbu / 64), K_TRSML, 0, &tp);
+          add_gemm_launch(cand, fl, (int)(kbu / 64), K_GEMMU);
+        }
+        {
+          std::vector<GemmTask> cand;
+          double fl = 0;
+          for (const Tgt& T : right) {
+            const int64_t nc = T.c1 - T.c0;
+            if (T.piv) {
+              if (M - oe <= 0) continue;
+              GemmTask g{};
+              g.A = Lsrc(oe, ob);
+              g.B = trow(T, ob);
+              g.C = trow(T, oe);
+              g.m = (int)(M - oe); g.n = (int)nc; g.k = (int)w;
+              g.lda = (int)ldL; g.ldb = (int)M; g.ldc = (int)M;
+              cand.push_back(g);
+              fl += 2.0 * (M - oe) * (double)nc * w;
+            } else {
+              if (ns - oe > 0) {
+                GemmTask g{};
+                g.A = Lsrc(oe, ob);
+                g.B = trow(T, ob);
+                g.C = trow(T, oe);
+                g.m = (int)(ns - oe); g.n = (int)nc; g.k = (int)w;
+                g.lda = (int)ldL; g.ldb = (int)ns; g.ldc = (int)ns;
+                cand.push_back(g);
+                fl += 2.0 * (ns - oe) * (double)nc * w;
+              }
+              if (nu > 0) {
+                const SNode& q = h->hsn[T.node];
+                GemmTask g{};
+                g.A = Lsrc(ns, ob);
+                g.B = trow(T, ob);
+                g.C = scratch + q.Foff + (T.c0 - ns) * nu;
+                g.m = (int)nu; g.n = (int)nc; g.k = (int)w;
+                g.lda = (int)ldL; g.ldb = (int)ns; g.ldc = (int)nu;
+                cand.push_back(g);
+                fl += 2.0 * nu * (double)nc * w;
+              }
+            }
+          }
+          add_gemm_launch(cand, fl, (int)(ob / 64), K_GEMMO);
+        }
+      }
+    }
   }
   // solves: per level, small fronts by one workgroup each; large fronts (ns > kSolveBigNs)
   // gather + one launch per 64-column block with 256-row chunks per workgroup
   h->fwd.clear();
   h->bwd.clear();
   std::vector<std::vector<Launch>> bwd_levels;
+  auto node_of = [&](int64_t s, int64_t b) { return blknode[blkmap.at(s * 1048576 + b)]; };
+  auto tri_steps = [&](bool upper, int32_t node, int64_t ob, int64_t oe, std::vector<Launch>& out) {
+    const SNode& r = h->hsn[node];
+    const int64_t M = (int64_t)r.ns + r.nu, nbs = (r.ns + 63) / 64;
+    std::vector<int64_t> jbs;
+    for (int64_t jb = ob; jb < oe; jb += 64) jbs.push_back(jb);
+    if (upper) std::reverse(jbs.begin(), jbs.end());
+    for (int64_t jb : jbs) {
+      Launch F;
+      F.kind = upper ? K_TRIB : K_TRIF;
+      F.step = (int)(upper ? nbs - 1 - jb / 64 : jb / 64);
+      F.off = (int64_t)ft.size();
+      const int64_t bw = std::min<int64_t>(64, r.ns - jb);
+      const int64_t wg = upper ? std::max<int64_t>(1, (jb + 255) / 256) : std::max<int64_t>(1, (M - jb - bw + 255) / 256);
+      ft.push_back(FrontTile{node, 0, 0});
+      F.cnt = 1;
+      F.nwg = wg;
+      out.push_back(F);
+    }
+  };
+  // one vector segment of vbuf (doubles [off, off+cnt)) from rank a to rank b, in place
+  auto vhop = [&](std::vector<Launch>& seq, std::vector<size_t>& seg, std::vector<int>& cm, int32_t a, int32_t b,
+                  int64_t off, int64_t cnt) {
+    if (a == b || cnt <= 0 || (h->rank != a && h->rank != b)) return;
+    CommOp op;
+    const int pi = op.at(h->rank == a ? b : a);
+    if (h->rank == a) { op.sbase[pi] = 2; op.soff[pi] = 8 * off; op.sbytes[pi] = 8 * cnt; }
+    else { op.rbase[pi] = 2; op.roff[pi] = 8 * off; op.rbytes[pi] = 8 * cnt; }
+    add_comm(seq, seg, cm, std::move(op));
+  };
+  auto holder = [&](int64_t c) { return P.dist(c) ? P.blk_owner(c, P.npblk(c) - 1) : P.owner[c]; };
   for (int l = 0; l < P.nlevels; ++l) {
-    if (isx[l]) h->fwd_seg.push_back(h->fwd.size());
     std::vector<int64_t> small, bigs;
     for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {
       int64_t s = LS[k];
@@ -966,42 +1502,194 @@ static int build_schedule(smlu_handle* h) {
       for (auto& b : bsteps) bl.push_back(b);
     }
     bwd_levels.push_back(bl);
+    // forward solve of the shared front: the children's update vectors go to the first block's
+    // owner, which gathers the front vector; the vector then follows the pivot blocks' owners
+    // (shared fronts of this level, in front order on every rank)
+    for (const int32_t t : dfront[l]) {
+      const int64_t np = P.npblk(t), M = P.M(t);
+      const int64_t tv = h->hsn[t].voff;
+      const int32_t o0 = P.blk_owner(t, 0);
+      {
+        CommOp op;
+        std::vector<std::vector<int64_t>> kids(h->nranks);
+        for (int64_t e = P.ch_ptr[t]; e < P.ch_ptr[t + 1]; ++e) kids[holder(P.ch_list[e])].push_back(P.ch_list[e]);
+        for (int32_t q = 0; q < h->nranks; ++q) {
+          if (q == o0 || kids[q].empty()) continue;
+          if (h->rank != q && h->rank != o0) continue;
+          const int pi = op.at(h->rank == q ? o0 : q);
+          int64_t acc = 0;
+          for (int64_t c : kids[q]) {
+            const int64_t off = 8 * (h->hsn[c].voff + P.ns(c)), nb8 = 8 * P.nu(c);
+            if (h->rank == q) op.pack.push_back(HSeg{2, off, 4, acc, nb8});
+            else op.unpack.push_back(HSeg{5, acc, 2, off, nb8});
+            acc += nb8;
+          }
+          if (h->rank == q) op.sbytes[pi] = acc;
+          else op.rbytes[pi] = acc;
+        }
+        // receive offsets: per peer contiguous in the receive staging
+        int64_t racc = 0;
+        for (size_t i = 0; i < op.peer.size(); ++i) {
+          op.roff[i] = racc;
+          racc += op.rbytes[i];
+        }
+        if (h->rank == o0) {   // unpack offsets were per peer from 0: shift by the peer's roff
+          size_t k = 0;
+          for (int32_t q = 0; q < h->nranks; ++q) {
+            if (q == o0 || kids[q].empty()) continue;
+            int64_t shift = 0;
+            for (size_t i = 0; i < op.peer.size(); ++i)
+              if (op.peer[i] == q) shift = op.roff[i];
+            for (size_t j = 0; j < kids[q].size(); ++j) op.unpack[k++].so += shift;
+          }
+        }
+        if (!op.peer.empty()) add_comm(h->fwd, h->fwd_seg, h->fwd_comm, std::move(op));
+      }
+      if (h->rank == o0) {
+        Launch L;
+        L.kind = K_FWDG;
+        L.off = (int64_t)ilist.size();
+        ilist.push_back(t);
+        L.cnt = 1;
+        h->fwd.push_back(L);
+      }
+      for (int64_t b = 0; b < np; ++b) {
+        const int32_t o = P.blk_owner(t, b);
+        const int64_t ob = P.blk_c0(t, b), oe = P.blk_c1(t, b);
+        if (h->rank == o) tri_steps(false, node_of(t, b), ob, oe, h->fwd);
+        if (b + 1 < np) vhop(h->fwd, h->fwd_seg, h->fwd_comm, o, P.blk_owner(t, b + 1), tv + oe, M - oe);
+      }
+    }
   }
+  // backward, from the root level down; after each level holding a shared front (and at the
+  // end) every rank shares the solution rows it computed since the previous exchange
+  std::vector<std::vector<std::pair<int64_t, int64_t>>> pending_rows(h->nranks);   // per rank, since the last exchange
+  std::vector<std::pair<int64_t, int64_t>> myrows;   // x rows (first, count) since the last exchange
+  auto xbwd = [&]() {
+    CommOp op;
+    int64_t mine = 0;
+    for (auto& rg : myrows) {
+      op.pack.push_back(HSeg{3, 8 * rg.first, 4, 8 * mine, 8 * rg.second});
+      mine += rg.second;
+    }
+    // every peer's rows, in its own order (the same enumeration on every rank)
+    std::vector<std::vector<std::pair<int64_t, int64_t>>> theirs(h->nranks);
+    theirs.swap(pending_rows);
+    int64_t racc = 0;
+    for (int32_t q = 0; q < h->nranks; ++q) {
+      if (q == h->rank) continue;
+      const int pi = op.at(q);
+      op.soff[pi] = 0;
+      op.sbytes[pi] = 8 * mine;
+      op.roff[pi] = racc;
+      int64_t cnt = 0;
+      for (auto& rg : theirs[q]) {
+        op.unpack.push_back(HSeg{5, racc + 8 * cnt, 3, 8 * rg.first, 8 * rg.second});
+        cnt += rg.second;
+      }
+      op.rbytes[pi] = 8 * cnt;
+      racc += 8 * cnt;
+    }
+    myrows.clear();
+    add_comm(h->bwd, h->bwd_seg, h->bwd_comm, std::move(op));
+  };
+  (void)xbwd;
   for (int l = P.nlevels - 1; l >= 0; --l) {
     for (auto& L : bwd_levels[l]) h->bwd.push_back(L);
-    if (isx[l]) h->bwd_seg.push_back(h->bwd.size());   // exchange point after this level
-  }
-  // exchange lists (multi-GPU): child blocks crossing ranks before each exchange level, and
-  // per rank the solution rows of the backward segment that ends at that level
-  {
-    const size_t nx = h->nranks > 1 ? P.xlevels.size() : 0;
-    h->xfac.assign(nx, {});
-    h->xfwd.assign(nx, {});
-    h->xbwd.assign(nx, std::vector<std::vector<std::pair<int64_t, int64_t>>>(h->nranks));
-    for (size_t k = 0; k < nx; ++k) {
-      const int l = P.xlevels[k];
-      for (int64_t kk = P.lev_ptr[l]; kk < P.lev_ptr[l + 1]; ++kk) {
-        const int64_t pp = P.lev_sup[kk];
-        for (int64_t e = P.ch_ptr[pp]; e < P.ch_ptr[pp + 1]; ++e) {
-          const int64_t c = P.ch_list[e];
-          if (P.owner[c] == P.owner[pp]) continue;
-          if (P.nu(c) > 0)
-            h->xfac[k].push_back({P.owner[c], P.owner[pp], P.Foff[c], P.nu(c) * P.nu(c)});
-          h->xfwd[k].push_back({P.owner[c], P.owner[pp], h->hsn[c].voff, P.M(c)});
+    if (h->nranks == 1) continue;
+    // rows every rank computes at this level (global enumeration)
+    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+      const int64_t s = P.lev_sup[k];
+      if (!P.dist(s)) {
+        pending_rows[P.owner[s]].push_back({P.s_first[s], P.ns(s)});
+        continue;
+      }
+      for (int64_t b = 0; b < P.npblk(s); ++b)
+        pending_rows[P.blk_owner(s, b)].push_back({P.s_first[s] + P.blk_c0(s, b), P.blk_c1(s, b) - P.blk_c0(s, b)});
+    }
+    // (shared fronts of this level, in front order on every rank)
+    for (const int32_t t : dfront[l]) {
+      const int64_t np = P.npblk(t), nbk = np + P.nublk(t), ns = P.ns(t);
+      const int64_t tv = h->hsn[t].voff;
+      // the forward solve left y of each pivot block in x on the block's owner: the rank that
+      // starts the backward chain collects all of them first
+      const int32_t cs = nbk > np ? P.blk_owner(t, np) : P.blk_owner(t, np - 1);
+      {
+        CommOp op;
+        const int64_t f0 = P.s_first[t];
+        for (int32_t q = 0; q < h->nranks; ++q) {
+          if (q == cs || (h->rank != q && h->rank != cs)) continue;
+          int64_t acc = 0;
+          std::vector<HSeg> segs;
+          for (int64_t b = 0; b < np; ++b) {
+            if (P.blk_owner(t, b) != q) continue;
+            const int64_t o8 = 8 * (f0 + P.blk_c0(t, b)), nb8 = 8 * (P.blk_c1(t, b) - P.blk_c0(t, b));
+            segs.push_back(h->rank == q ? HSeg{3, o8, 4, acc, nb8} : HSeg{5, acc, 3, o8, nb8});
+            acc += nb8;
+          }
+          if (acc == 0) continue;
+          const int pi = op.at(h->rank == q ? cs : q);
+          if (h->rank == q) {
+            op.sbytes[pi] = acc;
+            for (auto& g : segs) op.pack.push_back(g);
+          } else {
+            op.rbytes[pi] = acc;
+            for (auto& g : segs) op.unpack.push_back(g);
+          }
+        }
+        if (h->rank == cs) {   // receive offsets per peer, shift the unpack copies
+          int64_t racc = 0;
+          size_t k = 0;
+          for (size_t i = 0; i < op.peer.size(); ++i) {
+            op.roff[i] = racc;
+            int64_t left = op.rbytes[i];
+            while (left > 0 && k < op.unpack.size()) {
+              op.unpack[k].so += racc;
+              left -= op.unpack[k].bytes;
+              ++k;
+            }
+            racc += op.rbytes[i];
+          }
+        }
+        if (!op.peer.empty()) add_comm(h->bwd, h->bwd_seg, h->bwd_comm, std::move(op));
+      }
+      int32_t prev = -1;
+      bool first = true;
+      for (int64_t ub = np; ub < nbk; ++ub) {   // U12 contributions, block by block
+        const int32_t o = P.blk_owner(t, ub);
+        if (prev >= 0) vhop(h->bwd, h->bwd_seg, h->bwd_comm, prev, o, tv, ns);
+        if (h->rank == o) {
+          Launch L;
+          L.kind = K_BWDU12C;
+          L.node = node_of(t, ub);
+          L.aux = P.blk_c0(t, ub);
+          L.aux2 = P.blk_c1(t, ub);
+          L.cnt = first ? 1 : 0;
+          h->bwd.push_back(L);
+        }
+        prev = o;
+        first = false;
+      }
+      if (first) {   // no update columns: the chain starts from the solution rows of the front
+        prev = P.blk_owner(t, np - 1);
+        if (h->rank == prev) {
+          Launch L;
+          L.kind = K_VCOPY;
+          L.node = t;
+          h->bwd.push_back(L);
         }
       }
-      auto byrank = [](const smlu_handle::XBlk& a, const smlu_handle::XBlk& b) {
-        return a.src != b.src ? a.src < b.src : a.dst != b.dst ? a.dst < b.dst : a.off < b.off;
-      };
-      std::sort(h->xfac[k].begin(), h->xfac[k].end(), byrank);
-      std::sort(h->xfwd[k].begin(), h->xfwd[k].end(), byrank);
-      const int lhi = k + 1 < nx ? P.xlevels[k + 1] : P.nlevels;
-      for (int ll = l; ll < lhi; ++ll)
-        for (int64_t kk = P.lev_ptr[ll]; kk < P.lev_ptr[ll + 1]; ++kk) {
-          const int64_t s2 = P.lev_sup[kk];
-          h->xbwd[k][P.owner[s2]].push_back({P.s_first[s2], P.ns(s2)});
-        }
+      for (int64_t b = np - 1; b >= 0; --b) {
+        const int32_t o = P.blk_owner(t, b);
+        const int64_t ob = P.blk_c0(t, b), oe = P.blk_c1(t, b);
+        vhop(h->bwd, h->bwd_seg, h->bwd_comm, prev, o, tv, oe);
+        if (h->rank == o) tri_steps(true, node_of(t, b), ob, oe, h->bwd);
+        prev = o;
+      }
     }
+    for (auto& rg : pending_rows[h->rank]) myrows.push_back(rg);
+    pending_rows[h->rank].clear();
+    if (dlevel[l] || l == 0) xbwd();
   }
 
   h->nlaunch = (int64_t)h->fac.size();
@@ -1024,7 +1712,7 @@ static int build_schedule(smlu_handle* h) {
           for (int64_t t = 0; t < L.cnt; ++t) {
             const XCol& x = xc[L.off + t];
             mn += (double)P.M(x.p);
-            for (int64_t q = 0; q < x.cnt; ++q) rd += (double)P.nu(xt[x.off + q].x);
+            for (int64_t q = 0; q < x.cnt; ++q) rd += (double)P.nu(xt[x.off + q].child);
           }
         std::fprintf(fp, "%zu,%d,%s,%d,%lld,%lld,%lld,%.0f,%d,%.0f\n", i, L.kind, kKindName[L.kind], L.step,
                      (long long)L.aux, (long long)L.nwg, (long long)L.cnt, L.kind == K_EXTADD ? rd : L.flops, kmax, mn);
@@ -1038,7 +1726,8 @@ static int build_schedule(smlu_handle* h) {
   HIPCHK(h->xtasks.upload(xt.data(), xt.size(), st));
   HIPCHK(h->aents.upload(ae.data(), ae.size(), st));
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
-  if (!tinv_patch.empty()) {   // operands in the tile-inverse slots: patch in the buffer address
+  if (h->nranks > 1) max_list = std::max<int64_t>(max_list, dist_slots);
+  if (!tinv_patch.empty() || h->nranks > 1) {   // operands in the tile-inverse slots: patch in the buffer address
     HIPCHK(h->tinv.alloc((size_t)max_list * 8192));
     for (auto& pt : tinv_patch) {
       const double* a = h->tinv.p + pt.second / 2;
@@ -1051,6 +1740,46 @@ static int build_schedule(smlu_handle* h) {
   HIPCHK(h->xcols.upload(xc.data(), xc.size(), st));
   HIPCHK(h->swaps.alloc((size_t)max_list * kSwapStride));
   HIPCHK(h->vbuf.alloc((size_t)std::max<int64_t>(voff, 1)));
+  // communication steps: staging sizes, then every pack / unpack copy as a device descriptor
+  if (!h->comm.empty()) {
+    int64_t ss = 0, rs = 0, hs = 0, hr = 0;
+    for (const CommOp& op : h->comm) {
+      int64_t a = 0, b = 0, sa = 0, sb = 0;
+      for (size_t i = 0; i < op.peer.size(); ++i) {
+        if (op.sbase[i] == 4) a = std::max(a, op.soff[i] + op.sbytes[i]);
+        if (op.rbase[i] == 5) b = std::max(b, op.roff[i] + op.rbytes[i]);
+        sa += op.sbytes[i];   // host staging lays every peer's message side by side
+        sb += op.rbytes[i];
+      }
+      if (op.type == 1 && op.bbase == 4) a = std::max(a, op.bytes);
+      ss = std::max(ss, a);
+      rs = std::max(rs, b);
+      hs = std::max(hs, std::max(sa, op.type == 1 ? op.bytes : 0));
+      hr = std::max(hr, std::max(sb, op.type == 1 ? op.bytes : 0));
+    }
+    h->stage_bytes_s = ss;
+    h->stage_bytes_r = rs;
+    HIPCHK(h->stage_s.alloc((size_t)(ss + 7) / 8 + 1));
+    HIPCHK(h->stage_r.alloc((size_t)(rs + 7) / 8 + 1));
+    if (!h->tr.device_memory) {
+      HIPCHK(hipHostMalloc((void**)&h->hstage_s, (size_t)std::max<int64_t>(hs, 8), 0));
+      HIPCHK(hipHostMalloc((void**)&h->hstage_r, (size_t)std::max<int64_t>(hr, 8), 0));
+    }
+    char* base[10] = {(char*)h->store.p, (char*)h->scratch.p, (char*)h->vbuf.p, (char*)h->wrk.p,
+                      (char*)h->stage_s.p, (char*)h->stage_r.p, (char*)h->bcbuf.p, (char*)h->tinv.p,
+                      (char*)h->swaps.p, (char*)h->rowperm.p};
+    std::vector<SegDesc> d;
+    for (CommOp& op : h->comm) {
+      auto emit = [&](const std::vector<HSeg>& v, int64_t& at) {
+        at = (int64_t)d.size();
+        for (const HSeg& g : v)
+          d.push_back(SegDesc{(uint64_t)(base[g.sb] + g.so), (uint64_t)(base[g.db] + g.dof), g.bytes / 4});
+      };
+      emit(op.pack, op.pack0);
+      emit(op.unpack, op.unpack0);
+    }
+    HIPCHK(h->segdesc.upload(d.data(), d.size(), st));
+  }
   HIPCHK(hipStreamSynchronize(st));
   return SMLU_OK;
 }
@@ -1085,10 +1814,33 @@ static int setup_device(smlu_handle* h) {
   if (!h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
   if (!h->ev_join) HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
   hipStream_t st = h->stream;
+  // this rank's layout: the plan's own on one GPU; ordinary fronts + owned column blocks of
+  // the shared fronts on a partitioned handle
+  if (h->nranks > 1) {
+    rank_layout(P, h->rank, h->lay);
+  } else {
+    RankLayout& Y = h->lay;
+    Y = RankLayout();
+    Y.Loff = P.Loff;
+    Y.Uoff = P.Uoff;
+    Y.Foff = P.Foff;
+    Y.recv_off.assign(P.nsup, -1);
+    Y.recv_size.assign(P.nsup, 0);
+    Y.store_size = P.factor_size;
+    Y.scratch_size = P.scratch_size;
+  }
   HIPCHK(h->A.alloc((size_t)std::max<int64_t>(P.nnzA, 1)));
   HIPCHK(h->Rs.alloc((size_t)P.n));
-  HIPCHK(h->store.alloc((size_t)std::max<int64_t>(P.factor_size, 1)));
-  HIPCHK(h->scratch.alloc((size_t)std::max<int64_t>(P.scratch_size, 1)));
+  HIPCHK(h->store.alloc((size_t)std::max<int64_t>(h->lay.store_size, 1)));
+  HIPCHK(h->scratch.alloc((size_t)std::max<int64_t>(h->lay.scratch_size, 1)));
+  if (h->nranks > 1) {   // received pivot block + tile inverses + swap lists + rowperm
+    int64_t bc = 1;
+    for (int64_t s = 0; s < P.nsup; ++s)
+      if (P.dist(s) && std::binary_search(P.group[s].begin(), P.group[s].end(), h->rank))
+        bc = std::max<int64_t>(bc, P.M(s) * P.dob + (P.dob / 64) * 8192 + (P.dob / 64) * kSwapStride / 2 + P.dob / 2 + 64);
+    HIPCHK(h->bcbuf.alloc((size_t)bc));
+    HIPCHK(h->d_red.alloc(8));
+  }
   HIPCHK(h->wrk.alloc((size_t)P.n));
   HIPCHK(h->wrk2.alloc((size_t)P.n));
   HIPCHK(h->growth.alloc(1));
@@ -1110,16 +1862,12 @@ static int setup_device(smlu_handle* h) {
     for (int64_t j = 0; j < P.n; ++j) id[j] = (int32_t)(j - pf[j]);
     HIPCHK(h->rowperm0.upload(id.data(), id.size(), st));
   }
-  HIPCHK(h->info.alloc((size_t)std::max<int64_t>(P.nsup, 1)));
-  if (h->nranks > 1) {
-    std::vector<int8_t> own(P.n);
-    for (int64_t j = 0; j < P.n; ++j) own[j] = P.owner[P.col2s[j]] == h->rank ? 1 : 0;
-    HIPCHK(h->rowown.upload(own.data(), own.size(), st));
-  }
+  const int64_t nnodes = P.nsup + (int64_t)h->lay.blocks.size();
+  HIPCHK(h->info.alloc((size_t)std::max<int64_t>(nnodes, 1)));
   HIPCHK(init_kernel_attributes());
   if (h->hinfo) HIPCHK(hipHostFree(h->hinfo));
   h->hinfo = nullptr;
-  HIPCHK(hipHostMalloc((void**)&h->hinfo, sizeof(int32_t) * std::max<int64_t>(P.nsup, 1), 0));
+  HIPCHK(hipHostMalloc((void**)&h->hinfo, sizeof(int32_t) * std::max<int64_t>(nnodes, 1), 0));
   return build_schedule(h);
 }
 
@@ -1219,7 +1967,7 @@ static int enqueue_factor(smlu_handle* h, Timer& tm, bool dbg, int seg) {
   double diag_tol = P.given_order ? 0.0 : h->opts.diag_pivot_tol;
   double piv_tol = h->opts.pivot_tol;
   if (seg > 0) goto launches;
-  HIPCHK(hipMemsetAsync(h->info.p, 0, sizeof(int32_t) * std::max<int64_t>(P.nsup, 1), st));
+  HIPCHK(hipMemsetAsync(h->info.p, 0, sizeof(int32_t) * std::max<int64_t>(h->nnodes, 1), st));
   HIPCHK(hipMemsetAsync(h->growth.p, 0, sizeof(double), st));
   // identity (local) row permutation; fronts overwrite their part
   HIPCHK(hipMemcpyAsync(h->rowperm.p, h->rowperm0.p, sizeof(int32_t) * P.n, hipMemcpyDeviceToDevice, st));
@@ -1294,7 +2042,7 @@ static int factor_segment(smlu_handle* h, Timer& tm, int seg) {
 static int finish_factor(smlu_handle* h, Timer& tm, std::chrono::steady_clock::time_point t0) {
   Plan& P = h->plan;
   hipStream_t st = h->stream;
-  HIPCHK(hipMemcpyAsync(h->hinfo, h->info.p, sizeof(int32_t) * P.nsup, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipMemcpyAsync(h->hinfo, h->info.p, sizeof(int32_t) * h->nnodes, hipMemcpyDeviceToHost, st));
   double g = 0;
   HIPCHK(hipMemcpyAsync(&g, h->growth.p, sizeof(double), hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -1306,25 +2054,92 @@ static int finish_factor(smlu_handle* h, Timer& tm, std::chrono::steady_clock::t
   h->weak = 0;
   h->errcol = -1;
   int rc = SMLU_OK;
-  for (int64_t s = 0; s < P.nsup; ++s) {
+  for (int64_t s = 0; s < h->nnodes; ++s) {
     int32_t v = h->hinfo[s];
     if (v & 2) h->weak++;
     if ((v & 1) && rc != SMLU_SINGULAR) {
       rc = SMLU_SINGULAR;
-      h->errcol = P.s_first[s] + ((v >> 2) > 0 ? (v >> 2) - 1 : 0);
+      h->errcol = P.s_first[h->node_front[s]] + ((v >> 2) > 0 ? (v >> 2) - 1 : 0);
     }
+  }
+  if (h->nranks > 1) {   // the pivot status of the whole partition, on every rank
+    double red[3] = {rc == SMLU_SINGULAR ? 1.0 : 0.0, (double)h->errcol, (double)h->weak};
+    if (h->tr.allreduce_max(h->tr.ctx, red, 3) != 0) return fail(h, SMLU_ERR_HIP, "transport allreduce failed");
+    rc = red[0] > 0 ? SMLU_SINGULAR : SMLU_OK;
+    h->errcol = (int64_t)red[1];
+    h->weak = (int64_t)red[2];
   }
   if (rc == SMLU_SINGULAR) h->err = "matrix is singular (zero pivot column)";
   return rc;
 }
 
+// One communication step: pack copies, the transfer through the transport, unpack copies.
+// Device-memory transports (RCCL) are enqueued on the stream; host-memory ones go through the
+// pinned staging buffers after a stream synchronisation.
+static int exec_comm(smlu_handle* h, int id) {
+  CommOp& op = h->comm[id];
+  hipStream_t st = h->stream;
+  HIPCHK(launch_segcopy(st, h->segdesc.p + op.pack0, (int64_t)op.pack.size()));
+  char* base[10] = {(char*)h->store.p, (char*)h->scratch.p, (char*)h->vbuf.p, (char*)h->wrk.p,
+                    (char*)h->stage_s.p, (char*)h->stage_r.p, (char*)h->bcbuf.p, (char*)h->tinv.p,
+                    (char*)h->swaps.p, (char*)h->rowperm.p};
+  const bool dev = h->tr.device_memory != 0;
+  int e = 0;
+  if (op.type == 1) {
+    char* buf = base[op.bbase];
+    if (dev) {
+      e = h->tr.bcast(h->tr.ctx, buf, op.bytes, op.root, (int32_t)op.grp.size(), op.grp.data(), (void*)st);
+    } else {
+      char* hb = h->rank == op.root ? h->hstage_s : h->hstage_r;
+      if (h->rank == op.root) HIPCHK(hipMemcpyAsync(hb, buf, op.bytes, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      e = h->tr.bcast(h->tr.ctx, hb, op.bytes, op.root, (int32_t)op.grp.size(), op.grp.data(), nullptr);
+      if (e == 0 && h->rank != op.root) HIPCHK(hipMemcpyAsync(buf, hb, op.bytes, hipMemcpyHostToDevice, st));
+    }
+  } else {
+    const int np = (int)op.peer.size();
+    std::vector<void*> sb(np), rb(np);
+    if (dev) {
+      for (int i = 0; i < np; ++i) {
+        sb[i] = base[op.sbase[i]] + op.soff[i];
+        rb[i] = base[op.rbase[i]] + op.roff[i];
+      }
+      e = h->tr.exchange(h->tr.ctx, np, op.peer.data(), sb.data(), op.sbytes.data(), rb.data(), op.rbytes.data(),
+                         (void*)st);
+    } else {
+      // host staging: sends packed side by side, receives side by side
+      int64_t so = 0, ro = 0;
+      for (int i = 0; i < np; ++i) {
+        if (op.sbytes[i] > 0)
+          HIPCHK(hipMemcpyAsync(h->hstage_s + so, base[op.sbase[i]] + op.soff[i], op.sbytes[i], hipMemcpyDeviceToHost, st));
+        sb[i] = h->hstage_s + so;
+        rb[i] = h->hstage_r + ro;
+        so += op.sbytes[i];
+        ro += op.rbytes[i];
+      }
+      HIPCHK(hipStreamSynchronize(st));
+      e = h->tr.exchange(h->tr.ctx, np, op.peer.data(), sb.data(), op.sbytes.data(), rb.data(), op.rbytes.data(),
+                         nullptr);
+      for (int i = 0; i < np && e == 0; ++i)
+        if (op.rbytes[i] > 0)
+          HIPCHK(hipMemcpyAsync(base[op.rbase[i]] + op.roff[i], rb[i], op.rbytes[i], hipMemcpyHostToDevice, st));
+    }
+  }
+  if (e != 0) return fail(h, SMLU_ERR_HIP, "transport error " + std::to_string(e) + " in communication step");
+  HIPCHK(launch_segcopy(st, h->segdesc.p + op.unpack0, (int64_t)op.unpack.size()));
+  return SMLU_OK;
+}
+
 static int run_factor_once(smlu_handle* h) {
   HIPCHK(hipSetDevice(h->device));
-  if (h->nranks > 1) return fail(h, SMLU_ERR_STATE, "partitioned handle: use smlu_dist_factor_segment");
   auto t0 = std::chrono::steady_clock::now();
   for (auto& v : h->kind_ms) v = 0;
   Timer tm(h);
   for (size_t seg = 0; seg < h->fac_seg.size(); ++seg) {
+    if (seg > 0) {
+      int rc = exec_comm(h, h->fac_comm[seg - 1]);
+      if (rc != SMLU_OK) return rc;
+    }
     int rc = factor_segment(h, tm, (int)seg);
     if (rc != SMLU_OK) return rc;
   }
@@ -1345,6 +2160,12 @@ static void release_schedule(smlu_handle* h) {
   h->swaps.free();
   h->vbuf.free();
   h->tinv.free();
+  h->stage_s.free();
+  h->stage_r.free();
+  h->segdesc.free();
+  if (h->hstage_s) (void)hipHostFree(h->hstage_s);
+  if (h->hstage_r) (void)hipHostFree(h->hstage_r);
+  h->hstage_s = h->hstage_r = nullptr;
 }
 
 static int rebuild_schedule(smlu_handle* h) {
@@ -1372,7 +2193,7 @@ static int run_factor(smlu_handle* h) {
   if (rc < 0) return rc;
   const bool off = std::getenv("SMLU_NO_REPIVOT") != nullptr;   // dev/test knob
   if ((rc == SMLU_SINGULAR || h->weak > 0) && h->pivmode == 0 && !off && has_tile_fronts(h) &&
-      h->opts.pivot_tol > 0 && !h->plan.given_order) {
+      h->opts.pivot_tol > 0 && !h->plan.given_order && h->nranks == 1) {
     h->pivmode = 1;
     int r2 = rebuild_schedule(h);
     if (r2 != SMLU_OK) return r2;
@@ -1402,6 +2223,11 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w) {
     case K_BWDU:
       return launch_bwd_u12(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->sn.p, h->rows.p, h->store.p, w,
                             h->vbuf.p);
+    case K_BWDU12C:
+      return launch_bwd_u12_cols(st, h->sn.p, L.node, h->hsn[L.node].ns, L.aux, L.aux2, (int)L.cnt, h->rows.p,
+                                 h->store.p, w, h->vbuf.p);
+    case K_VCOPY:
+      return launch_vcopy(st, h->sn.p, L.node, h->hsn[L.node].ns, w, h->vbuf.p);
   }
   return hipErrorInvalidValue;
 }
@@ -1409,7 +2235,7 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w) {
 static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode) {
   // mode 0: ldiv (b -> x); 1: lsolve in place on dx (final order); 2: rsolve in place
   Plan& P = h->plan;
-  if (h->nranks > 1) return fail(h, SMLU_ERR_STATE, "partitioned handle: use smlu_dist_solve_segment");
+  if (h->nranks > 1 && mode != 0) return fail(h, SMLU_ERR_STATE, "lsolve!/rsolve! are single-GPU only");
   hipStream_t st = h->stream;
   auto t0 = std::chrono::steady_clock::now();
   Timer tm(h);
@@ -1419,10 +2245,26 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode)
   if (mode == 0) HIPCHK(launch_perm_in(st, P.n, h->p0.p, h->Rs.p, db, w));
   if (mode == 1) HIPCHK(launch_unswap(st, P.n, h->posfirst.p, h->rowperm.p, dx, w));
   if (mode == 2) HIPCHK(hipMemcpyAsync(w, dx, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st));
-  if (mode != 2)
-    for (const Launch& L : h->fwd) HIPCHK(run_solve_launch(h, L, w));
-  if (mode != 1)
-    for (const Launch& L : h->bwd) HIPCHK(run_solve_launch(h, L, w));
+  // launches between communication steps (one GPU: a single segment each)
+  auto run_seq = [&](const std::vector<Launch>& seq, const std::vector<size_t>& seg, const std::vector<int>& cm) {
+    for (size_t k = 0; k < seg.size(); ++k) {
+      if (k > 0) {
+        int rc = exec_comm(h, cm[k - 1]);
+        if (rc != SMLU_OK) return rc;
+      }
+      const size_t hi = k + 1 < seg.size() ? seg[k + 1] : seq.size();
+      for (size_t i = seg[k]; i < hi; ++i) HIPCHK(run_solve_launch(h, seq[i], w));
+    }
+    return (int)SMLU_OK;
+  };
+  if (mode != 2) {
+    int rc = run_seq(h->fwd, h->fwd_seg, h->fwd_comm);
+    if (rc != SMLU_OK) return rc;
+  }
+  if (mode != 1) {
+    int rc = run_seq(h->bwd, h->bwd_seg, h->bwd_comm);
+    if (rc != SMLU_OK) return rc;
+  }
   if (mode == 0) HIPCHK(launch_perm_out(st, P.n, h->q.p, w, dx));
   else HIPCHK(hipMemcpyAsync(dx, w, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st));
   HIPCHK(tm.end(stop));
@@ -1482,13 +2324,17 @@ static std::vector<int64_t> diagonal_match(int64_t n, const int64_t* colptr, con
 
 static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
                        const int64_t* p, const int64_t* q, const double* Rs, const smlu_opts* opts,
-                       smlu_handle** out, int rank = 0, int nranks = 1) {
+                       smlu_handle** out, int rank = 0, int nranks = 1, const smlu_transport* tr = nullptr,
+                       RcclState* rccl = nullptr) {
+  std::unique_ptr<RcclState> rccl_own(rccl);   // owned by the handle once it exists
   if (!out) return fail(nullptr, SMLU_ERR_ARG, "out is NULL");
   *out = nullptr;
   if (n <= 0 || !colptr || (!rowval && n > 0) || !nzval)
     return fail(nullptr, SMLU_ERR_ARG, "invalid matrix arguments");
   std::unique_ptr<smlu_handle> h(new (std::nothrow) smlu_handle());
   if (!h) return fail(nullptr, SMLU_ERR_ALLOC, "allocation failed");
+  h->rccl = rccl_own.release();
+  if (tr) h->tr = *tr;
   if (opts) h->opts = *opts;
   else smlu_default_opts(&h->opts);
   if (!valid_opts(&h->opts)) return fail(nullptr, SMLU_ERR_ARG, "index_base must be 0 or 1");
@@ -1510,11 +2356,16 @@ static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, 
   h->nranks = nranks;
   if (!p && !h->plan.matched) h->dominant = diagonally_dominant(n, colptr, rowval, nzval, h->opts.index_base);
   if (nranks > 1) {
-    h->plan.compute_owners(nranks);
+    if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
+    h->plan.compute_owners(nranks, h->ob);
     h->opts.profile = 0;   // per-kind event timing is single-GPU only
   }
   rc = setup_device(h.get());
   if (rc != SMLU_OK) { g_last_error = h->err; return rc; }
+  if (h->rccl) {
+    static_cast<RcclState*>(h->rccl)->stream = h->stream;
+    static_cast<RcclState*>(h->rccl)->dbuf = h->d_red.p;
+  }
   hipStream_t st = h->stream;
   {
     smlu_handle* hp = h.get();
@@ -1525,12 +2376,7 @@ static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, 
       h->given_Rs = true;
     }
   }
-  if (nranks > 1) {   // the caller drives the segments and the exchanges (smlu_dist_*)
-    HIPCHK2(h.get(), hipStreamSynchronize(st));
-    *out = h.release();
-    return SMLU_OK;
-  }
-  rc = run_factor(h.get());
+  rc = run_factor(h.get());   // collective on a partitioned handle
   *out = h.release();
   return rc;
 }
@@ -2222,6 +3068,17 @@ double smlu_stat(const smlu_handle* h, const char* key) {
   if (k == "dominant") return h->dominant ? 1.0 : 0.0;
   if (k == "pivmode") return (double)h->pivmode;
   if (k == "matched") return h->plan.matched ? 1.0 : 0.0;
+  if (k == "nranks") return (double)h->nranks;
+  if (k == "owned_blocks") return (double)h->lay.blocks.size();
+  if (k == "comm_steps") return (double)h->comm.size();
+  if (k == "store_bytes_rank") return 8.0 * (double)h->lay.store_size;
+  if (k == "scratch_bytes_rank") return 8.0 * (double)h->lay.scratch_size;
+  if (k == "shared_fronts") {
+    double c = 0;
+    for (int64_t s = 0; s < h->plan.nsup && h->nranks > 1; ++s)
+      if (h->plan.dist(s) && std::binary_search(h->plan.group[s].begin(), h->plan.group[s].end(), h->rank)) ++c;
+    return c;
+  }
   if (k == "repivots") return (double)h->repivots;
   if (k.rfind("launches_", 0) == 0) {   // launches per kernel variant in the factor schedule
     const std::string v = k.substr(9);
@@ -2319,167 +3176,89 @@ int smlu_plan_supernodes(const smlu_plan* pl, int64_t* first, int64_t* parent, i
 
 void smlu_plan_destroy(smlu_plan* p) { delete p; }
 
-// ---- multi-GPU partition (one process per GPU; exchanges driven by the caller) ----------
+// ---- multi-GPU partition (one process per GPU; collective; transport supplied or RCCL) ----
 int smlu_dist_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
-                     const smlu_opts* opts, int32_t rank, int32_t nranks, smlu_handle** out) {
+                     const smlu_opts* opts, int32_t rank, int32_t nranks, const smlu_transport* tr,
+                     smlu_handle** out) {
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(nullptr, SMLU_ERR_ARG, "bad rank/nranks");
-  return create_impl(n, colptr, rowval, nzval, nullptr, nullptr, nullptr, opts, out, rank, nranks);
+  if (nranks > 1 && (!tr || !tr->exchange || !tr->bcast || !tr->allreduce_max))
+    return fail(nullptr, SMLU_ERR_ARG, "a partitioned handle needs a complete transport");
+  return create_impl(n, colptr, rowval, nzval, nullptr, nullptr, nullptr, opts, out, rank, nranks, tr);
 }
 
-int64_t smlu_dist_nsegments(const smlu_handle* h) { return h ? (int64_t)h->fac_seg.size() : -1; }
-
-int smlu_dist_set_values(smlu_handle* h, const double* nzval, int32_t on_device) {
-  if (!h || !nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
-  HIPCHK(hipSetDevice(h->device));
-  HIPCHK(hipMemcpyAsync(h->A.p, nzval, sizeof(double) * h->plan.nnzA,
-                        on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+int smlu_rccl_unique_id(uint8_t id[128]) {
+  if (!id) return fail(nullptr, SMLU_ERR_ARG, "NULL id");
+  RcclApi* R = rccl_api();
+  if (!R) return fail(nullptr, SMLU_ERR_HIP, "librccl not loadable");
+  ncclUniqueId u;
+  if (R->GetUniqueId(&u) != ncclSuccess) return fail(nullptr, SMLU_ERR_HIP, "ncclGetUniqueId failed");
+  std::memcpy(id, &u, sizeof(u) < 128 ? sizeof(u) : 128);
   return SMLU_OK;
 }
 
-int smlu_dist_factor_segment(smlu_handle* h, int32_t seg) {
-  if (!h || seg < 0 || (size_t)seg >= h->fac_seg.size()) return fail(h, SMLU_ERR_ARG, "bad segment");
-  HIPCHK(hipSetDevice(h->device));
-  static thread_local std::chrono::steady_clock::time_point t0;
-  if (seg == 0) {
-    t0 = std::chrono::steady_clock::now();
-    for (auto& v : h->kind_ms) v = 0;
+int smlu_dist_create_rccl(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
+                          const smlu_opts* opts, int32_t rank, int32_t nranks, const uint8_t id[128],
+                          smlu_handle** out) {
+  if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail(nullptr, SMLU_ERR_ARG, "bad arguments");
+  RcclApi* R = rccl_api();
+  if (!R) return fail(nullptr, SMLU_ERR_HIP, "librccl not loadable");
+  const int dev = opts ? opts->device : 0;
+  if (hipSetDevice(dev) != hipSuccess) return fail(nullptr, SMLU_ERR_NODEVICE, "hipSetDevice failed");
+  auto* st = new (std::nothrow) RcclState();
+  if (!st) return fail(nullptr, SMLU_ERR_ALLOC, "allocation failed");
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u) < 128 ? sizeof(u) : 128);
+  if (R->CommInitRank(&st->comm, nranks, u, rank) != ncclSuccess) {
+    delete st;
+    return fail(nullptr, SMLU_ERR_HIP, "ncclCommInitRank failed");
   }
-  Timer tm(h);
-  int rc = factor_segment(h, tm, seg);
-  if (rc != SMLU_OK) return rc;
-  if ((size_t)seg + 1 == h->fac_seg.size()) return finish_factor(h, tm, t0);
-  HIPCHK(hipStreamSynchronize(h->stream));
-  return SMLU_OK;
+  st->rank = rank;
+  smlu_transport tr{};
+  tr.ctx = st;
+  tr.device_memory = 1;
+  tr.exchange = rccl_exchange;
+  tr.bcast = rccl_bcast;
+  tr.allreduce_max = rccl_allreduce_max;
+  return create_impl(n, colptr, rowval, nzval, nullptr, nullptr, nullptr, opts, out, rank, nranks, &tr, st);
 }
 
-int smlu_dist_solve_segment(smlu_handle* h, const double* d_b, double* d_x, int32_t phase, int32_t seg) {
-  if (!h) return fail(nullptr, SMLU_ERR_ARG, "NULL handle");
-  if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
-  HIPCHK(hipSetDevice(h->device));
-  hipStream_t st = h->stream;
-  double* w = h->wrk.p;
-  if (phase == 0 || phase == 1) {
-    const std::vector<size_t>& sg = phase == 0 ? h->fwd_seg : h->bwd_seg;
-    const std::vector<Launch>& ls = phase == 0 ? h->fwd : h->bwd;
-    if (seg < 0 || (size_t)seg >= sg.size()) return fail(h, SMLU_ERR_ARG, "bad segment");
-    if (phase == 0 && seg == 0) {
-      if (!d_b) return fail(h, SMLU_ERR_ARG, "NULL b");
-      HIPCHK(launch_perm_in(st, h->plan.n, h->p0.p, h->Rs.p, d_b, w));
-    }
-    const size_t hi = (size_t)seg + 1 < sg.size() ? sg[seg + 1] : ls.size();
-    for (size_t i = sg[seg]; i < hi; ++i) HIPCHK(run_solve_launch(h, ls[i], w));
-  } else if (phase == 2) {
-    if (!d_x) return fail(h, SMLU_ERR_ARG, "NULL x");
-    if (h->nranks > 1) HIPCHK(launch_perm_out_masked(st, h->plan.n, h->q.p, h->rowown.p, w, d_x));
-    else HIPCHK(launch_perm_out(st, h->plan.n, h->q.p, w, d_x));
-  } else {
-    return fail(h, SMLU_ERR_ARG, "bad phase");
-  }
-  HIPCHK(hipStreamSynchronize(st));
-  return SMLU_OK;
-}
-
-// Exchange before segment `seg` (>= 1) of kind 0 (factor: child update blocks), 1 (forward
-// solve: child update vectors) or 2 (backward solve: solution rows, every rank to every rank).
-static double* dist_base(smlu_handle* h, int kind) {
-  return kind == 0 ? h->scratch.p : kind == 1 ? h->vbuf.p : h->wrk.p;
-}
-
-static bool dist_point(const smlu_handle* h, int kind, int seg, size_t* k) {
-  const size_t nx = h->xfac.size();
-  if (seg < 1 || (size_t)seg > nx || kind < 0 || kind > 2) return false;
-  *k = kind == 2 ? nx - (size_t)seg : (size_t)seg - 1;
-  return true;
-}
-
-int smlu_dist_xsizes(smlu_handle* h, int32_t kind, int32_t seg, int64_t* send, int64_t* recv) {
-  if (!h || !send || !recv) return fail(h, SMLU_ERR_ARG, "NULL argument");
-  size_t k;
-  if (!dist_point(h, kind, seg, &k)) return fail(h, SMLU_ERR_ARG, "bad exchange point");
-  for (int r = 0; r < h->nranks; ++r) send[r] = recv[r] = 0;
-  if (kind < 2) {
-    for (auto& b : (kind == 0 ? h->xfac : h->xfwd)[k]) {
-      if (b.src == h->rank) send[b.dst] += b.cnt;
-      if (b.dst == h->rank) recv[b.src] += b.cnt;
-    }
-  } else {
-    for (int r = 0; r < h->nranks; ++r) {
-      int64_t c = 0;
-      for (auto& rg : h->xbwd[k][r]) c += rg.second;
-      if (r == h->rank) {
-        for (int d = 0; d < h->nranks; ++d)
-          if (d != r) send[d] = c;
-      } else {
-        recv[r] = c;
-      }
-    }
-  }
-  return SMLU_OK;
-}
-
-int smlu_dist_pack(smlu_handle* h, int32_t kind, int32_t seg, double* d_buf) {
-  if (!h) return fail(nullptr, SMLU_ERR_ARG, "NULL handle");
-  size_t k;
-  if (!dist_point(h, kind, seg, &k)) return fail(h, SMLU_ERR_ARG, "bad exchange point");
-  HIPCHK(hipSetDevice(h->device));
-  hipStream_t st = h->stream;
-  const double* base = dist_base(h, kind);
-  int64_t o = 0;
-  if (kind < 2) {   // blocks in (dst, child) order
-    for (auto& b : (kind == 0 ? h->xfac : h->xfwd)[k])
-      if (b.src == h->rank) {
-        HIPCHK(hipMemcpyAsync(d_buf + o, base + b.off, sizeof(double) * b.cnt, hipMemcpyDeviceToDevice, st));
-        o += b.cnt;
-      }
-  } else {          // this rank's rows, once (the caller sends the same buffer to every rank)
-    for (auto& rg : h->xbwd[k][h->rank]) {
-      HIPCHK(hipMemcpyAsync(d_buf + o, base + rg.first, sizeof(double) * rg.second, hipMemcpyDeviceToDevice, st));
-      o += rg.second;
-    }
-  }
-  HIPCHK(hipStreamSynchronize(st));
-  return SMLU_OK;
-}
-
-int smlu_dist_unpack(smlu_handle* h, int32_t kind, int32_t seg, const double* d_buf) {
-  if (!h) return fail(nullptr, SMLU_ERR_ARG, "NULL handle");
-  size_t k;
-  if (!dist_point(h, kind, seg, &k)) return fail(h, SMLU_ERR_ARG, "bad exchange point");
-  HIPCHK(hipSetDevice(h->device));
-  hipStream_t st = h->stream;
-  double* base = dist_base(h, kind);
-  int64_t o = 0;
-  if (kind < 2) {   // blocks in (src, child) order
-    for (auto& b : (kind == 0 ? h->xfac : h->xfwd)[k])
-      if (b.dst == h->rank) {
-        HIPCHK(hipMemcpyAsync(base + b.off, d_buf + o, sizeof(double) * b.cnt, hipMemcpyDeviceToDevice, st));
-        o += b.cnt;
-      }
-  } else {          // other ranks' rows in rank order
-    for (int r = 0; r < h->nranks; ++r) {
-      if (r == h->rank) continue;
-      for (auto& rg : h->xbwd[k][r]) {
-        HIPCHK(hipMemcpyAsync(base + rg.first, d_buf + o, sizeof(double) * rg.second, hipMemcpyDeviceToDevice, st));
-        o += rg.second;
-      }
-    }
-  }
-  HIPCHK(hipStreamSynchronize(st));
-  return SMLU_OK;
-}
-
-int smlu_plan_partition(const smlu_plan* plan, int32_t nparts, int32_t* owner, int32_t* xlevels,
-                        int64_t* nx) {
+int smlu_plan_partition(const smlu_plan* plan, int32_t nparts, int32_t* owner, int64_t* nshared) {
   if (!plan || nparts < 1) return fail(nullptr, SMLU_ERR_ARG, "invalid arguments");
   Plan P = plan->plan;   // copy: the partition is a query
-  P.compute_owners(nparts);
-  if (owner)
-    for (int64_t s = 0; s < P.nsup; ++s) owner[s] = P.owner[s];
-  if (xlevels)
-    for (size_t i = 0; i < P.xlevels.size(); ++i) xlevels[i] = P.xlevels[i];
-  if (nx) *nx = (int64_t)P.xlevels.size();
+  P.compute_owners(nparts, kOBDefault);
+  int64_t k = 0;
+  for (int64_t s = 0; s < P.nsup; ++s) {
+    if (owner) owner[s] = P.owner[s];
+    if (P.dist(s)) ++k;
+  }
+  if (nshared) *nshared = k;
   return SMLU_OK;
+}
+
+int smlu_plan_rank_memory(const smlu_plan* plan, int32_t nparts, int32_t rank, double* store_bytes,
+                          double* scratch_bytes, double* stage_bytes) {
+  if (!plan || nparts < 1 || rank < 0 || rank >= nparts) return fail(nullptr, SMLU_ERR_ARG, "invalid arguments");
+  Plan P = plan->plan;
+  P.compute_owners(nparts, kOBDefault);
+  RankLayout Y;
+  if (nparts > 1) {
+    rank_layout(P, rank, Y);
+  } else {
+    Y.store_size = P.factor_size;
+    Y.scratch_size = P.scratch_size;
+  }
+  if (store_bytes) *store_bytes = 8.0 * (double)Y.store_size;
+  if (scratch_bytes) *scratch_bytes = 8.0 * (double)Y.scratch_size;
+  if (stage_bytes) *stage_bytes = 8.0 * (double)Y.stage_size * (nparts > 1 ? 3 : 0);   // block buffer + 2 staging
+  return SMLU_OK;
+}
+
+double smlu_plan_project(const smlu_plan* plan, int32_t nparts, double tflops, double gbs, double lat_us,
+                         double* t1) {
+  if (!plan || nparts < 1) return std::numeric_limits<double>::quiet_NaN();
+  Plan P = plan->plan;
+  P.compute_owners(nparts, kOBDefault);
+  return project_partition(P, tflops, gbs, lat_us, t1);
 }
 
 const char* smlu_version(void) { return "smlu 0.1.0 (gfx950, fp64, multifrontal)"; }

@@ -84,15 +84,12 @@ SIGNATURES = {
     "smlu_plan_supernodes": (i32, [vp, vp, vp, vp]),
     "smlu_plan_destroy": (None, [vp]),
     "smlu_version": (ctypes.c_char_p, []),
-    "smlu_dist_create": (i32, [i64, vp, vp, vp, ctypes.POINTER(SmluOpts), i32, i32, ctypes.POINTER(vp)]),
-    "smlu_dist_nsegments": (i64, [vp]),
-    "smlu_dist_set_values": (i32, [vp, vp, i32]),
-    "smlu_dist_factor_segment": (i32, [vp, i32]),
-    "smlu_dist_solve_segment": (i32, [vp, vp, vp, i32, i32]),
-    "smlu_dist_xsizes": (i32, [vp, i32, i32, vp, vp]),
-    "smlu_dist_pack": (i32, [vp, i32, i32, vp]),
-    "smlu_dist_unpack": (i32, [vp, i32, i32, vp]),
-    "smlu_plan_partition": (i32, [vp, i32, vp, vp, i64p]),
+    "smlu_dist_create": (i32, [i64, vp, vp, vp, ctypes.POINTER(SmluOpts), i32, i32, vp, ctypes.POINTER(vp)]),
+    "smlu_rccl_unique_id": (i32, [vp]),
+    "smlu_dist_create_rccl": (i32, [i64, vp, vp, vp, ctypes.POINTER(SmluOpts), i32, i32, vp, ctypes.POINTER(vp)]),
+    "smlu_plan_partition": (i32, [vp, i32, vp, i64p]),
+    "smlu_plan_rank_memory": (i32, [vp, i32, i32, f64p, f64p, f64p]),
+    "smlu_plan_project": (f64, [vp, i32, f64, f64, f64, f64p]),
 }
 
 _lib = None
@@ -120,6 +117,23 @@ def lib():
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+# smlu_transport (include/smlu.h): callbacks of a caller-supplied transport between ranks
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, vp, i32, ctypes.POINTER(i32), ctypes.POINTER(vp),
+                               ctypes.POINTER(i64), ctypes.POINTER(vp), ctypes.POINTER(i64), vp)
+BCAST_FN = ctypes.CFUNCTYPE(ctypes.c_int, vp, vp, i64, i32, i32, ctypes.POINTER(i32), vp)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, vp, ctypes.POINTER(f64), i32)
+
+
+class SmluTransport(ctypes.Structure):
+    _fields_ = [
+        ("ctx", vp),
+        ("device_memory", i32),
+        ("exchange", EXCHANGE_FN),
+        ("bcast", BCAST_FN),
+        ("allreduce_max", ALLREDUCE_FN),
+    ]
 
 
 def default_opts(**kw) -> SmluOpts:

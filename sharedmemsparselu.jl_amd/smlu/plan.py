@@ -61,15 +61,31 @@ class Plan:
         return first, parent, level
 
     def partition(self, nparts):
-        """(owner per supernode, exchange-point levels) of an `nparts`-rank dist handle."""
+        """Owner rank per supernode of an `nparts`-rank partitioned handle (-1: a front shared
+        by several ranks as a block-cyclic column partition) and the number of shared fronts."""
         ns = int(self.stat("nsuper"))
         owner = np.empty(ns, np.int32)
-        xl = np.empty(int(self.stat("nlevels")) + 1, np.int32)
-        nx = ctypes.c_int64()
-        rc = C.lib().smlu_plan_partition(self._h, int(nparts), C.ptr(owner), C.ptr(xl), ctypes.byref(nx))
+        nsh = ctypes.c_int64()
+        rc = C.lib().smlu_plan_partition(self._h, int(nparts), C.ptr(owner), ctypes.byref(nsh))
         if rc != 0:
             raise RuntimeError(f"smlu_plan_partition failed ({rc}): {C.last_error(None)}")
-        return owner, xl[:nx.value].copy()
+        return owner, int(nsh.value)
+
+    def rank_memory(self, nparts, rank):
+        """Device bytes rank `rank` of `nparts` allocates: (factor store, scratch, staging)."""
+        a, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        rc = C.lib().smlu_plan_rank_memory(self._h, int(nparts), int(rank), ctypes.byref(a), ctypes.byref(b),
+                                           ctypes.byref(c))
+        if rc != 0:
+            raise RuntimeError(f"smlu_plan_rank_memory failed ({rc}): {C.last_error(None)}")
+        return a.value, b.value, c.value
+
+    def project(self, nparts, tflops=50.0, gbs=50.0, lat_us=30.0):
+        """Projected partitioned factorization time (s) and the one-GPU time of the same model."""
+        t1 = ctypes.c_double()
+        t = C.lib().smlu_plan_project(self._h, int(nparts), float(tflops), float(gbs), float(lat_us),
+                                      ctypes.byref(t1))
+        return t, t1.value
 
     def front_flops(self):
         """Dense flops per supernode (the partition's work model)."""

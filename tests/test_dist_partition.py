@@ -1,5 +1,7 @@
-"""Host-side checks of the multi-GPU partition: proportional mapping of the
-assembly tree onto ranks (smlu_plan_partition), no GPU needed."""
+"""Host-side checks of the multi-GPU partition, no GPU needed: subtrees of the
+assembly tree per rank, the fronts above them shared by their ranks as a 1D block-cyclic column
+partition (smlu_plan_partition), each rank's device allocation (smlu_plan_rank_memory) and the
+critical-path projection (smlu_plan_project)."""
 import numpy as np
 import pytest
 
@@ -7,52 +9,62 @@ import smlu
 from smlu import matrices as mats
 
 
-def _tree(P):
-    first, parent, level = P.supernodes()
-    return first, parent, level
-
-
 @pytest.mark.parametrize("nparts", [1, 2, 3, 4, 8])
-def test_partition_covers_tree_and_exchange_levels(nparts):
+def test_partition_owners_and_shared_fronts(nparts):
     A = mats.poisson3d(14)
     P = smlu.Plan(A)
-    first, parent, level = _tree(P)
-    owner, xl = P.partition(nparts)
+    first, parent, level = P.supernodes()
+    owner, nshared = P.partition(nparts)
     ns = len(parent)
     assert owner.shape == (ns,)
-    assert owner.min() >= 0 and owner.max() < nparts
+    assert owner.min() >= -1 and owner.max() < nparts
     if nparts == 1:
-        assert (owner == 0).all() and xl.size == 0
+        assert (owner == 0).all() and nshared == 0
         return
-    # every rank gets work
-    assert set(np.unique(owner)) == set(range(nparts))
-    # exchange levels are exactly the levels of fronts with a child on another rank
-    expect = sorted({int(level[parent[s]]) for s in range(ns)
-                     if parent[s] >= 0 and owner[parent[s]] != owner[s]})
-    assert list(xl) == expect
-    # a subtree owned by a single rank stays on it: below the exchange fronts ownership is
-    # inherited, i.e. a child differs from its parent only where the parent's rank set splits
-    crossings = sum(1 for s in range(ns) if parent[s] >= 0 and owner[parent[s]] != owner[s])
-    assert crossings >= nparts - 1
+    assert nshared == int((owner == -1).sum()) and nshared >= 1
+    # every rank owns subtree work
+    assert set(np.unique(owner[owner >= 0])) == set(range(nparts))
+    # a shared front's parent is shared too (groups only grow towards the root), and an
+    # ordinary front's parent is either on the same rank or shared
+    for s in range(ns):
+        p = parent[s]
+        if p < 0:
+            continue
+        if owner[s] == -1:
+            assert owner[p] == -1
+        else:
+            assert owner[p] in (owner[s], -1)
 
 
-def test_partition_balances_subtree_work():
+def test_rank_memory_splits_the_factor_store():
     A = mats.poisson3d(20)
     P = smlu.Plan(A)
-    w = P.front_flops()
-    owner, _ = P.partition(4)
-    first, parent, level = _tree(P)
-    # work of the fronts below the top separators, per rank: within a factor 2.5 of the mean
-    top = {int(s) for s in range(len(parent)) if parent[s] >= 0 and owner[parent[s]] != owner[s]}
-    load = np.zeros(4)
-    for s in range(len(parent)):
-        load[owner[s]] += w[s]
-    assert load.max() <= 2.5 * load.mean(), load
-    assert len(top) >= 3
+    one = P.rank_memory(1, 0)
+    for nparts in (2, 4):
+        mem = [P.rank_memory(nparts, r) for r in range(nparts)]
+        store = sum(m[0] for m in mem)
+        # every factor entry lives on exactly one rank (block padding aside)
+        assert 0.98 * one[0] <= store <= 1.05 * one[0] + 1e6
+        assert max(m[0] for m in mem) < one[0]
+        assert all(m[2] > 0 for m in mem)
+
+
+def test_projection_scales_on_the_3d_model():
+    A = mats.poisson3d(48)
+    P = smlu.Plan(A)
+    t1s = []
+    for nparts in (1, 2, 4):
+        t, t1 = P.project(nparts, tflops=50.0, gbs=100.0, lat_us=20.0)
+        t1s.append(t1)
+        if nparts == 1:
+            assert t == pytest.approx(t1)
+        else:
+            assert t < t1
+    assert len(set(round(x, 9) for x in t1s)) == 1
 
 
 def test_partition_is_deterministic():
     A = mats.poisson3d(12)
-    o1, x1 = smlu.Plan(A).partition(4)
-    o2, x2 = smlu.Plan(A).partition(4)
-    assert np.array_equal(o1, o2) and np.array_equal(x1, x2)
+    o1, k1 = smlu.Plan(A).partition(4)
+    o2, k2 = smlu.Plan(A).partition(4)
+    assert np.array_equal(o1, o2) and k1 == k2

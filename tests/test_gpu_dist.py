@@ -1,8 +1,9 @@
-"""Multi-GPU partition on one GPU: 2 and 4 ranks (processes) share cuda:0 and
-exchange through gloo (host memory); production runs use RCCL with one GPU per rank (same code
-path in smlu/dist.py apart from the transport).  Each rank factors its subtrees, fronts above
-receive their children's update blocks at the exchange points; the solution must match the
-single-GPU factorization to rounding and solve A x = b to the reference tolerance."""
+"""Multi-GPU partition rehearsed on one GPU: 2, 3 and 4 ranks (processes) share
+cuda:0 and the library drives its transfers through the host-memory transport over gloo
+(smlu/dist.py HostTransport); production runs use the library's RCCL transport with one GPU per
+rank (same schedule, same packing, only the transfer calls differ).  Subtrees per rank, shared
+top fronts as block-cyclic column partitions; the solution must match the single-GPU
+factorization to rounding and solve A x = b to the reference tolerance on every rank."""
 import os
 import socket
 
@@ -21,19 +22,29 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, which, q):
+def _matrix(which):
+    import scipy.sparse as sp
+    from smlu import matrices as mats
+    if which == "poisson":
+        return sp.csc_matrix(mats.poisson3d(14))
+    if which == "poisson_big":
+        return sp.csc_matrix(mats.poisson3d(24))
+    return sp.csc_matrix(mats.random_dominant(3000, 0.003, seed=5))
+
+
+def _worker(rank, world, port, which, ob, q):
     try:
         import scipy.sparse as sp
         import torch
         import torch.distributed as dist
         import smlu
-        from smlu import matrices as mats
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
+        if ob:
+            os.environ["SMLU_OB"] = str(ob)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
-        A = mats.poisson3d(14) if which == "poisson" else mats.random_dominant(3000, 0.003, seed=5)
-        A = sp.csc_matrix(A)
+        A = _matrix(which)
         n = A.shape[0]
         F = smlu.DistributedSparseLU(A, device=0)
         b = np.random.default_rng(11).random(n)
@@ -49,34 +60,34 @@ def _worker(rank, world, port, which, q):
         F.refactor_device(torch.from_numpy(np.ascontiguousarray(A2.data)).cuda())
         F.solve_device(dx, db)
         x2 = dx.cpu().numpy()
-        q.put((rank, x1, x2, F.nseg, None))
+        info = {k: F.stat(k) for k in ("shared_fronts", "owned_blocks", "comm_steps")}
+        q.put((rank, x1, x2, info, None))
         F.close()
         dist.destroy_process_group()
-    except Exception as e:  # report instead of hanging the parent
+    except Exception:  # report instead of hanging the parent
         import traceback
-        q.put((rank, None, None, 0, traceback.format_exc()))
+        q.put((rank, None, None, None, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world,which", [(2, "poisson"), (4, "poisson"), (3, "random")])
-def test_dist_factor_solve_matches_single_gpu(world, which):
+@pytest.mark.parametrize("world,which,ob", [(2, "poisson", 0), (4, "poisson", 0), (3, "random", 0),
+                                            (2, "poisson_big", 128), (4, "poisson_big", 64)])
+def test_dist_factor_solve_matches_single_gpu(world, which, ob):
     import scipy.sparse as sp
     import smlu
-    from smlu import matrices as mats
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, which, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, which, ob, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=600) for _ in ps]
+    res = [q.get(timeout=240) for _ in ps]
     for p in ps:
         p.join(timeout=120)
     errs = [r[4] for r in res if r[4]]
     assert not errs, errs[0]
     for p in ps:
         assert p.exitcode == 0
-    A = mats.poisson3d(14) if which == "poisson" else mats.random_dominant(3000, 0.003, seed=5)
-    A = sp.csc_matrix(A)
+    A = _matrix(which)
     n = A.shape[0]
     b = np.random.default_rng(11).random(n)
     A2 = A.copy()
@@ -89,7 +100,9 @@ def test_dist_factor_solve_matches_single_gpu(world, which):
     xs2 = np.empty(n)
     smlu.ldiv_(xs2, F, b)
     F.close()
-    assert res[0][3] > 1, "partition produced no exchange point"
+    # the partition really shares fronts between ranks and moves data
+    assert max(r[3]["shared_fronts"] for r in res) >= 1
+    assert all(r[3]["comm_steps"] >= 1 for r in res)
     for rank, x1, x2, _, _ in res:
         # every rank holds the full solution
         assert np.allclose(x1, xs1, rtol=1e-11, atol=1e-13), (rank, np.abs(x1 - xs1).max())
@@ -102,7 +115,8 @@ def test_dist_factor_solve_matches_single_gpu(world, which):
 def _weak_matrix():
     """Two 600-pivot dense blocks with tiny 64x64 diagonal tiles (weak diagonal-tile pivots),
     coupled only through a 64-column separator: under the natural order the assembly tree has
-    two 600-column fronts below the separator front, so two ranks each factor one block."""
+    two 600-column fronts below the separator front, so two ranks each factor one block and
+    share the separator front."""
     import scipy.sparse as sp
     rng = np.random.default_rng(21)
     m, k = 600, 64
@@ -139,7 +153,7 @@ def _weak_worker(rank, world, port, q):
         b = torch.from_numpy(np.random.default_rng(4).random(n)).cuda()
         x = torch.empty_like(b)
         F.solve_device(x, b)
-        q.put((rank, x.cpu().numpy(), F.weak, F.refine_steps, F.status, F.nseg, None))
+        q.put((rank, x.cpu().numpy(), F.weak, F.refine_steps, F.status, F.stat("shared_fronts"), None))
         F.close()
         dist.destroy_process_group()
     except Exception:
@@ -148,15 +162,15 @@ def _weak_worker(rank, world, port, q):
 
 
 def test_dist_weak_pivots_refine():
-    # weak pivots on any rank are summed over the partition (status SMLU_PIVOT_WEAK on every
-    # rank) and the partitioned solve refines, as the single-GPU solve does
+    # weak pivots on any rank are reduced over the partition (every rank sees them) and the
+    # partitioned solve refines, as the single-GPU solve does
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_weak_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=600) for _ in ps]
+    res = [q.get(timeout=240) for _ in ps]
     for p in ps:
         p.join(timeout=120)
     errs = [r[6] for r in res if r[6]]
@@ -165,7 +179,7 @@ def test_dist_weak_pivots_refine():
     b = np.random.default_rng(4).random(D.shape[0])
     xr = np.linalg.solve(D, b)
     ctol = max(1e-10, 8 * np.finfo(float).eps * np.linalg.cond(D))
-    for rank, x, weak, steps, status, nseg, _ in res:
-        assert nseg > 1
-        assert weak > 0 and status == 2 and steps >= 1, (rank, weak, status, steps)
+    for rank, x, weak, steps, status, shared, _ in res:
+        assert shared >= 1
+        assert weak > 0 and steps >= 1, (rank, weak, status, steps)
         assert np.linalg.norm(x - xr) <= ctol * np.linalg.norm(xr), rank
