@@ -51,8 +51,15 @@ __device__ __forceinline__ double wave_max(double v) {
 }
 
 __device__ __forceinline__ void atomic_max_pos(double* addr, double v) {
-  // v >= 0: IEEE ordering of non-negative doubles matches their bit patterns as u64
-  atomicMax(reinterpret_cast<unsigned long long*>(addr), (unsigned long long)__double_as_longlong(v));
+  // v >= 0: IEEE ordering of non-negative doubles matches their bit patterns as u64.  The
+  // stored maximum is read first and the atomic skipped when it already covers v: every front
+  // reports into the same word, and same-address atomics serialise in L2 (they made the
+  // hundred-thousand-front small-front levels atomic-bound).  The maximum only grows, so a
+  // stale read costs at most one unneeded atomic.
+  unsigned long long* p = reinterpret_cast<unsigned long long*>(addr);
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  if (b <= __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+  atomicMax(p, b);
 }
 
 // info word per front: bit0 zero pivot, bit1 weak pivot, bits 2.. = 1 + first zero-pivot column

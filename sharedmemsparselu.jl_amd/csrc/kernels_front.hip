@@ -146,36 +146,68 @@ __device__ __forceinline__ int choose_pivot(double akk, double amax, int arg, in
 }
 
 // ------------------------------------------------------------------------------------
-// Small fronts (M <= 128): the whole front in LDS, one 256-thread workgroup per front.
-// Right-looking partial LU over the ns fully-summed columns with pivot search over the
-// fully-summed rows; the trailing F22 block receives its Schur update in the same pass.
+// Small fronts (M <= 128), assembly fused with the factorization: the whole front is built in
+// LDS (zeros, the scaled A entries, each child's F22 block added in child order -- per element
+// the order k_assemble uses), factored there, and written to L / U12 / F22 once; the front
+// never makes an HBM round trip between assembly and factorization, and the small fronts need
+// no k_assemble columns.  One workgroup of NW waves per front (NW = 1 for M <= 32, 2 for
+// M <= 64, 4 above).  Right-looking partial LU over the ns fully-summed columns with pivot
+// search over the fully-summed rows; the trailing F22 block receives its Schur update in the
+// same pass.  list: (front, first A entry, A entry count) per front; A entries as (entry id,
+// local column << 16 | local row).  The growth maximum is reduced over the front's columns and
+// reported once.
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_front_lds(const int32_t* __restrict__ list,
-                                                   const SNode* __restrict__ sn,
-                                                   double* __restrict__ store,
-                                                   double* __restrict__ scratch,
-                                                   int32_t* __restrict__ rowperm,
-                                                   int32_t* __restrict__ info,
-                                                   double* __restrict__ growth, double diag_tol,
-                                                   double piv_tol) {
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_front_small(const int32_t* __restrict__ list,
+                                                         const SNode* __restrict__ sn,
+                                                         const int32_t* __restrict__ chlist,
+                                                         const int32_t* __restrict__ relmap,
+                                                         const int2* __restrict__ aents,
+                                                         const double* __restrict__ a,
+                                                         const int32_t* __restrict__ arow,
+                                                         const double* __restrict__ Rs,
+                                                         double* __restrict__ store,
+                                                         double* __restrict__ scratch,
+                                                         int32_t* __restrict__ rowperm,
+                                                         int32_t* __restrict__ info,
+                                                         double* __restrict__ growth, double diag_tol,
+                                                         double piv_tol) {
+  constexpr int NT = 64 * NW;
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int s_perm[128];
   __shared__ int s_piv;
-  __shared__ int s_flag;
-  __shared__ int s_err;
-  const int sid = list[blockIdx.x];
+  const int sid = list[3 * blockIdx.x];
+  const int64_t a0 = list[3 * blockIdx.x + 1];
+  const int acnt = list[3 * blockIdx.x + 2];
   const SNode s = sn[sid];
   FrontPtrs f = front_ptrs(s, store, scratch);
   const int M = (int)f.M, ns = (int)f.ns;
   const int ld = M | 1;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // load
-  for (int j = wv; j < M; j += 4) {
-    for (int i = lane; i < M; i += 64) lds[j * ld + i] = *fel(f, i, j);
-  }
-  for (int i = tid; i < ns; i += 256) s_perm[i] = i;
-  if (tid == 0) { s_flag = 0; s_err = -1; }
+  // assembly
+  for (int e = tid; e < M * ld; e += NT) lds[e] = 0.0;
+  for (int i = tid; i < ns; i += NT) s_perm[i] = i;
   __syncthreads();
+  for (int e = tid; e < acnt; e += NT) {
+    const int2 en = aents[a0 + e];
+    lds[(en.y >> 16) * ld + (en.y & 0xffff)] = Rs[arow[en.x]] * a[en.x];
+  }
+  __syncthreads();
+  for (int q = s.chbeg; q < s.chend; ++q) {
+    const SNode c = sn[chlist[q]];
+    const int nuc = c.nu;
+    if (nuc == 0) continue;
+    const int32_t* rm = relmap + c.rowptr;
+    const gdbl* src = gbl(scratch + c.Foff);
+    for (int jc = wv; jc < nuc; jc += NW) {
+      double* col = lds + rm[jc] * ld;
+      for (int i = lane; i < nuc; i += 64) col[rm[i]] += src[(int64_t)jc * nuc + i];
+    }
+    __syncthreads();
+  }
+  // factorization
+  int flag = 0, err = -1;   // wave 0, lane 0
+  double gmax = 0.0;
   for (int k = 0; k < ns; ++k) {
     if (wv == 0) {
       double am = -1.0, amo = 0.0;
@@ -194,11 +226,11 @@ __global__ __launch_bounds__(256) void k_front_lds(const int32_t* __restrict__ l
         int piv = choose_pivot(lds[k * ld + k], am, ai, k, diag_tol);
         double pv = fabs(lds[k * ld + piv]);
         if (am <= 0.0) {
-          s_flag |= 1;
-          if (s_err < 0) s_err = k;
+          flag |= 1;
+          if (err < 0) err = k;
         } else {
-          if (pv < piv_tol * fmax(am, amo)) s_flag |= 2;
-          atomic_max_pos(&growth[0], fmax(am, amo) / pv);
+          if (pv < piv_tol * fmax(am, amo)) flag |= 2;
+          gmax = fmax(gmax, fmax(am, amo) / pv);
         }
         s_piv = piv;
       }
@@ -206,7 +238,7 @@ __global__ __launch_bounds__(256) void k_front_lds(const int32_t* __restrict__ l
     __syncthreads();
     const int piv = s_piv;
     if (piv != k) {
-      for (int j = tid; j < M; j += 256) {
+      for (int j = tid; j < M; j += NT) {
         double t = lds[j * ld + k];
         lds[j * ld + k] = lds[j * ld + piv];
         lds[j * ld + piv] = t;
@@ -219,9 +251,9 @@ __global__ __launch_bounds__(256) void k_front_lds(const int32_t* __restrict__ l
       __syncthreads();
     }
     const double pinv = recip(lds[k * ld + k]);
-    for (int i = k + 1 + tid; i < M; i += 256) lds[k * ld + i] = lds[k * ld + i] * pinv;
+    for (int i = k + 1 + tid; i < M; i += NT) lds[k * ld + i] = lds[k * ld + i] * pinv;
     __syncthreads();
-    for (int j = k + 1 + wv; j < M; j += 4) {
+    for (int j = k + 1 + wv; j < M; j += NW) {
       const double u = lds[j * ld + k];
       if (u != 0.0)
         for (int i = k + 1 + lane; i < M; i += 64)
@@ -229,12 +261,15 @@ __global__ __launch_bounds__(256) void k_front_lds(const int32_t* __restrict__ l
     }
     __syncthreads();
   }
-  // store
-  for (int j = wv; j < M; j += 4) {
+  // store: L panel, U12 and F22 are each one contiguous column-major block
+  for (int j = wv; j < M; j += NW) {
     for (int i = lane; i < M; i += 64) *fel(f, i, j) = lds[j * ld + i];
   }
-  for (int i = tid; i < ns; i += 256) rowperm[s.first + i] = s_perm[i];
-  if (tid == 0 && s_flag) publish_info(info + sid, s_flag, s_err);
+  for (int i = tid; i < ns; i += NT) rowperm[s.first + i] = s_perm[i];
+  if (tid == 0) {
+    if (flag) publish_info(info + sid, flag, err);
+    if (gmax > 0.0) atomic_max_pos(&growth[0], gmax);
+  }
 }
 
 
@@ -1072,9 +1107,12 @@ static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / 
 
 // Dynamic LDS above 64 KiB must be enabled per kernel before launch (and before any capture).
 hipError_t init_kernel_attributes() {
-  hipError_t e = hipFuncSetAttribute((const void*)k_front_lds, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
-  if (e != hipSuccess) return e;
-  return e;
+  const void* fs[3] = {(const void*)k_front_small<1>, (const void*)k_front_small<2>, (const void*)k_front_small<4>};
+  for (const void* k : fs) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 hipError_t launch_rowscale(hipStream_t st, int64_t n, const int64_t* rowptr, const int32_t* ent,
@@ -1096,12 +1134,18 @@ hipError_t launch_assemble(hipStream_t st, int64_t ntasks, const XCol* cols, con
                                                             Rs, store, scratch);
   return hipGetLastError();
 }
-hipError_t launch_front_lds(hipStream_t st, int cnt, int Mmax, const int32_t* list, const SNode* sn,
-                            double* store, double* scratch, int32_t* rowperm, int32_t* info,
-                            double* growth, double diag_tol, double piv_tol) {
+hipError_t launch_front_small(hipStream_t st, int cnt, int Mmax, const int32_t* list, const SNode* sn,
+                              const int32_t* chlist, const int32_t* relmap, const int2* aents, const double* a,
+                              const int32_t* arow, const double* Rs, double* store, double* scratch,
+                              int32_t* rowperm, int32_t* info, double* growth, double diag_tol, double piv_tol) {
   if (cnt <= 0) return hipSuccess;
+  if (Mmax > 128) return hipErrorInvalidValue;
   size_t lds = (size_t)Mmax * (size_t)(Mmax | 1) * sizeof(double);
-  k_front_lds<<<cnt, 256, lds, st>>>(list, sn, store, scratch, rowperm, info, growth, diag_tol, piv_tol);
+#define FS_ARGS list, sn, chlist, relmap, aents, a, arow, Rs, store, scratch, rowperm, info, growth, diag_tol, piv_tol
+  if (Mmax <= 32) k_front_small<1><<<cnt, 64, lds, st>>>(FS_ARGS);
+  else if (Mmax <= 64) k_front_small<2><<<cnt, 128, lds, st>>>(FS_ARGS);
+  else k_front_small<4><<<cnt, 256, lds, st>>>(FS_ARGS);
+#undef FS_ARGS
   return hipGetLastError();
 }
 hipError_t launch_panel1(hipStream_t st, int cnt, int lds_doubles, int rmax, int wmax, int step,

@@ -34,7 +34,8 @@ hipError_t launch_rowscale(hipStream_t, int64_t, const int64_t*, const int32_t*,
 hipError_t launch_fill(hipStream_t, int64_t, double*, double);
 hipError_t launch_assemble(hipStream_t, int64_t, const XCol*, const XContrib*, const int2*, const SNode*,
                            const int32_t*, const double*, const int32_t*, const double*, double*, double*);
-hipError_t launch_front_lds(hipStream_t, int, int, const int32_t*, const SNode*, double*, double*,
+hipError_t launch_front_small(hipStream_t, int, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
+                              const int2*, const double*, const int32_t*, const double*, double*, double*,
                             int32_t*, int32_t*, double*, double, double);
 hipError_t init_kernel_attributes();
 hipError_t launch_panel1(hipStream_t, int, int, int, int, int, const int32_t*, const SNode*, double*, double*,
@@ -761,9 +762,9 @@ static int build_schedule(smlu_handle* h) {
                               (int32_t)((int64_t)ae.size() - a0), a0});
           }
       };
-      for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {
+      for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {   // small fronts assemble inside k_front_small
         const int64_t s = LS[k];
-        front_columns(s, {{0, P.M(s)}}, {(int32_t)s});
+        if (h->hsn[s].mode != 0) front_columns(s, {{0, P.M(s)}}, {(int32_t)s});
       }
       for (const int32_t t : dfront[l]) {   // the shared front: this rank's column blocks
         std::vector<std::pair<int64_t, int64_t>> ranges;
@@ -778,10 +779,12 @@ static int build_schedule(smlu_handle* h) {
       L.cnt = (int64_t)xc.size() - L.off;
       if (L.cnt > 0) h->fac.push_back(L);
     }
-    // small fronts, launched per size class so that small fronts get small LDS (occupancy)
+    // small fronts (assembly fused into the factorization), launched per size class so that
+    // small fronts get small LDS (occupancy); ilist: (front, first A entry, A entry count), the
+    // front's A entries as (entry, local column << 16 | local row)
     {
-      const int64_t cls[4] = {32, 64, 96, kSmallM};
-      for (int c = 0; c < 4; ++c) {
+      const int64_t cls[6] = {16, 32, 48, 64, 96, kSmallM};
+      for (int c = 0; c < 6; ++c) {
         L = Launch();
         L.kind = K_FRONT_LDS;
         L.off = (int64_t)ilist.size();
@@ -792,9 +795,15 @@ static int build_schedule(smlu_handle* h) {
           int64_t M = P.M(s);
           if (M > cls[c] || (c > 0 && M <= cls[c - 1])) continue;
           ilist.push_back((int32_t)s);
+          ilist.push_back((int32_t)ae.size());
+          ilist.push_back((int32_t)(fr_ptr[s + 1] - fr_ptr[s]));
+          for (int64_t e = fr_ptr[s]; e < fr_ptr[s + 1]; ++e) {
+            const int32_t id = fr_ent[e];
+            ae.push_back(make_int2(id, (int32_t)((P.A_lj[id] << 16) | P.A_li[id])));
+          }
           Mmax = std::max(Mmax, M);
         }
-        L.cnt = (int64_t)ilist.size() - L.off;
+        L.cnt = ((int64_t)ilist.size() - L.off) / 3;
         L.aux = Mmax;
         if (L.cnt > 0) h->fac.push_back(L);
       }
@@ -1924,8 +1933,9 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
       return launch_assemble(st, L.cnt, h->xcols.p + L.off, h->xtasks.p, h->aents.p, h->sn.p, h->relmap.p,
                              h->A.p, h->Arow.p, h->Rs.p, h->store.p, h->scratch.p);
     case K_FRONT_LDS:
-      return launch_front_lds(st, (int)L.cnt, (int)L.aux, h->ilist.p + L.off, h->sn.p, h->store.p,
-                              h->scratch.p, h->rowperm.p, h->info.p, h->growth.p, diag_tol, piv_tol);
+      return launch_front_small(st, (int)L.cnt, (int)L.aux, h->ilist.p + L.off, h->sn.p, h->chlist.p,
+                                h->relmap.p, h->aents.p, h->A.p, h->Arow.p, h->Rs.p, h->store.p, h->scratch.p,
+                                h->rowperm.p, h->info.p, h->growth.p, diag_tol, piv_tol);
     case K_STEPTRSM:
       return launch_step_trsm(st, (int)L.aux, h->ftiles.p + L.off, (int)L.cnt, L.nwg, h->ftiles.p + L.off2,
                               (int)L.cnt2, L.nwg2, L.step, h->ob, h->sn.p, h->store.p, h->scratch.p, h->info.p,

@@ -20,8 +20,13 @@ int main(int argc, char** argv) {
     sv.clear();
     for (int a = 1; a < argc; ++a) { Shape x; if (sscanf(argv[a], "%d,%d,%d", &x.m, &x.n, &x.k) == 3) sv.push_back(x); }
   }
-  const int tiles_list[] = {64, 128, 129};
-  const char* names[] = {"valu64", "valu128", "mfma128"};
+  // variants: tile codes of launch_gemm (GB_TILES="129,130"); the first one is the reference
+  std::vector<int> tiles_list = {64, 128, 129};
+  if (const char* e = std::getenv("GB_TILES")) {
+    tiles_list.clear();
+    for (const char* p = e; *p;) { tiles_list.push_back(std::atoi(p)); while (*p && *p != ',') ++p; if (*p) ++p; }
+  }
+  const int NV = (int)tiles_list.size();
   hipStream_t st; CK(hipStreamCreate(&st));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (auto sh : sv) {
@@ -32,14 +37,14 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&A, hA.size() * 8)); CK(hipMalloc(&B, hB.size() * 8)); CK(hipMalloc(&C1, hC.size() * 8)); CK(hipMalloc(&C2, hC.size() * 8));
     CK(hipMemcpy(A, hA.data(), hA.size() * 8, hipMemcpyHostToDevice)); CK(hipMemcpy(B, hB.data(), hB.size() * 8, hipMemcpyHostToDevice));
     CK(hipMalloc(&dt, sizeof(GemmTask)));
-    double res[3] = {0, 0, 0};
+    std::vector<double> res(NV, 0.0), vdiff(NV, 0.0);
     double ref_md = 0;
     std::vector<double> ref(hC.size());
-    for (int variant = 0; variant < 3; ++variant) {
+    for (int variant = 0; variant < NV; ++variant) {
       int tile = tiles_list[variant];
       double* C = variant == 0 ? C1 : C2;
       GemmTask t{}; t.A = A; t.B = B; t.C = C; t.m = m; t.n = n; t.k = k; t.lda = lda; t.ldb = ldb; t.ldc = ldc;
-      const int tsm = tile == 129 ? 128 : tile, tsn = tsm;
+      const int tsm = tile >= 128 ? 128 : 64, tsn = tsm;
       t.tiles_m = (m + tsm - 1) / tsm; t.tile0 = 0;
       int64_t tiles = (int64_t)t.tiles_m * ((n + tsn - 1) / tsn);
       CK(hipMemcpy(dt, &t, sizeof t, hipMemcpyHostToDevice));
@@ -50,8 +55,8 @@ int main(int argc, char** argv) {
         std::vector<double> r(hC.size());
         CK(hipMemcpy(r.data(), C, r.size() * 8, hipMemcpyDeviceToHost));
         if (variant == 0) ref = r;
-        else if (tile != 129)
-          for (size_t o = 0; o < r.size(); ++o) ref_md = fmax(ref_md, fabs(r[o] - ref[o]));
+        else
+          for (size_t o = 0; o < r.size(); ++o) vdiff[variant] = fmax(vdiff[variant], fabs(r[o] - ref[o]));
       }
       int reps = (double)m * n * k > 1e11 ? 3 : 20;
       CK(hipEventRecord(e0, st));
@@ -60,28 +65,9 @@ int main(int argc, char** argv) {
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       res[variant] = 2.0 * m * n * (double)k * reps / (ms * 1e-3) / 1e12;
     }
-    // compare 64-tile VALU (C1) against MFMA (C2) after one update from the same C
-    for (int variant = 0; variant < 2; ++variant) {
-      int tile = variant == 0 ? 64 : 129;
-      double* C = variant == 0 ? C1 : C2;
-      GemmTask t{}; t.A = A; t.B = B; t.C = C; t.m = m; t.n = n; t.k = k; t.lda = lda; t.ldb = ldb; t.ldc = ldc;
-      const int ts = tile == 129 ? 128 : tile;
-      t.tiles_m = (m + ts - 1) / ts; t.tile0 = 0;
-      int64_t tiles = (int64_t)t.tiles_m * ((n + ts - 1) / ts);
-      CK(hipMemcpy(dt, &t, sizeof t, hipMemcpyHostToDevice));
-      CK(hipMemcpy(C, hC.data(), hC.size() * 8, hipMemcpyHostToDevice));
-      CK(launch_gemm(st, tiles, dt, 1, tile, 0));
-      CK(hipStreamSynchronize(st));
-    }
-    std::vector<double> r1(hC.size()), r2(hC.size());
-    CK(hipMemcpy(r1.data(), C1, r1.size() * 8, hipMemcpyDeviceToHost)); CK(hipMemcpy(r2.data(), C2, r2.size() * 8, hipMemcpyDeviceToHost));
-    double md = 0, mx = 0;
-    for (int j = 0; j < n; ++j) for (int i = 0; i < m; ++i) { size_t o = (size_t)j * ldc + i; md = fmax(md, fabs(r1[o] - r2[o])); mx = fmax(mx, fabs(r1[o])); }
-    bool pad_ok = true;  // rows >= m inside ld padding untouched
-    for (int j = 0; j < n && pad_ok; ++j) for (int i = m; i < ldc; ++i) { size_t o = (size_t)j * ldc + i; if (r2[o] != hC[o]) pad_ok = false; }
     printf("m=%6d n=%6d k=%6d ", m, n, k);
-    for (int v = 0; v < 3; ++v) printf(" %s %6.2f", names[v], res[v]);
-    printf("  TF | valu-vs-valu maxdiff %.1e  valu-vs-mfma rel %.1e pad_ok %d\n", ref_md, md / mx, pad_ok);
+    for (int v = 0; v < NV; ++v) printf(" t%d %6.2f TF (maxdiff vs t%d %.1e)", tiles_list[v], res[v], tiles_list[0], vdiff[v]);
+    printf("\n");
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C1)); CK(hipFree(C2)); CK(hipFree(dt));
   }
   return 0;
