@@ -346,23 +346,18 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__
 // C[row = 16 bi + (l & 15)][col = 16 bj + (l >> 4) + 4 r], r = 0..3.
 // ------------------------------------------------------------------------------------
 typedef double v4d __attribute__((ext_vector_type(4)));
-template <bool TRSM>
-__global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restrict__ tasks, int ntask,
-                                                         GrowthArgs ga) {
-  __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
-  __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
-  const int64_t b = blockIdx.x;
-  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+// Guard-free operand and C traffic on interior tiles (m, n in range), K guards only in the
+// last, partial slice (FULL = false: every access guarded).  +1-4 % over the guarded form
+// (k = 384 trailing shapes 48.4 -> 50.1 TFLOP/s, tools/gemm_bench).
+template <bool TRSM, bool FULL>
+__device__ __forceinline__ void gemm128_mfma_body(const GemmTask& t, int m0, int n0,
+                                                double (&As)[2][HBK_][HBM_], double (&Bs)[2][HBK_][HLDB_],
+                                                const GrowthArgs& ga) {
   const gdbl* gA = gbl(t.A);
   const gdbl* gB = gbl(t.B);
   gdbl* gC = gbl(t.C);
-  int tm, tn;
-  tile_rc<HBM_>(t, b - t.tile0, tm, tn);
-  const int m0 = tm * HBM_, n0 = tn * HBM_;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wr = (wv & 1) * 64, wc = (wv >> 1) * 64;   // wave quadrant (rows, cols)
-  // accumulators start from C (loads overlap the first K slice's), B staged negated in LDS:
-  // acc = C + sum(A * -B); the epilogue is stores only
+  const int wr = (wv & 1) * 64, wc = (wv >> 1) * 64;
   const int li = lane & 15, lk = lane >> 4;
   v4d acc[4][4];
 #pragma unroll
@@ -373,23 +368,26 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int col = n0 + wc + 16 * j + lk + 4 * r;
-        acc[i][j][r] = (row < t.m && col < t.n) ? gC[(int64_t)col * t.ldc + row] : 0.0;
+        acc[i][j][r] = (FULL || (row < t.m && col < t.n)) ? gC[(int64_t)col * t.ldc + row] : 0.0;
       }
   }
   const int ar = tid & 127, ak = tid >> 7;
   const int bk = tid & 15, bc = tid >> 4;
   const int K = t.k;
   const int arow = m0 + ar;
-  const bool arow_ok = arow < t.m;
+  const bool arow_ok = FULL || arow < t.m;
   const gdbl* Ap = gA + arow;
+  const gdbl* Bp = gB + (int64_t)(n0 + bc) * t.ldb + bk;
   double ra[8], rb[8];
-  auto gload = [&](int k0) {
+  auto gload = [&](int k0, bool kguard) {
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int kk = k0 + ak + 2 * r;
-      ra[r] = (arow_ok && kk < K) ? Ap[(int64_t)kk * t.lda] : 0.0;
+      if (!kguard && FULL) ra[r] = Ap[(int64_t)kk * t.lda];
+      else ra[r] = (arow_ok && kk < K) ? Ap[(int64_t)kk * t.lda] : 0.0;
       const int col = n0 + bc + 16 * r;
-      rb[r] = (col < t.n && k0 + bk < K) ? gB[(int64_t)col * t.ldb + k0 + bk] : 0.0;
+      if (!kguard && FULL) rb[r] = Bp[(int64_t)16 * r * t.ldb + k0];
+      else rb[r] = ((FULL || col < t.n) && k0 + bk < K) ? Bp[(int64_t)16 * r * t.ldb + k0] : 0.0;
     }
   };
   auto sstore = [&](int buf) {
@@ -400,20 +398,21 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
     }
   };
   const int nk = (K + HBK_ - 1) / HBK_;
-  gload(0);
+  const int nfull = K / HBK_;   // slices with every k in range
+  gload(0, nfull == 0);
   sstore(0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * HBK_);
+    if (kt + 1 < nk) gload((kt + 1) * HBK_, kt + 1 >= nfull);
 #pragma unroll
     for (int kq = 0; kq < HBK_ / 4; ++kq) {
       const int k = kq * 4 + lk;
       double fa[4], fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = As[cur][k][wr + 16 * i + li];   // A[row][k]
+      for (int i = 0; i < 4; ++i) fa[i] = As[cur][k][wr + 16 * i + li];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = Bs[cur][k][wc + 16 * j + li];   // B[k][col]
+      for (int j = 0; j < 4; ++j) fb[j] = Bs[cur][k][wc + 16 * j + li];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -432,120 +431,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restr
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int col = n0 + wc + 16 * j + lk + 4 * r;
-        if (row < t.m && col < t.n) {
-          gC[(int64_t)col * t.ldc + row] = acc[i][j][r];
-          gmax = fmax(gmax, fabs(acc[i][j][r]));
-        }
-      }
-  }
-  if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
-}
-
-
-// ------------------------------------------------------------------------------------
-// MFMA tile, v2 (dev, tile code 130): the same 128x128 tile and per-element arithmetic as
-// k_gemm128_mfma (bitwise-identical results), with (a) branch-free operand loads (clamped
-// addresses + selects instead of one branch per element), unguarded C traffic on interior
-// tiles, (b) the next k-quad's LDS fragments read before the current quad's MFMAs, and
-// (c) s_setprio(1) around each MFMA cluster.
-// ------------------------------------------------------------------------------------
-template <bool TRSM, bool FULL>
-__device__ __forceinline__ void gemm128_mfma2_body(const GemmTask& t, int m0, int n0,
-                                                   double (&As)[2][HBK_][HBM_], double (&Bs)[2][HBK_][HLDB_],
-                                                   const GrowthArgs& ga) {
-  const gdbl* gA = gbl(t.A);
-  const gdbl* gB = gbl(t.B);
-  gdbl* gC = gbl(t.C);
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wr = (wv & 1) * 64, wc = (wv >> 1) * 64;
-  const int li = lane & 15, lk = lane >> 4;
-  const int M = t.m, N = t.n, K = t.k;
-  v4d acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = m0 + wr + 16 * i + li;
-    const int rc = FULL ? row : min(row, M - 1);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int col = n0 + wc + 16 * j + lk + 4 * r;
-        const int cc = FULL ? col : min(col, N - 1);
-        const double v = gC[(int64_t)cc * t.ldc + rc];
-        acc[i][j][r] = (FULL || (row < M && col < N)) ? v : 0.0;
-      }
-  }
-  const int ar = tid & 127, ak = tid >> 7;
-  const int bk = tid & 15, bc = tid >> 4;
-  const int arow = m0 + ar;
-  const bool arow_ok = FULL || arow < M;
-  const gdbl* Ap = gA + (FULL ? arow : min(arow, M - 1));
-  double ra[8], rb[8];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int kk = k0 + ak + 2 * r;
-      const double va = Ap[(int64_t)min(kk, K - 1) * t.lda];
-      ra[r] = (arow_ok && kk < K) ? va : 0.0;
-      const int col = n0 + bc + 16 * r;
-      const int cc = FULL ? col : min(col, N - 1);
-      const int kb = k0 + bk;
-      const double vb = gB[(int64_t)cc * t.ldb + min(kb, K - 1)];
-      rb[r] = ((FULL || col < N) && kb < K) ? vb : 0.0;
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      As[buf][ak + 2 * r][ar] = ra[r];
-      Bs[buf][bk][bc + 16 * r] = -rb[r];
-    }
-  };
-  const int nk = (K + HBK_ - 1) / HBK_;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * HBK_);
-    double fa[2][4], fb[2][4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      fa[0][i] = As[cur][lk][wr + 16 * i + li];
-      fb[0][i] = Bs[cur][lk][wc + 16 * i + li];
-    }
-#pragma unroll
-    for (int kq = 0; kq < HBK_ / 4; ++kq) {
-      const int c = kq & 1;
-      if (kq + 1 < HBK_ / 4) {
-        const int k = (kq + 1) * 4 + lk;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          fa[c ^ 1][i] = As[cur][k][wr + 16 * i + li];
-          fb[c ^ 1][i] = Bs[cur][k][wc + 16 * i + li];
-        }
-      }
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[c][j], fa[c][i], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
-    if (kt + 1 < nk) sstore(cur ^ 1);
-    __syncthreads();
-  }
-  double gmax = 0.0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int row = m0 + wr + 16 * i + li;
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int col = n0 + wc + 16 * j + lk + 4 * r;
-        if (FULL || (row < M && col < N)) {
+        if (FULL || (row < t.m && col < t.n)) {
           gC[(int64_t)col * t.ldc + row] = acc[i][j][r];
           if (TRSM) gmax = fmax(gmax, fabs(acc[i][j][r]));
         }
@@ -555,8 +441,8 @@ __device__ __forceinline__ void gemm128_mfma2_body(const GemmTask& t, int m0, in
 }
 
 template <bool TRSM>
-__global__ __launch_bounds__(256, 2) void k_gemm128_mfma2(const GemmTask* __restrict__ tasks, int ntask,
-                                                          GrowthArgs ga) {
+__global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restrict__ tasks, int ntask,
+                                                         GrowthArgs ga) {
   __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
   __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
   const int64_t b = blockIdx.x;
@@ -564,8 +450,8 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma2(const GemmTask* __rest
   int tm, tn;
   tile_rc<HBM_>(t, b - t.tile0, tm, tn);
   const int m0 = tm * HBM_, n0 = tn * HBM_;
-  if (m0 + HBM_ <= t.m && n0 + HBM_ <= t.n) gemm128_mfma2_body<TRSM, true>(t, m0, n0, As, Bs, ga);
-  else gemm128_mfma2_body<TRSM, false>(t, m0, n0, As, Bs, ga);
+  if (m0 + HBM_ <= t.m && n0 + HBM_ <= t.n) gemm128_mfma_body<TRSM, true>(t, m0, n0, As, Bs, ga);
+  else gemm128_mfma_body<TRSM, false>(t, m0, n0, As, Bs, ga);
 }
 
 // ------------------------------------------------------------------------------------
@@ -656,9 +542,7 @@ hipError_t launch_gemm_g(hipStream_t st, int64_t ntiles, const GemmTask* tasks, 
   if (ntiles <= 0) return hipSuccess;
   const GrowthArgs ga{info, growth, piv_tol};
   const bool trsm = info != nullptr;
-  if (tile == 130 && trsm) k_gemm128_mfma2<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 130) k_gemm128_mfma2<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 129 && trsm) k_gemm128_mfma<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  if (tile == 129 && trsm) k_gemm128_mfma<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 129) k_gemm128_mfma<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 128)   // VALU 128 tile (SMLU_VALU_GEMM only; never used for the TRSM form)
     k_gemm128<<<(unsigned)(maxwg > 0 ? std::min<int64_t>(ntiles, maxwg) : ntiles), 256, 0, st>>>(
