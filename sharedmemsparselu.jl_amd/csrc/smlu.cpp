@@ -103,6 +103,7 @@ struct Launch {
   int64_t off2 = 0, cnt2 = 0, nwg2 = 0;   // second work list (merged launches)
   double flops = 0;
   int side = 0;                           // 1 = issued on the look-ahead stream
+  int vendor = 0;                         // 1 = GEMM tasks [off, off+cnt) issued as rocBLAS dgemm calls
 };
 
 template <class T>
@@ -204,6 +205,45 @@ RcclApi* rccl_api() {
   api.lib = l;
   return &api;
 }
+
+// ---- rocBLAS for the large plain Schur-update GEMMs (loaded at run time; absent -> the
+// hand-written MFMA tile runs them).  Deterministic mode: atomics (split-K) off, so a repeated
+// refactorization is bitwise identical. ----------------------------------------------------------
+struct RocblasApi {
+  void* lib = nullptr;
+  int (*create)(void**);
+  int (*destroy)(void*);
+  int (*set_stream)(void*, hipStream_t);
+  int (*set_atomics)(void*, int);
+  int (*dgemm)(void*, int, int, int, int, int, const double*, const double*, int, const double*, int,
+               const double*, double*, int);
+};
+
+RocblasApi* rocblas_api() {
+  static RocblasApi api;
+  static bool tried = false;
+  if (tried) return api.lib ? &api : nullptr;
+  tried = true;
+  void* l = dlopen("librocblas.so.5", RTLD_NOW | RTLD_LOCAL);
+  if (!l) l = dlopen("librocblas.so", RTLD_NOW | RTLD_LOCAL);
+  if (!l) return nullptr;
+  bool ok = true;
+  auto sym = [&](const char* n) {
+    void* f = dlsym(l, n);
+    ok = ok && f != nullptr;
+    return f;
+  };
+  api.create = (decltype(api.create))sym("rocblas_create_handle");
+  api.destroy = (decltype(api.destroy))sym("rocblas_destroy_handle");
+  api.set_stream = (decltype(api.set_stream))sym("rocblas_set_stream");
+  api.set_atomics = (decltype(api.set_atomics))sym("rocblas_set_atomics_mode");
+  api.dgemm = (decltype(api.dgemm))sym("rocblas_dgemm");
+  if (!ok) return nullptr;
+  api.lib = l;
+  return &api;
+}
+constexpr int kRbOpNone = 111;          // rocblas_operation_none
+constexpr int kRbAtomicsNotAllowed = 0; // rocblas_atomics_not_allowed
 
 struct RcclState {
   ncclComm_t comm = nullptr;
@@ -339,6 +379,11 @@ struct smlu_handle {
   bool trsm_gemm = true;      // GEMM-form triangular solves of the blocked fronts
   bool trsm_gemm64_only = false;   // SMLU_TRSM_GEMM=2: only for diagonal-tile (nb = 64) fronts
   int64_t side_wg = 0;        // grid cap of look-ahead GEMMs (SMLU_SIDE_WG; 0 = uncapped)
+  void* rocblas = nullptr;    // rocBLAS handle (opts.vendor_gemm and librocblas present)
+  int64_t vendor_min = 256;   // rocBLAS for GEMM tasks with at least this many 128x128 tiles (SMLU_ROCBLAS_MIN)
+  int64_t vendor_calls = 0;   // rocBLAS dgemm calls per factorization
+  int vendor_kinds = 3;       // launch kinds routed to rocBLAS: 1 F22, 2 trailing, 4 U rows, 8 in-block (SMLU_ROCBLAS_KINDS)
+  std::vector<GemmTask> hgt;  // host copy of the GEMM tasks (rocBLAS calls read their operands from it)
   ~smlu_handle() { release_all(); }
   void release_buffers() {
     if (stream) (void)hipSetDevice(device);
@@ -400,6 +445,10 @@ struct smlu_handle {
     ev_fork = ev_join = nullptr;
     if (side) (void)hipStreamDestroy(side);
     side = nullptr;
+    if (rocblas) {
+      if (RocblasApi* R = rocblas_api()) (void)R->destroy(rocblas);
+      rocblas = nullptr;
+    }
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
   }
@@ -609,6 +658,9 @@ static int build_schedule(smlu_handle* h) {
   std::vector<std::pair<int64_t, int64_t>> tinv_patch;   // (gt index * 2 + operand B?, offset)
   h->gemm_flops = 0;
   h->gemm_launches = h->gemm128_launches = 0;
+  h->vendor_calls = 0;
+  if (const char* e = std::getenv("SMLU_ROCBLAS_MIN")) h->vendor_min = std::max<int64_t>(1, std::atoll(e));
+  if (const char* e = std::getenv("SMLU_ROCBLAS_KINDS")) h->vendor_kinds = std::atoi(e);
   h->gemm_bytes = 0;
   h->gemm22_flops = 0;
   h->dense_flops = P.flops;
@@ -619,6 +671,43 @@ static int build_schedule(smlu_handle* h) {
                              int side = 0, const std::vector<int64_t>* tpatch = nullptr) {
     if (cand.empty()) return;
     const bool count = kind != K_TRSML;   // GEMM-form TRSM is accounted as "trsm", not GEMM
+    // large plain Schur updates (F22, trailing): one rocBLAS dgemm per task; the rest stays in
+    // one batched launch of the hand-written tiles
+    const int vbit = step < 0 ? 1 : kind == K_GEMMO ? 2 : kind == K_GEMMU ? 4 : kind == K_GEMM ? 8 : 0;
+    if (h->rocblas && !side && !tpatch && (h->vendor_kinds & vbit)) {
+      std::vector<GemmTask> big, rest;
+      double flb = 0;
+      for (auto& g : cand) {
+        const int64_t t128 = (int64_t)((g.m + 127) / 128) * ((g.n + 127) / 128);
+        if (t128 >= h->vendor_min) {
+          big.push_back(g);
+          flb += 2.0 * g.m * (double)g.n * g.k;
+        } else {
+          rest.push_back(g);
+        }
+      }
+      if (!big.empty()) {
+        Launch V;
+        V.kind = step < 0 ? K_GEMM22 : kind;
+        V.step = step;
+        V.vendor = 1;
+        V.off = (int64_t)gt.size();
+        V.cnt = (int64_t)big.size();
+        V.flops = flb;
+        for (auto& g : big) {
+          h->gemm_bytes += 8.0 * ((double)g.m * g.k + (double)g.k * g.n + 2.0 * g.m * g.n);
+          gt.push_back(g);
+        }
+        h->fac.push_back(V);
+        h->gemm_flops += flb;
+        h->gemm_launches += V.cnt;
+        h->vendor_calls += V.cnt;
+        if (step < 0) h->gemm22_flops += flb;
+        cand.swap(rest);
+        fl -= flb;
+        if (cand.empty()) return;
+      }
+    }
     int64_t t128 = 0;
     for (auto& g : cand) t128 += (int64_t)((g.m + 127) / 128) * ((g.n + 127) / 128);
     int tile = t128 >= h->t128_min ? 128 : 64;
@@ -1707,6 +1796,14 @@ static int build_schedule(smlu_handle* h) {
       std::fprintf(fp, "idx,kind,name,step,tile,nwg,cnt,flops,kmax,mn\n");
       for (size_t i = 0; i < h->fac.size(); ++i) {
         const Launch& L = h->fac[i];
+        if (L.vendor) {   // one row per rocBLAS call (one kernel dispatch each), tile code 200
+          for (int64_t t = 0; t < L.cnt; ++t) {
+            const GemmTask& q = gt[L.off + t];
+            std::fprintf(fp, "%zu,%d,%s,%d,200,0,1,%.0f,%d,%.0f\n", i, L.kind, kKindName[L.kind], L.step,
+                         2.0 * q.m * (double)q.n * q.k, q.k, (double)q.m * q.n);
+          }
+          continue;
+        }
         int kmax = 0;
         double mn = 0;
         const bool g = L.kind == K_GEMM || L.kind == K_GEMMU || L.kind == K_GEMMO || L.kind == K_GEMM22 ||
@@ -1745,6 +1842,7 @@ static int build_schedule(smlu_handle* h) {
     }
   }
   HIPCHK(h->gtasks.upload(gt.data(), gt.size(), st));
+  h->hgt = gt;
   HIPCHK(h->stasks.upload(st_tasks.data(), st_tasks.size(), st));
   HIPCHK(h->xcols.upload(xc.data(), xc.size(), st));
   HIPCHK(h->swaps.alloc((size_t)max_list * kSwapStride));
@@ -1818,6 +1916,15 @@ static int setup_device(smlu_handle* h) {
       std::fprintf(stderr, "smlu: side stream on %d of %d CUs\n", kept, ncu);
     } else {
       HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_lo));
+    }
+  }
+  if (!h->rocblas && h->opts.vendor_gemm) {   // rocBLAS for the large plain Schur updates
+    if (RocblasApi* R = rocblas_api()) {
+      void* rb = nullptr;
+      if (R->create(&rb) == 0 && rb) {
+        if (R->set_stream(rb, h->stream) == 0 && R->set_atomics(rb, kRbAtomicsNotAllowed) == 0) h->rocblas = rb;
+        else (void)R->destroy(rb);
+      }
     }
   }
   if (!h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
@@ -1916,6 +2023,17 @@ struct Timer {
 
 static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, double piv_tol) {
   hipStream_t st = L.side ? h->side : h->stream;
+  if (L.vendor) {   // C -= A*B per task, rocBLAS dgemm on the handle's stream
+    RocblasApi* R = rocblas_api();
+    const double minus1 = -1.0, one = 1.0;
+    for (int64_t i = L.off; i < L.off + L.cnt; ++i) {
+      const GemmTask& g = h->hgt[i];
+      if (R->dgemm(h->rocblas, kRbOpNone, kRbOpNone, g.m, g.n, g.k, &minus1, g.A, g.lda, g.B, g.ldb, &one,
+                   g.C, g.ldc) != 0)
+        return hipErrorLaunchFailure;
+    }
+    return hipSuccess;
+  }
   switch (L.kind) {
     case K_FORK: {
       hipError_t e = hipEventRecord(h->ev_fork, h->stream);
@@ -2411,6 +2529,7 @@ void smlu_default_opts(smlu_opts* o) {
   o->leaf_size = 64;
   o->use_mfma = std::getenv("SMLU_VALU_GEMM") ? 0 : 1;   // fp64 MFMA by default
   o->refine = -1;
+  o->vendor_gemm = std::getenv("SMLU_NO_ROCBLAS") ? 0 : 1;
 }
 
 int smlu_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
@@ -3121,6 +3240,7 @@ double smlu_stat(const smlu_handle* h, const char* key) {
   if (k == "gemm_launches") return (double)h->gemm_launches;
   if (k == "gemm_bytes") return h->gemm_bytes;
   if (k == "gemm128_launches") return (double)h->gemm128_launches;
+  if (k == "vendor_calls") return (double)h->vendor_calls;
   if (k.rfind("ms_", 0) == 0) {
     std::string name = k.substr(3);
     double t = 0;

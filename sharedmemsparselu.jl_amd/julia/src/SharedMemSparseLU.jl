@@ -12,7 +12,7 @@ const libsmlu = get(ENV, "SMLU_LIB", joinpath(@__DIR__, "..", "deps", "libsmlu.s
 mutable struct SmluOpts
     chunk_size::Int64; index_base::Int32; ordering::Int32; grid::NTuple{3,Int64}
     scale::Int32; relax::Int32; pivot_tol::Float64; diag_pivot_tol::Float64
-    device::Int32; profile::Int32; leaf_size::Int64; use_mfma::Int32; refine::Int32
+    device::Int32; profile::Int32; leaf_size::Int64; use_mfma::Int32; refine::Int32; vendor_gemm::Int32
 end
 function default_opts()
     o = SmluOpts(0, 0, 0, (0, 0, 0), 0, 0, 0.0, 0.0, 0, 0, 0, 0, 0)

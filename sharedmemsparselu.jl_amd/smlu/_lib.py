@@ -48,6 +48,7 @@ class SmluOpts(ctypes.Structure):
         ("leaf_size", i64),
         ("use_mfma", i32),
         ("refine", i32),
+        ("vendor_gemm", i32),
     ]
 
 

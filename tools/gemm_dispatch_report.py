@@ -13,9 +13,9 @@ from collections import defaultdict
 tr = list(csv.DictReader(open(sys.argv[1])))
 tr.sort(key=lambda x: int(x["Start_Timestamp"]))
 # first factorization only: up to the first k_perm_in (a solve) or the end
-g_tr = [x for x in tr if "k_gemm" in x["Kernel_Name"]]
+g_tr = [x for x in tr if "k_gemm" in x["Kernel_Name"] or x["Kernel_Name"].startswith("Cijk")]
 sched = [r for r in csv.DictReader(open(sys.argv[2])) if r["name"] in ("gemm", "gemm22", "gemmu", "gemmo", "trsm")
-         and int(r["tile"]) in (64, 65, 128, 129)]
+         and int(r["tile"]) in (64, 65, 128, 129, 200)]
 n = min(len(g_tr), len(sched))
 print(f"trace gemm dispatches {len(g_tr)}, schedule gemm launches {len(sched)}; joining {n}")
 rows = []
@@ -66,7 +66,7 @@ def kb(r):
 
 agg(lambda r: (r["kind"], kb(r)), "by kind, k")
 # wave quantisation estimate for the 128 tiles: fraction of the last wave filled
-q = [r for r in rows if r["tile"] == 129 and r["flops"] > 0]
+q = [r for r in rows if r["tile"] in (129, 200) and r["flops"] > 0]
 if q:
     eff = sum(r["flops"] for r in q) / sum(r["us"] for r in q) / 1e6
     waste = 0.0

@@ -5,7 +5,7 @@ import csv
 import sys
 from collections import defaultdict
 
-tr = [x for x in csv.DictReader(open(sys.argv[1])) if x["Kernel_Name"].startswith(("smlu::", "void smlu::"))
+tr = [x for x in csv.DictReader(open(sys.argv[1])) if x["Kernel_Name"].startswith(("smlu::", "void smlu::", "Cijk"))
       and "k_rowscale" not in x["Kernel_Name"]]
 tr.sort(key=lambda x: int(x["Start_Timestamp"]))
 sched = list(csv.DictReader(open(sys.argv[2])))
