@@ -369,6 +369,9 @@ struct smlu_handle {
   bool graph_failed = false;
   bool lookahead = false;     // SMLU_LOOKAHEAD=1: trailing updates beyond the next block on a side stream
   int ob = kOBDefault;        // outer block width (SMLU_OB overrides; multiple of 64)
+  int64_t sb = kOBDefault;     // super-block width of the GEMM-form fronts (SMLU_SB; multiple of ob;
+                              // == ob: two-level scheme, the default -- SB 768..6144 measured 537..550 ms
+                              // vs 531 at 128^3: the extra sub-panel TRSMs cost more than k = SB gains)
   int64_t t128_min = 512;     // 128x128 GEMM tiles when a launch has at least this many
   bool small_k = true;        // k <= 64 launches use k_gemm_k64 (SMLU_SMALLK=0: off)
   bool dominant = false;      // A diagonally dominant (by rows or columns): last host values seen
@@ -744,6 +747,15 @@ static int build_schedule(smlu_handle* h) {
     if (tile >= 128) ++h->gemm128_launches;
     if (step < 0) h->gemm22_flops += fl;
   };
+  // fronts whose triangular solves run in GEMM form (tile inverses); they also take the
+  // super-block level of the three-level blocking (SB columns; OB for the others)
+  auto gform = [&](int64_t s) {
+    return h->trsm_gemm && (h->hsn[s].nb == kNbTile || !h->trsm_gemm64_only);
+  };
+  if (const char* e = std::getenv("SMLU_SB")) h->sb = std::atoi(e);
+  h->sb = std::max<int64_t>(h->ob, (h->sb / h->ob) * h->ob);
+  auto sbw = [&](int64_t s) -> int64_t { return (gform(s) && !h->lookahead && h->nranks == 1) ? h->sb : h->ob; };
+  const int64_t spf = std::max<int64_t>(h->sb, h->ob) / 32;   // swap / tile-inverse slots per front
   // tinv operand encoding in tpatch: offset * 2 + (1 if the operand is B, 0 if A)
   auto tinv_slot_off = [](int64_t slot, bool upper) { return slot * 8192 + (upper ? 4096 : 0); };
   for (int l = 0; l < P.nlevels; ++l) {
@@ -909,9 +921,9 @@ static int build_schedule(smlu_handle* h) {
       big.push_back(s);
       maxsteps = std::max<int64_t>(maxsteps, (r.ns + r.nb - 1) / r.nb);
     }
-    max_list = std::max<int64_t>(max_list, dist_slots + (int64_t)big.size() * (h->ob / 32));
+    max_list = std::max<int64_t>(max_list, dist_slots + (int64_t)big.size() * spf);
     // swap-list slot of sub-panel u of a front's current outer block
-    auto slot_of = [&](int64_t s, int64_t u) { return dist_slots + bidx[s] * (h->ob / 32) + u; };
+    auto slot_of = [&](int64_t s, int64_t u) { return dist_slots + bidx[s] * spf + u; };
     bool side_busy = false;
     auto join = [&]() {
       if (!side_busy) return;
@@ -950,7 +962,7 @@ static int build_schedule(smlu_handle* h) {
             rmax = std::max(rmax, r.mode == 1 ? r.ns - kb : w);
             wmax = std::max<int64_t>(wmax, r.nb);
             ilist.push_back((int32_t)act[pos]);
-            ilist.push_back((int32_t)slot_of(act[pos], t % (h->ob / r.nb)));
+            ilist.push_back((int32_t)slot_of(act[pos], t % (sbw(act[pos]) / r.nb)));
             ++pos;
             ++cnt;
           }
@@ -962,9 +974,6 @@ static int build_schedule(smlu_handle* h) {
         }
         if (pos != act.size()) return fail(h, SMLU_ERR_ARG, "internal: panel classes");
       }
-      auto gform = [&](int64_t s) {
-        return h->trsm_gemm && (h->hsn[s].nb == kNbTile || !h->trsm_gemm64_only);
-      };
       // inverses of the diagonal tiles of the GEMM-form fronts (I - L_kk^-1, I - U_kk^-1)
       {
         L = Launch();
@@ -974,7 +983,7 @@ static int build_schedule(smlu_handle* h) {
         for (auto s : act) {
           if (!gform(s)) continue;
           ilist.push_back((int32_t)s);
-          ilist.push_back((int32_t)slot_of(s, t % (h->ob / h->hsn[s].nb)));
+          ilist.push_back((int32_t)slot_of(s, t % (sbw(s) / h->hsn[s].nb)));
         }
         L.cnt = ((int64_t)ilist.size() - L.off) / 2;
         if (L.cnt > 0) h->fac.push_back(L);
@@ -992,7 +1001,7 @@ static int build_schedule(smlu_handle* h) {
           int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
           int64_t ncol = oend - ostart - w;
           if (ncol <= 0) continue;
-          st_tasks.push_back(SwapTask{(int32_t)s, (int32_t)kb, 1, (int32_t)slot_of(s, t % (h->ob / r.nb)),
+          st_tasks.push_back(SwapTask{(int32_t)s, (int32_t)kb, 1, (int32_t)slot_of(s, t % (sbw(s) / r.nb)),
                                       (int32_t)ostart, (int32_t)oend, (int32_t)kb, (int32_t)(kb + w), wg});
           wg += (ncol + 63) / 64;
         }
@@ -1045,7 +1054,7 @@ static int build_schedule(smlu_handle* h) {
           const SNode& r = h->hsn[s];
           int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
           int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
-          const int64_t slot = slot_of(s, t % (h->ob / r.nb));
+          const int64_t slot = slot_of(s, t % (sbw(s) / r.nb));
           if (oend - kb - w > 0) {
             GemmTask g{};
             g.B = g.C = store + r.Loff + (kb + w) * M + kb;
@@ -1113,142 +1122,204 @@ static int build_schedule(smlu_handle* h) {
           int64_t ncol = M - (oend - ostart);
           if (ncol <= 0) continue;
           st_tasks.push_back(SwapTask{(int32_t)s, (int32_t)ostart, (int32_t)((oend - ostart + r.nb - 1) / r.nb),
-                                      (int32_t)slot_of(s, 0), 0, (int32_t)M, (int32_t)ostart, (int32_t)oend, wg});
+                                      (int32_t)slot_of(s, (ostart % sbw(s)) / r.nb), 0, (int32_t)M, (int32_t)ostart,
+                                      (int32_t)oend, wg});
           wg += (ncol + 63) / 64;
         }
         L.cnt = (int64_t)st_tasks.size() - L.off;
         L.nwg = wg;
         if (wg > 0) h->fac.push_back(L);
       }
-      std::vector<int64_t> fin;
-      int64_t nsubmax = 0;
-      for (auto s : fin_all) {
-        const SNode& r = h->hsn[s];
-        int64_t kb = t * r.nb;
-        int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
-        int64_t M = (int64_t)r.ns + r.nu;
-        if (oend == M) continue;   // nothing right of the block
-        fin.push_back(s);
-        nsubmax = std::max<int64_t>(nsubmax, (oend - ostart + r.nb - 1) / r.nb);
-      }
-      for (int64_t u = 0; u < nsubmax; ++u) {
-        // (a) U row block of sub-panel u: TRSM on columns [oend, M)
-        L = Launch();
-        L.kind = K_TRSMU;
-        L.step = (int)t;
-        L.aux = 1;   // outer mode
-        L.off = (int64_t)ft.size();
-        int64_t wg = 0, cnt = 0;
-        std::vector<GemmTask> cand, ctri;
-        std::vector<int64_t> tp;
-        double fl = 0;
-        for (auto s : fin) {
-          const SNode& r = h->hsn[s];
-          int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb;
-          int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
-          int64_t kbu = ostart + u * r.nb;
-          if (kbu >= oend) continue;
-          int64_t wu = std::min<int64_t>(r.nb, oend - kbu);
-          if (gform(s)) {   // U rows [kbu, kbu+wu) right of the block: L_uu^-1 C, in place
-            const int64_t off = tinv_slot_off(slot_of(s, u), false) * 2;
-            if (r.ns - oend > 0) {
-              GemmTask g{};
-              g.B = g.C = store + r.Loff + oend * M + kbu;
-              g.m = (int)wu; g.n = (int)(r.ns - oend); g.k = (int)wu;
-              g.lda = 64; g.ldb = (int)M; g.ldc = (int)M;
-              ctri.push_back(g);
-              tp.push_back(off);
+      // Three-level blocking: outer blocks (OB) are grouped in super-blocks (SB, GEMM-form
+      // fronts only, SMLU_SB).  At the end of an OB that does not close its SB, the OB's U rows
+      // and the trailing update reach only the SB's own columns [oend, se); at the end of the
+      // SB, its U rows for every column right of it are solved OB by OB (each OB's rows
+      // updated by the earlier ones, k = OB width), then one trailing update with k = SB
+      // width covers the rest of the front.  SB == OB is the plain two-level scheme.
+      struct URows {
+        int64_t s, ob0, ob1, c0, c1;   // OB rows [ob0, ob1); L-panel columns [c0, c1); + U12 if u12
+        bool u12;
+      };
+      // TRSM of the U rows of a set of OBs (one per front), sub-panel by sub-panel: L_uu^-1 C in
+      // place on the given columns, then the rows below the sub-panel inside the OB
+      auto urows = [&](const std::vector<URows>& items) {
+        int64_t nsub = 0;
+        for (auto& it : items) nsub = std::max<int64_t>(nsub, (it.ob1 - it.ob0 + h->hsn[it.s].nb - 1) / h->hsn[it.s].nb);
+        for (int64_t u = 0; u < nsub; ++u) {
+          L = Launch();
+          L.kind = K_TRSMU;
+          L.step = (int)t;
+          L.aux = 1;   // outer mode
+          L.off = (int64_t)ft.size();
+          int64_t wg = 0, cnt = 0;
+          std::vector<GemmTask> cand, ctri;
+          std::vector<int64_t> tp;
+          double fl = 0;
+          for (auto& it : items) {
+            const int64_t s = it.s;
+            const SNode& r = h->hsn[s];
+            const int64_t M = (int64_t)r.ns + r.nu;
+            const int64_t kbu = it.ob0 + u * r.nb;
+            if (kbu >= it.ob1) continue;
+            const int64_t wu = std::min<int64_t>(r.nb, it.ob1 - kbu);
+            const int64_t n1 = it.c1 - it.c0;
+            if (gform(s)) {   // U rows [kbu, kbu+wu) on the columns: L_uu^-1 C, in place
+              const int64_t off = tinv_slot_off(slot_of(s, (kbu % sbw(s)) / r.nb), false) * 2;
+              if (n1 > 0) {
+                GemmTask g{};
+                g.B = g.C = store + r.Loff + it.c0 * M + kbu;
+                g.m = (int)wu; g.n = (int)n1; g.k = (int)wu;
+                g.lda = 64; g.ldb = (int)M; g.ldc = (int)M;
+                ctri.push_back(g);
+                tp.push_back(off);
+              }
+              if (it.u12 && r.nu > 0) {
+                GemmTask g{};
+                g.B = g.C = store + r.Uoff + kbu;
+                g.m = (int)wu; g.n = r.nu; g.k = (int)wu;
+                g.lda = 64; g.ldb = r.ns; g.ldc = r.ns;
+                ctri.push_back(g);
+                tp.push_back(off);
+              }
+            } else {          // k_trsm_u: columns [oend, M) of the plain two-level scheme
+              ft.push_back(FrontTile{(int32_t)s, (int32_t)kbu, wg});
+              wg += (M - it.c0 + 255) / 256;
+              ++cnt;
             }
-            if (r.nu > 0) {
-              GemmTask g{};
-              g.B = g.C = store + r.Uoff + kbu;
-              g.m = (int)wu; g.n = r.nu; g.k = (int)wu;
-              g.lda = 64; g.ldb = r.ns; g.ldc = r.ns;
-              ctri.push_back(g);
-              tp.push_back(off);
+            // rows below the sub-panel inside the OB: [kbu+wu, ob1) x the columns
+            const int64_t m = it.ob1 - kbu - wu;
+            if (m > 0) {
+              if (n1 > 0) {
+                GemmTask g{};
+                g.A = store + r.Loff + kbu * M + kbu + wu;
+                g.B = store + r.Loff + it.c0 * M + kbu;
+                g.C = store + r.Loff + it.c0 * M + kbu + wu;
+                g.m = (int)m; g.n = (int)n1; g.k = (int)wu;
+                g.lda = (int)M; g.ldb = (int)M; g.ldc = (int)M;
+                cand.push_back(g);
+                fl += 2.0 * m * n1 * wu;
+              }
+              if (it.u12 && r.nu > 0) {
+                GemmTask g{};
+                g.A = store + r.Loff + kbu * M + kbu + wu;
+                g.B = store + r.Uoff + kbu;
+                g.C = store + r.Uoff + kbu + wu;
+                g.m = (int)m; g.n = r.nu; g.k = (int)wu;
+                g.lda = (int)M; g.ldb = r.ns; g.ldc = r.ns;
+                cand.push_back(g);
+                fl += 2.0 * m * (double)r.nu * wu;
+              }
             }
-          } else {
-            ft.push_back(FrontTile{(int32_t)s, (int32_t)kbu, wg});
-            wg += (M - oend + 255) / 256;
-            ++cnt;
           }
-          // (b) rows below the sub-panel inside the block: [kbu+wu, oend) x [oend, M)
-          int64_t m = oend - kbu - wu;
-          if (m > 0) {
-            int64_t n1 = r.ns - oend;       // L-panel columns
-            if (n1 > 0) {
-              GemmTask g{};
-              g.A = store + r.Loff + kbu * M + kbu + wu;
-              g.B = store + r.Loff + oend * M + kbu;
-              g.C = store + r.Loff + oend * M + kbu + wu;
-              g.m = (int)m; g.n = (int)n1; g.k = (int)wu;
-              g.lda = (int)M; g.ldb = (int)M; g.ldc = (int)M;
-              cand.push_back(g);
-              fl += 2.0 * m * n1 * wu;
-            }
-            if (r.nu > 0) {                 // U12 columns
-              GemmTask g{};
-              g.A = store + r.Loff + kbu * M + kbu + wu;
-              g.B = store + r.Uoff + kbu;
-              g.C = store + r.Uoff + kbu + wu;
-              g.m = (int)m; g.n = r.nu; g.k = (int)wu;
-              g.lda = (int)M; g.ldb = r.ns; g.ldc = r.ns;
-              cand.push_back(g);
-              fl += 2.0 * m * (double)r.nu * wu;
-            }
-          }
+          L.cnt = cnt;
+          L.nwg = wg;
+          if (wg > 0) h->fac.push_back(L);
+          add_gemm_launch(ctri, 0.0, (int)t, K_TRSML, 0, &tp);
+          add_gemm_launch(cand, fl, (int)t, K_GEMMU);
         }
-        L.cnt = cnt;
-        L.nwg = wg;
-        if (wg > 0) h->fac.push_back(L);
-        add_gemm_launch(ctri, 0.0, (int)t, K_TRSML, 0, &tp);
-        add_gemm_launch(cand, fl, (int)t, K_GEMMU);
-      }
-      // (c) trailing update, k = oend - ostart <= 256.  With look-ahead the columns of the next
-      // outer block [oend, oend2) are updated on the main stream and the rest (columns
-      // [oend2, ns) and the U12 rows) on the side stream, overlapping the next block's panels.
-      std::vector<GemmTask> c1, c2;
-      double fl1 = 0, fl2 = 0;
-      for (auto s : fin) {
+      };
+      // C(rows [r0, r1) x L-panel columns [c0, c1) (+ U12 when u12)) -= L(rows, [k0, k1)) U([k0, k1), cols)
+      auto rank_update = [&](int64_t s, int64_t r0, int64_t r1, int64_t c0, int64_t c1, bool u12, int64_t k0,
+                             int64_t k1, std::vector<GemmTask>& cand, double& fl) {
         const SNode& r = h->hsn[s];
-        int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb;
-        int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
-        int64_t oend2 = h->lookahead ? std::min<int64_t>(r.ns, oend + h->ob) : r.ns;
-        int64_t kk = oend - ostart;
-        int64_t m1 = M - oend;
-        auto lpart = [&](int64_t ca, int64_t cb, std::vector<GemmTask>& cand, double& fl) {
-          if (m1 <= 0 || cb <= ca) return;      // rows [oend, M) x L-panel columns [ca, cb)
+        const int64_t M = (int64_t)r.ns + r.nu, kk = k1 - k0;
+        if (r1 > r0 && c1 > c0 && kk > 0) {
           GemmTask g{};
-          g.A = store + r.Loff + ostart * M + oend;
-          g.B = store + r.Loff + ca * M + ostart;
-          g.C = store + r.Loff + ca * M + oend;
-          g.m = (int)m1; g.n = (int)(cb - ca); g.k = (int)kk;
+          g.A = store + r.Loff + k0 * M + r0;
+          g.B = store + r.Loff + c0 * M + k0;
+          g.C = store + r.Loff + c0 * M + r0;
+          g.m = (int)(r1 - r0); g.n = (int)(c1 - c0); g.k = (int)kk;
           g.lda = (int)M; g.ldb = (int)M; g.ldc = (int)M;
           cand.push_back(g);
-          fl += 2.0 * m1 * (double)(cb - ca) * kk;
-        };
-        lpart(oend, oend2, c1, fl1);
-        lpart(oend2, r.ns, h->lookahead ? c2 : c1, h->lookahead ? fl2 : fl1);
-        int64_t m2 = r.ns - oend;
-        if (m2 > 0 && r.nu > 0) {     // rows [oend, ns) x U12 columns
-          GemmTask g{};
-          g.A = store + r.Loff + ostart * M + oend;
-          g.B = store + r.Uoff + ostart;
-          g.C = store + r.Uoff + oend;
-          g.m = (int)m2; g.n = r.nu; g.k = (int)kk;
-          g.lda = (int)M; g.ldb = r.ns; g.ldc = r.ns;
-          (h->lookahead ? c2 : c1).push_back(g);
-          (h->lookahead ? fl2 : fl1) += 2.0 * m2 * (double)r.nu * kk;
+          fl += 2.0 * (double)(r1 - r0) * (double)(c1 - c0) * kk;
         }
+        const int64_t ru1 = std::min<int64_t>(r1, r.ns);   // U12 rows live above ns
+        if (u12 && r.nu > 0 && ru1 > r0 && kk > 0) {
+          GemmTask g{};
+          g.A = store + r.Loff + k0 * M + r0;
+          g.B = store + r.Uoff + k0;
+          g.C = store + r.Uoff + r0;
+          g.m = (int)(ru1 - r0); g.n = r.nu; g.k = (int)kk;
+          g.lda = (int)M; g.ldb = r.ns; g.ldc = r.ns;
+          cand.push_back(g);
+          fl += 2.0 * (double)(ru1 - r0) * (double)r.nu * kk;
+        }
+      };
+      std::vector<URows> open_ob;                  // OBs that do not close their SB
+      std::vector<int64_t> close_sb;               // fronts whose SB ends here
+      for (auto s : fin_all) {
+        const SNode& r = h->hsn[s];
+        const int64_t kb = t * r.nb, M = (int64_t)r.ns + r.nu;
+        const int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
+        const int64_t ss = (ostart / sbw(s)) * sbw(s), se = std::min<int64_t>(r.ns, ss + sbw(s));
+        if (oend == M) continue;   // nothing right of the block
+        if (oend < se) open_ob.push_back(URows{s, ostart, oend, oend, se, false});
+        else close_sb.push_back(s);
       }
-      if (!c2.empty()) {
-        Launch F;
-        F.kind = K_FORK;
-        h->fac.push_back(F);
-        add_gemm_launch(c2, fl2, (int)t, K_GEMMO, 1);
-        side_busy = true;
+      // OBs inside their SB: U rows and trailing update on the SB's columns only
+      if (!open_ob.empty()) {
+        urows(open_ob);
+        std::vector<GemmTask> c1;
+        double fl1 = 0;
+        for (auto& it : open_ob) {
+          const SNode& r = h->hsn[it.s];
+          rank_update(it.s, it.ob1, (int64_t)r.ns + r.nu, it.c0, it.c1, false, it.ob0, it.ob1, c1, fl1);
+        }
+        add_gemm_launch(c1, fl1, (int)t, K_GEMMO);
       }
-      add_gemm_launch(c1, fl1, (int)t, K_GEMMO);
+      // SBs ending here: their U rows on every column right of the SB, OB by OB, then the
+      // trailing update with k = SB width (look-ahead, when on, splits it over two streams)
+      if (!close_sb.empty()) {
+        int64_t nob = 0;
+        for (auto s : close_sb) {
+          const int64_t kb = t * h->hsn[s].nb, ostart = (kb / h->ob) * h->ob;
+          const int64_t ss = (ostart / sbw(s)) * sbw(s);
+          nob = std::max<int64_t>(nob, (ostart - ss) / h->ob + 1);
+        }
+        for (int64_t b = 0; b < nob; ++b) {
+          std::vector<URows> items;
+          std::vector<GemmTask> cb;
+          double flb = 0;
+          for (auto s : close_sb) {
+            const SNode& r = h->hsn[s];
+            const int64_t kb = t * r.nb, ostart = (kb / h->ob) * h->ob, M = (int64_t)r.ns + r.nu;
+            const int64_t ss = (ostart / sbw(s)) * sbw(s), se = std::min<int64_t>(r.ns, ostart + h->ob);
+            const int64_t b0 = ss + b * h->ob;
+            if (b0 >= se) continue;
+            const int64_t b1 = std::min<int64_t>(se, b0 + h->ob);
+            items.push_back(URows{s, b0, b1, se, r.ns, true});
+            // later OBs' rows of the SB receive this OB's contribution (right of the SB)
+            if (b1 < se) rank_update(s, b1, se, se, r.ns, true, b0, b1, cb, flb);
+            (void)M;
+          }
+          urows(items);
+          add_gemm_launch(cb, flb, (int)t, K_GEMMO);
+        }
+        std::vector<GemmTask> c1, c2;
+        double fl1 = 0, fl2 = 0;
+        for (auto s : close_sb) {
+          const SNode& r = h->hsn[s];
+          const int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb;
+          const int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
+          const int64_t ss = (ostart / sbw(s)) * sbw(s);
+          const int64_t oend2 = h->lookahead ? std::min<int64_t>(r.ns, oend + h->ob) : r.ns;
+          rank_update(s, oend, M, oend, oend2, false, ss, oend, c1, fl1);
+          if (h->lookahead) {
+            rank_update(s, oend, M, oend2, r.ns, false, ss, oend, c2, fl2);
+            rank_update(s, oend, r.ns, oend, oend, true, ss, oend, c2, fl2);   // U12 rows only
+          } else {
+            rank_update(s, oend, r.ns, oend, oend, true, ss, oend, c1, fl1);  // U12 rows only
+          }
+        }
+        if (!c2.empty()) {
+          Launch F;
+          F.kind = K_FORK;
+          h->fac.push_back(F);
+          add_gemm_launch(c2, fl2, (int)t, K_GEMMO, 1);
+          side_busy = true;
+        }
+        add_gemm_launch(c1, fl1, (int)t, K_GEMMO);
+      }
     }
     join();
     // F22 -= L21 * U12 for the blocked fronts of this level
