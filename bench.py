@@ -181,12 +181,12 @@ def main():
     if args.test_one_gpu:
         local = 0
     if world > 1:
+        # control plane (barriers, the max-over-ranks timing, the RCCL unique id) over gloo; the
+        # data path is the library's own RCCL communicator (xGMI point-to-point), so a process
+        # holds exactly one RCCL instance
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        if args.test_one_gpu:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
@@ -203,6 +203,7 @@ def main():
     t0 = time.perf_counter()
     if partitioned:   # one factorization split over the ranks (subtrees + RCCL exchanges)
         F = smlu.DistributedSparseLU(A, device=local, ordering=args.ordering,
+                                     transport="host" if args.test_one_gpu else "rccl",
                                      **({"grid": grid} if grid else {}))
     else:
         F = smlu.ParallelSparseLU(A, grid=grid, device=local, profile=not args.no_profile)
@@ -234,8 +235,7 @@ def main():
         log(f"rank {rank}: {'warmup' if r < args.warmup else 'step'} {r} refactor "
             f"{F.stat('refactor_ms_last'):.1f} ms")
 
-    dt = timed_region(step, args.steps, args.warmup, torch.cuda.synchronize,
-                      dev if world > 1 and not args.test_one_gpu else None)
+    dt = timed_region(step, args.steps, args.warmup, torch.cuda.synchronize)
     # one solve (reported, not the metric)
     b = torch.from_numpy(np.random.default_rng(5).random(n)).to(dev)   # same b on every rank
     x = torch.empty_like(b)
