@@ -186,7 +186,16 @@ def main():
         # holds exactly one RCCL instance
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("gloo")
+        # gloo prints its connection banner on the C-level stdout: keep stdout for the JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     else:
         torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
@@ -211,7 +220,7 @@ def main():
     nnzLU = F.stat("nnzLU")
     log(f"rank {rank}: analysis {F.stat('analysis_ms')/1e3:.1f}s, create+first factor {t_create:.1f}s, "
         f"nnz(L+U)={nnzLU:.4g}, upd={F.stat('upd'):.4g}, launches={F.stat('launches'):.0f}"
-        + (f", segments={F.nseg}" if partitioned else ""))
+        + (f", comm steps={F.stat('comm_steps'):.0f}, shared fronts={F.stat('shared_fronts'):.0f}" if partitioned else ""))
 
     # C5 inputs: same pattern, new values (diag += U(0,1) from default_rng(47+r)), uploaded to HBM
     dpos = torch.from_numpy(mats.diag_positions(A)).to(dev)
