@@ -174,8 +174,12 @@ __global__ __launch_bounds__(256) void k_fwd_gather(const int32_t* __restrict__ 
   for (int64_t i = tid; i < ns; i += 256) v[i] = xo[i];
 }
 
+// One 64-column step of a large front: wave 0 of every workgroup solves the 64x64 diagonal
+// block (tri64; each workgroup re-solves it, no inter-workgroup hand-off), waves 1-4 own one row
+// each of the workgroup's 256-row chunk and load that row's 64 slab values before the solved
+// block arrives (the two memory round trips overlap instead of following each other).
 template <bool UPPER>
-__global__ __launch_bounds__(256) void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step,
+__global__ __launch_bounds__(320) void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step,
                                                    const SNode* __restrict__ sn,
                                                    const double* __restrict__ store,
                                                    double* __restrict__ x, double* __restrict__ vbuf) {
@@ -198,13 +202,25 @@ __global__ __launch_bounds__(256) void k_tri_block(const FrontTile* __restrict__
       xs[lane] = xi;
       if (chunk == 0) x[s.first + jb + lane] = xi;
     }
+    __syncthreads();
+    return;
   }
-  __syncthreads();
   // rows updated by this chunk: forward -> [jb+bw, M), backward -> [0, jb)
   const int64_t r0 = UPPER ? chunk * 256 : jb + bw + chunk * 256;
   const int64_t r1 = UPPER ? jb : M;
-  const int64_t i = r0 + tid;
-  if (i < r1 && i < r0 + 256) v[i] -= dot64(Lp + jb * M, M, i, bw, xs, 0.0);
+  const int64_t i = r0 + tid - 64;
+  const bool has = i < r1;
+  double d[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) d[j] = (has && j < bw) ? Lp[(jb + j) * M + i] : 0.0;
+  __syncthreads();
+  if (has) {
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < 64; ++j)
+      if (j < bw) acc = fma(d[j], xs[j], acc);
+    v[i] -= acc;
+  }
 }
 
 // x_s[i] (in v) = x[first+i] - sum_j U12[i,j] * x[R_j], 256 rows per workgroup
@@ -367,8 +383,8 @@ hipError_t launch_fwd_gather(hipStream_t st, int cnt, const int32_t* list, const
 hipError_t launch_tri_block(hipStream_t st, bool upper, int64_t nwg, const FrontTile* ft, int nft,
                             int step, const SNode* sn, const double* store, double* x, double* vbuf) {
   if (nwg <= 0) return hipSuccess;
-  if (upper) k_tri_block<true><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, x, vbuf);
-  else k_tri_block<false><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, step, sn, store, x, vbuf);
+  if (upper) k_tri_block<true><<<(unsigned)nwg, 320, 0, st>>>(ft, nft, step, sn, store, x, vbuf);
+  else k_tri_block<false><<<(unsigned)nwg, 320, 0, st>>>(ft, nft, step, sn, store, x, vbuf);
   return hipGetLastError();
 }
 hipError_t launch_bwd_u12(hipStream_t st, int64_t nwg, const FrontTile* ft, int nft, const SNode* sn,
