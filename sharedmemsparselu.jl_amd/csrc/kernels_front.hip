@@ -70,7 +70,20 @@ __global__ __launch_bounds__(256) void k_assemble(int64_t ntasks, const XCol* __
   gdbl* colL = tj < P.ns ? P.L + tj * P.M : nullptr;
   gdbl* colU = tj < P.ns ? nullptr : P.U + (tj - P.ns) * P.ns;
   gdbl* colF = (tj < P.ns || P.nu == 0) ? nullptr : P.F + (tj - P.ns) * P.nu - P.ns;
+  // contribution q < 64: its descriptor lives in lane q for the whole column (read once),
+  // together with its running position; each chunk then costs one row-map round trip (the
+  // chunk's at most 256 entries of that child column are a prefix of the next 256) and one
+  // round trip for the values it takes
   int cur = 0;                  // lane q: position in contribution q's child column
+  int64_t q_src = 0, q_rm = 0;
+  int q_nu = 0;
+  if (lane < t.cnt) {
+    const XContrib ck = contrib[t.off + lane];
+    const SNode c = sn[ck.child];
+    q_src = ck.src;
+    q_rm = c.rowptr;
+    q_nu = c.nu;
+  }
   int64_t ap = 0;               // next A entry
   for (int64_t r0 = 0; r0 < len; r0 += 256) {
     const int64_t r1 = min<int64_t>(len, r0 + 256);
@@ -90,33 +103,48 @@ __global__ __launch_bounds__(256) void k_assemble(int64_t ntasks, const XCol* __
     }
     wave_lds_sync();
     for (int q = 0; q < t.cnt; ++q) {
-      const XContrib ck = contrib[t.off + q];
-      const SNode c = sn[ck.child];
-      const int64_t nuc = c.nu;
-      const double* src = ck.src >= 0 ? scratch + ck.src : store + (-1 - ck.src);
-      const int32_t* rm = relmap + c.rowptr;
-      int64_t pos;
+      int64_t srco, rmo, nuc, pos;
       if (q < 64) {
+        srco = ((int64_t)__builtin_amdgcn_readlane((int)(q_src >> 32), q) << 32) |
+               (uint32_t)__builtin_amdgcn_readlane((int)(q_src & 0xffffffff), q);
+        rmo = ((int64_t)__builtin_amdgcn_readlane((int)(q_rm >> 32), q) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((int)(q_rm & 0xffffffff), q);
+        nuc = __builtin_amdgcn_readlane(q_nu, q);
         pos = __builtin_amdgcn_readlane(cur, q);
       } else {                  // binary search for the first row >= r0
+        const XContrib ck = contrib[t.off + q];
+        const SNode c = sn[ck.child];
+        srco = ck.src;
+        rmo = c.rowptr;
+        nuc = c.nu;
+        const int32_t* rmq = relmap + rmo;
         int64_t lo = 0, hi = nuc;
         while (lo < hi) {
           const int64_t mid = (lo + hi) >> 1;
-          if (rm[mid] < r0) lo = mid + 1;
+          if (rmq[mid] < r0) lo = mid + 1;
           else hi = mid;
         }
         pos = lo;
       }
-      while (pos < nuc) {
-        const int64_t i = pos + lane;
-        const int32_t r = i < nuc ? rm[i] : 0x7fffffff;
-        const bool take = r < r1;
-        const unsigned long long m = __ballot(take);
-        if (take) b[r - r0] += src[i];
-        const int cn = __popcll(m);
-        pos += cn;
-        if (cn < 64) break;
+      const double* src = srco >= 0 ? scratch + srco : store + (-1 - srco);
+      const int32_t* rm = relmap + rmo;
+      int32_t rv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t i = pos + lane + 64 * k;
+        rv[k] = i < nuc ? rm[i] : 0x7fffffff;
       }
+      double sv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) sv[k] = rv[k] < r1 ? src[pos + lane + 64 * k] : 0.0;
+      int cn = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool take = rv[k] < r1;
+        if (take) b[rv[k] - r0] += sv[k];
+        cn += __popcll(__ballot(take));
+      }
+      pos += cn;
       if (q < 64 && lane == q) cur = (int)pos;
       wave_lds_sync();
     }
