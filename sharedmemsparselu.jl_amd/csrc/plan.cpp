@@ -8,6 +8,8 @@
 //    pre-relaxation supernodes so that exported factors carry the structural fill of
 //    (Rs.*A)[p,q] and nothing else.
 #include <algorithm>
+#include <cstdlib>
+#include <map>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -827,23 +829,47 @@ double project_partition(const Plan& P, double tflops, double gbs, double lat_us
       for (int64_t e = P.ch_ptr[s]; e < P.ch_ptr[s + 1]; ++e)
         xbytes += 8.0 * (double)P.nu(P.ch_list[e]) * (double)P.nu(P.ch_list[e]);
       t += lat + xbytes / G.size() / bw;
-      const double M = (double)P.M(s), ns = (double)P.ns(s);
+      const double M = (double)P.M(s);
       const int64_t np = P.npblk(s), nb = np + P.nublk(s);
+      // per-member clocks through the block-cyclic factorization with depth-1 look-ahead (the
+      // schedule of build_schedule): the owner of pivot block b+1 applies b to block b+1 only,
+      // factors b+1 and broadcasts it; it applies b to its other blocks after that broadcast
+      std::map<int, double> c, pend;
+      for (int r : G) { c[r] = t; pend[r] = 0.0; }
+      static const bool la = !(std::getenv("SMLU_DIST_LOOKAHEAD") && std::atoi(std::getenv("SMLU_DIST_LOOKAHEAD")) == 0);
       for (int64_t b = 0; b < np; ++b) {
         const double c0 = (double)P.blk_c0(s, b), c1 = (double)P.blk_c1(s, b), w = c1 - c0;
-        double inner = 2.0 * (M - c0) * w * w / rate + step_lat * std::ceil(w / 64.0);
-        double bc = lat + 8.0 * (M - c0) * w / bw;
-        double trail = 0;
+        const int o = P.blk_owner(s, b);
+        const double inner = 2.0 * (M - c0) * w * w / rate + step_lat * std::ceil(w / 64.0);
+        const double bcast = lat + 8.0 * (M - c0) * w / bw;
+        double ready = c[o] + inner;
+        for (int r : G)
+          if (r != o) ready = std::max(ready, c[r]);
+        const double tb = ready + bcast;
+        const int nxt = (la && b + 1 < np) ? P.blk_owner(s, b + 1) : -1;
         for (int r : G) {   // trailing update of r's blocks right of this one
-          double cols = 0;
+          double cols = 0, first = 0;
           for (int64_t bb = b + 1; bb < nb; ++bb)
-            if (P.blk_owner(s, bb) == r) cols += (double)(P.blk_c1(s, bb) - P.blk_c0(s, bb));
-          trail = std::max(trail, 2.0 * (M - c0) * w * cols / rate);
+            if (P.blk_owner(s, bb) == r) {
+              const double wc = (double)(P.blk_c1(s, bb) - P.blk_c0(s, bb));
+              cols += wc;
+              if (bb == b + 1) first = wc;
+            }
+          const double upd = 2.0 * (M - c0) * w * cols / rate, upd1 = 2.0 * (M - c0) * w * first / rate;
+          double cr = tb + pend[r];
+          pend[r] = 0.0;
+          if (r == nxt) {
+            cr += upd1;
+            pend[r] = upd - upd1;
+          } else {
+            cr += upd;
+          }
+          c[r] = cr;
         }
-        t += inner + bc + trail;
-        (void)ns;
       }
-      for (int r : G) clk[r] = t;
+      double tend = 0;
+      for (int r : G) tend = std::max(tend, c[r] + pend[r]);
+      for (int r : G) clk[r] = tend;
     }
   return *std::max_element(clk.begin(), clk.end());
 }

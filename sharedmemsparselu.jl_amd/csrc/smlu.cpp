@@ -1354,6 +1354,11 @@ static int build_schedule(smlu_handle* h) {
       std::vector<size_t> mine;
       for (size_t i = 0; i < Y.blocks.size(); ++i)
         if (Y.blocks[i].s == t) mine.push_back(i);
+      // look-ahead (depth 1): the owner of pivot block b+1 applies block b to block b+1 first,
+      // factors and broadcasts b+1, and only then applies b to its other blocks (`pending`),
+      // so the panel chain of b+1 overlaps the other members' trailing updates with b
+      static const bool dist_lookahead = !(std::getenv("SMLU_DIST_LOOKAHEAD") && std::atoi(std::getenv("SMLU_DIST_LOOKAHEAD")) == 0);
+      std::vector<Launch> pending;
       for (int64_t b = 0; b < np; ++b) {
         const int64_t ob = P.blk_c0(t, b), oe = P.blk_c1(t, b), w = oe - ob;
         const int64_t nsub = (w + 63) / 64;
@@ -1452,6 +1457,8 @@ static int build_schedule(smlu_handle* h) {
           }
           add_comm(h->fac, h->fac_seg, h->fac_comm, std::move(op));
         }
+        for (auto& q : pending) h->fac.push_back(q);   // the previous block's deferred updates
+        pending.clear();
         const double* bc = h->bcbuf.p;
         const int64_t ldL = own ? M : M - ob;
         auto Lsrc = [&](int64_t row, int64_t col) -> const double* {
@@ -1476,11 +1483,21 @@ static int build_schedule(smlu_handle* h) {
         }
         // target blocks right of this one: (node, columns, pivot block?) and their row pointers
         struct Tgt { int32_t node; int64_t c0, c1; bool piv; };
-        std::vector<Tgt> right;
+        std::vector<Tgt> right_all, right;
         for (size_t i : mine) {
           const RankLayout::Blk& T = Y.blocks[i];
-          if (T.c0 >= oe) right.push_back({blknode[i], T.c0, T.c1, T.c0 < ns});
+          if (T.c0 >= oe) right_all.push_back({blknode[i], T.c0, T.c1, T.c0 < ns});
         }
+        // this rank owns pivot block b+1 (look-ahead): block b+1 first, the rest deferred
+        const bool ahead = dist_lookahead && b + 1 < np && P.blk_owner(t, b + 1) == h->rank;
+        for (int pass = 0; pass < 2; ++pass) {
+        if (!ahead && pass == 1) break;
+        right.clear();
+        for (const Tgt& T : right_all)
+          if (!ahead || (pass == 0) == (T.c0 == P.blk_c0(t, b + 1))) right.push_back(T);
+        if (right.empty()) continue;
+        std::vector<Launch> saved;
+        if (ahead && pass == 1) saved.swap(h->fac);   // emit the deferred part into `pending`
         auto trow = [&](const Tgt& T, int64_t row) -> double* {   // rows < ns of the target's first column
           const SNode& q = h->hsn[T.node];
           return T.piv ? store + q.Loff + T.c0 * M + row : store + q.Uoff + (T.c0 - ns) * ns + row;
@@ -1555,7 +1572,14 @@ static int build_schedule(smlu_handle* h) {
           }
           add_gemm_launch(cand, fl, (int)(ob / 64), K_GEMMO);
         }
+        if (ahead && pass == 1) {
+          pending.swap(h->fac);
+          h->fac.swap(saved);
+        }
+        }
       }
+      for (auto& q : pending) h->fac.push_back(q);
+      pending.clear();
     }
   }
   // solves: per level, small fronts by one workgroup each; large fronts (ns > kSolveBigNs)
