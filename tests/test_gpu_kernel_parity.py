@@ -9,6 +9,8 @@
     valu64   SMLU_T128MIN=2^60, SMLU_SMALLK=0 every GEMM launch on the VALU 64x64 tile k_gemm
     valu128  SMLU_T128MIN=1, use_mfma=0       the VALU 128x128 tile k_gemm128
     default  as shipped (k_gemm_k64 for k <= 64 launches, k_tri_inv, 64x64 tiles)
+    rocblas  SMLU_ROCBLAS_MIN=1                every F22 / trailing GEMM task through rocBLAS dgemm
+             (deterministic mode), which the 128^3 refactor uses for its large fronts
 * Error paths of the reference surface: SingularException from lu(A) (src/SharedMemSparseLU.jl:74)
   and lu!(F, A) (:247), lu! with a changed pattern (the reallocate branch :252-273), the
   re-pivoting refactor (a zero or weak diagonal-tile pivot re-factors with full-candidate
@@ -28,9 +30,10 @@ pytestmark = pytest.mark.gpu
 
 VARIANTS = {
     "default": ({}, {}),
-    "mfma128": ({"SMLU_T128MIN": "1"}, {}),
-    "valu64": ({"SMLU_T128MIN": str(1 << 60), "SMLU_SMALLK": "0"}, {}),
-    "valu128": ({"SMLU_T128MIN": "1"}, {"use_mfma": False}),
+    "mfma128": ({"SMLU_T128MIN": "1", "SMLU_NO_ROCBLAS": "1"}, {}),
+    "valu64": ({"SMLU_T128MIN": str(1 << 60), "SMLU_SMALLK": "0", "SMLU_NO_ROCBLAS": "1"}, {}),
+    "valu128": ({"SMLU_T128MIN": "1", "SMLU_NO_ROCBLAS": "1"}, {"use_mfma": False}),
+    "rocblas": ({"SMLU_ROCBLAS_MIN": "1"}, {}),
 }
 
 
@@ -53,6 +56,10 @@ def check_variant_ran(F, variant):
         assert F.stat("launches_mfma128") == 0 and F.stat("launches_k64") == 0
     elif variant == "valu128":
         assert F.stat("launches_valu128") > 0 and F.stat("launches_mfma128") == 0
+    if variant == "rocblas":
+        assert F.stat("vendor_calls") > 0
+    elif variant != "default":
+        assert F.stat("vendor_calls") == 0
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
@@ -74,7 +81,7 @@ def test_poisson3d_nd_gemm_variants(gpu, monkeypatch, N, variant):
     assert isapprox(x, spla.spsolve(A, b), TOL, TOL)
 
 
-@pytest.mark.parametrize("variant", ["default", "mfma128"])
+@pytest.mark.parametrize("variant", ["default", "mfma128", "rocblas"])
 def test_poisson3d_32_nd_oracle(gpu, monkeypatch, variant):
     # the largest oracle case (~2.6 s on one core): root separator of 1024 pivots
     A = mats.poisson3d(32)
