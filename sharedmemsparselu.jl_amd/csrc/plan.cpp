@@ -836,7 +836,7 @@ double project_partition(const Plan& P, double tflops, double gbs, double lat_us
       // factors b+1 and broadcasts it; it applies b to its other blocks after that broadcast
       std::map<int, double> c, pend;
       for (int r : G) { c[r] = t; pend[r] = 0.0; }
-      static const bool la = !(std::getenv("SMLU_DIST_LOOKAHEAD") && std::atoi(std::getenv("SMLU_DIST_LOOKAHEAD")) == 0);
+      static const bool la = (std::getenv("SMLU_DIST_LOOKAHEAD") && std::atoi(std::getenv("SMLU_DIST_LOOKAHEAD")) == 1);
       for (int64_t b = 0; b < np; ++b) {
         const double c0 = (double)P.blk_c0(s, b), c1 = (double)P.blk_c1(s, b), w = c1 - c0;
         const int o = P.blk_owner(s, b);
