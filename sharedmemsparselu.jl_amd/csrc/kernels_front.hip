@@ -617,6 +617,164 @@ __global__ __launch_bounds__(64) void k_panel_wave(const int32_t* __restrict__ l
   }
 }
 
+// Column-block variant of k_panel_cols (the default for 64-wide panels): wave w owns the
+// CW = 64/NWV consecutive columns [w*CW, (w+1)*CW) in registers (lane = candidate row).  The
+// owner of a block factors its CW columns wave-locally -- pivot search, scaling, rank-1 updates
+// of its own later columns, no workgroup barrier -- and publishes the block's pivots and
+// multipliers through LDS (double-buffered); after ONE barrier every later wave applies the CW
+// rank-1 updates to its columns in column order, and every wave replays the transpositions.
+// One barrier per CW columns instead of one per column.  Same pivot choices and the same
+// element-wise FMAs in the same order as k_panel_cols (bitwise-identical panel).
+template <int NWV>
+__global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restrict__ list, int step,
+                                                        const SNode* __restrict__ sn,
+                                                        double* __restrict__ store,
+                                                        double* __restrict__ scratch,
+                                                        int32_t* __restrict__ rowperm,
+                                                        int32_t* __restrict__ swaps,
+                                                        int64_t swap_stride,
+                                                        int32_t* __restrict__ info,
+                                                        double* __restrict__ growth, double diag_tol) {
+  constexpr int CW = 64 / NWV;
+  __shared__ double s_l[2][CW][64];
+  __shared__ int s_p[2][CW];
+  __shared__ int s_flag[NWV], s_err[NWV];
+  const int sid = list[2 * blockIdx.x];
+  const SNode s = sn[sid];
+  FrontPtrs f = front_ptrs(s, store, scratch);
+  const int64_t M = f.M;
+  const int ns = (int)f.ns;
+  const int kb = step * s.nb;
+  const int w = min(s.nb, ns - kb);
+  const int R = (s.mode == 1) ? ns - kb : w;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool has = lane < R;
+  gdbl* P = f.L + (int64_t)kb * M + kb;
+  double x[CW];
+#pragma unroll
+  for (int j = 0; j < CW; ++j) {
+    const int c = wv * CW + j;
+    x[j] = (has && c < w) ? P[(int64_t)c * M + lane] : 0.0;
+  }
+  int pos = lane, who = lane;   // replicated in every wave
+  int flag = 0, err = -1;
+  double lmax = 0.0;
+  auto transpose = [&](int k, int p, int q) {   // positions k and pos[p] exchange rows
+    if (p != q) {
+      const int ppos = __builtin_amdgcn_readlane(pos, p);
+      if (lane == p) pos = k;
+      else if (lane == q) pos = ppos;
+      if (lane == k) who = p;
+      else if (lane == ppos) who = q;
+    }
+  };
+  for (int blk = 0; blk < NWV; ++blk) {
+    const int k0 = blk * CW;
+    if (k0 >= w) break;
+    const int buf = blk & 1;
+    if (wv == blk) {   // the owner factors its block
+#pragma unroll
+      for (int j = 0; j < CW; ++j) {
+        const int k = k0 + j;
+        if (k < w) {
+          const int q = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(who, k));
+          const double cur = x[j];
+          const bool cand = has && pos >= k;
+          const double akk = readlane_f64(cur, q);
+          const bool beats = cand && pos != k && fabs(cur) * diag_tol > fabs(akk);
+          int p = q;
+          if (__ballot(beats) != 0ull || akk == 0.0) {   // full argmax (rare under dominance)
+            double am = cand ? fabs(cur) : -1.0;
+            int ai = cand ? pos : 0x7fffffff;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+              const double ov = __shfl_xor(am, o, 64);
+              const int oi = __shfl_xor(ai, o, 64);
+              if (ov > am || (ov == am && oi < ai)) { am = ov; ai = oi; }
+            }
+            if (am <= 0.0) {
+              flag |= 1;
+              if (err < 0) err = kb + k;
+            } else {
+              p = __builtin_amdgcn_readlane(who, __builtin_amdgcn_readfirstlane(ai));
+            }
+            p = __builtin_amdgcn_readfirstlane(p);
+          }
+          const double pinv = recip(readlane_f64(cur, p));
+          double l = 0.0;
+          if (cand && lane != p) {
+            l = cur * pinv;
+            lmax = fmax(lmax, fabs(l));
+            x[j] = l;
+          }
+          s_l[buf][j][lane] = l;
+          if (lane == 0) s_p[buf][j] = p;
+          if (l != 0.0) {
+#pragma unroll
+            for (int j2 = j + 1; j2 < CW; ++j2) x[j2] = fma(-l, readlane_f64(x[j2], p), x[j2]);
+          }
+          transpose(k, p, q);
+        }
+      }
+    }
+    __syncthreads();
+    if (wv != blk) {   // later waves apply the block's updates; every wave replays the swaps
+#pragma unroll
+      for (int j = 0; j < CW; ++j) {
+        const int k = k0 + j;
+        if (k < w) {
+          const int q = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(who, k));
+          const int p = __builtin_amdgcn_readfirstlane(s_p[buf][j]);
+          if (wv > blk) {
+            const double l = s_l[buf][j][lane];
+            if (l != 0.0) {
+#pragma unroll
+              for (int jj = 0; jj < CW; ++jj) x[jj] = fma(-l, readlane_f64(x[jj], p), x[jj]);
+            }
+          }
+          transpose(k, p, q);
+        }
+      }
+    }
+  }
+  if (has) {
+#pragma unroll
+    for (int j = 0; j < CW; ++j) {
+      const int c = wv * CW + j;
+      if (c < w) P[(int64_t)c * M + pos] = x[j];
+    }
+  }
+  lmax = wave_max(lmax);
+  if (lane == 0) {
+    if (lmax > 0.0) atomic_max_pos(&growth[0], lmax);
+    s_flag[wv] = flag;
+    s_err[wv] = err;
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  int32_t* rp = rowperm + s.first + kb;
+  const int old = has ? rp[lane] : 0;
+  if (has) rp[pos] = old;
+  int32_t* sw = swaps + (int64_t)list[2 * blockIdx.x + 1] * swap_stride;
+  const bool mv = has && pos != lane;
+  const unsigned long long m = __ballot(mv);
+  if (mv) {
+    const int o = __popcll(m & ((1ull << lane) - 1ull));
+    sw[1 + 2 * o] = pos;
+    sw[2 + 2 * o] = lane;
+  }
+  if (lane == 0) {
+    sw[0] = __popcll(m);
+    int fl = 0, er = -1;
+    for (int v = 0; v < NWV; ++v) {   // first failing column over all waves
+      fl |= s_flag[v];
+      if (s_err[v] >= 0 && (er < 0 || s_err[v] < er)) er = s_err[v];
+    }
+    if (fl) publish_info(info + sid, fl, er);
+  }
+}
+
 // Column-split variant of k_panel_wave<64> (R <= 64 candidate rows, up to 64 columns): NWV waves,
 // lane = row as before, columns dealt round-robin (column c lives in wave c % NWV at register
 // c / NWV, so the column loop unrolls with static register indices).  Per column k the owning
@@ -1192,7 +1350,14 @@ hipError_t launch_panel1(hipStream_t st, int cnt, int lds_doubles, int rmax, int
     const char* e = std::getenv("SMLU_PANEL_COLS");
     return e ? std::atoi(e) : 16;
   }();
-  if (wmax > 32 && !lds_panel && cols_waves == 16) k_panel_cols<16><<<cnt, 1024, 0, st>>>(PANEL1_ARGS);
+  // column-block panel (one barrier per 64/NWV columns) unless SMLU_PANEL_BLK=0
+  static const int blk_waves = [] {
+    const char* e = std::getenv("SMLU_PANEL_BLK");
+    return e ? std::atoi(e) : 16;
+  }();
+  if (wmax > 32 && !lds_panel && blk_waves == 16) k_panel_blk<16><<<cnt, 1024, 0, st>>>(PANEL1_ARGS);
+  else if (wmax > 32 && !lds_panel && blk_waves == 8) k_panel_blk<8><<<cnt, 512, 0, st>>>(PANEL1_ARGS);
+  else if (wmax > 32 && !lds_panel && cols_waves == 16) k_panel_cols<16><<<cnt, 1024, 0, st>>>(PANEL1_ARGS);
   else if (wmax > 32 && !lds_panel && cols_waves == 8) k_panel_cols<8><<<cnt, 512, 0, st>>>(PANEL1_ARGS);
   else if (wmax > 32 && !lds_panel && cols_waves == 4) k_panel_cols<4><<<cnt, 256, 0, st>>>(PANEL1_ARGS);
   else if (wmax > 32 && !lds_panel) k_panel_wave<64><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
