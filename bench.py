@@ -254,6 +254,17 @@ def main():
     F.solve_device(x, b)
     torch.cuda.synchronize()
     solve_ms = (time.perf_counter() - t1) * 1e3
+    # eight right-hand sides in one batched call (single GPU)
+    solve8_ms = None
+    if not partitioned and hasattr(F, "solve_multi_device"):
+        B8 = torch.from_numpy(np.random.default_rng(6).random((8, n))).to(dev)
+        X8 = torch.empty_like(B8)
+        F.solve_multi_device(X8, B8)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        F.solve_multi_device(X8, B8)
+        torch.cuda.synchronize()
+        solve8_ms = (time.perf_counter() - t1) * 1e3
     # residual of that solve on the last refactored values (host SpMV)
     Al = A.copy()
     Al.data = vals[-1].cpu().numpy()
@@ -333,6 +344,7 @@ def main():
             "achieved_hbm_GBs": (hbm_refactor / (ms_per_step * 1e-3) / 1e9) if hbm_refactor else None,
             "achieved_hbm_frac": (hbm_refactor / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS) if hbm_refactor else None,
             "solve_ms": solve_ms,
+            "solve_8rhs_ms": solve8_ms,
             "solve_residual": solve_residual,
             "create_s": t_create,
         }

@@ -44,6 +44,7 @@ extern "C" {
 #define SMLU_ORDER_GEOMETRIC_ND 2   /* needs grid[0..2]: vertex v = i + nx*(j + ny*k) */
 #define SMLU_ORDER_GRAPH_ND     3   /* BFS level-structure nested dissection on A+A' */
 #define SMLU_ORDER_GIVEN        4   /* use smlu_create_with_pivots' p and q unchanged */
+#define SMLU_ORDER_AMD          5   /* approximate minimum degree on A+A' (UMFPACK's symmetric-strategy kind) */
 
 typedef struct smlu_opts {
     int64_t chunk_size;   /* reference `chunk_size` (src/SharedMemSparseLU.jl:64-72); accepted, clamped to n */

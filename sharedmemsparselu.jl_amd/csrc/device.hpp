@@ -78,6 +78,14 @@ struct SwapTask {
   int64_t wg0;
 };
 
+// Right-hand sides of a solve launch: n vectors, vector r of x at x + r*ldx and of the front
+// vectors at vbuf + r*ldv.
+struct Rhs {
+  int32_t n;
+  int64_t ldx, ldv;
+};
+constexpr int kMultiRhs = 16;   // right-hand sides per solve launch
+
 // One dense chunk of the reference's solve layout (src/SharedMemSparseLU.jl:101-243), 0-based:
 // the s x s diagonal block over x[c0, c0+s) at data[tri] (column-major, ld s) and the negated
 // nr x s rectangle over rows x[r0, r0+nr) at data[rect] (column-major, ld nr).

@@ -182,11 +182,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 // holds x_i.  Row i of the block is loaded into registers up front (64 independent loads, one
 // memory latency), so the 64-step chain only waits on readlane broadcasts, never on memory.
 template <bool UPPER>
-__device__ __forceinline__ double tri64(double xi, const double* __restrict__ D, int64_t M, int bw,
-                                        int lane) {
-  double row[64];
-#pragma unroll
-  for (int j = 0; j < 64; ++j) row[j] = (lane < bw && j < bw) ? D[(int64_t)j * M + lane] : 0.0;
+// dinv: 1 / (diagonal entry of row `lane`), used by the upper solve only (one reciprocal per lane,
+// computed before the chain).
+__device__ __forceinline__ double tri64_row(double xi, const double (&row)[64], double dinv, int bw, int lane) {
   if (!UPPER) {
 #pragma unroll
     for (int j = 0; j < 64; ++j) {
@@ -199,13 +197,28 @@ __device__ __forceinline__ double tri64(double xi, const double* __restrict__ D,
 #pragma unroll
     for (int j = 63; j >= 0; --j) {
       if (j < bw) {
-        if (lane == j) xi = xi * recip(row[j]);
+        if (lane == j) xi = xi * dinv;
         const double xj = readlane_f64(xi, j);
         if (lane < j) xi = fma(-row[j], xj, xi);
       }
     }
   }
   return xi;
+}
+__device__ __forceinline__ void load_row64(double (&row)[64], const double* __restrict__ D, int64_t M, int bw,
+                                           int lane) {
+#pragma unroll
+  for (int j = 0; j < 64; ++j) row[j] = (lane < bw && j < bw) ? D[(int64_t)j * M + lane] : 0.0;
+}
+__device__ __forceinline__ double diag_recip(const double* __restrict__ D, int64_t M, int bw, int lane) {
+  return lane < bw ? recip(D[(int64_t)lane * M + lane]) : 1.0;
+}
+template <bool UPPER>
+__device__ __forceinline__ double tri64(double xi, const double* __restrict__ D, int64_t M, int bw,
+                                        int lane) {
+  double row[64];
+  load_row64(row, D, M, bw, lane);
+  return tri64_row<UPPER>(xi, row, UPPER ? diag_recip(D, M, bw, lane) : 1.0, bw, lane);
 }
 
 // acc += sum_{j < bw} D[j*M + i] * xs[j] (bw <= 64) in ascending j: all loads issued up front.

@@ -37,6 +37,120 @@ __device__ __forceinline__ double tri_lds(double xi, const double* __restrict__ 
   return xi;
 }
 
+// Multi-RHS: every solve kernel takes `rh` (rh.n right-hand sides, column r of x at
+// x + r*rh.ldx, of the front vectors at vbuf + r*rh.ldv) and is instantiated for a batch width
+// NR >= rh.n (1, 4, 8, 16).  Element-wise loops run over (rhs, row) pairs flattened into one
+// index space (one memory round trip for all right-hand sides, not one per rhs); every factor
+// value loaded from HBM is applied to all right-hand sides; read-modify-writes of the front
+// vectors load all right-hand sides before the first store.  With NR == 1 the arithmetic and its
+// order are those of the single-vector solve.
+constexpr int kMaxRhs = kMultiRhs;
+
+// st(r, i, ld(r, i)) for r < nr, i < cnt, strided over the workgroup's nthr threads, four
+// (r, i) pairs per thread and round: the four loads are issued before the first store (the
+// pairs are distinct, so the stores never feed the loads of the same round).  cnt * nr < 2^31.
+template <int NR, class LD, class ST>
+__device__ __forceinline__ void map_ri(int nr, int64_t cnt, int tid, int nthr, LD&& ld, ST&& st) {
+  constexpr int U = 4;
+  const uint32_t c = (uint32_t)cnt, tot = c * (uint32_t)(NR == 1 ? 1 : nr);
+  for (uint32_t base = tid; base < tot; base += U * nthr) {
+    double val[U];
+    uint32_t rr[U], ii[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t e = base + u * nthr;
+      rr[u] = NR == 1 ? 0 : e / c;
+      ii[u] = e - rr[u] * c;
+      val[u] = e < tot ? ld((int)rr[u], (int64_t)ii[u]) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (base + u * nthr < tot) st((int)rr[u], (int64_t)ii[u], val[u]);
+  }
+}
+
+// Front vector = own rows of x + children's update vectors; the diagonal block's rows permuted
+// into x (the front's pivot order) and back into v.  Shared by the small-front and big-front
+// forward kernels.
+template <int NR>
+__device__ __forceinline__ void fwd_gather_front(const SNode& s, const SNode* __restrict__ sn,
+                                                 const int32_t* __restrict__ chlist,
+                                                 const int32_t* __restrict__ relmap,
+                                                 const int32_t* __restrict__ rowperm, double* __restrict__ x,
+                                                 double* __restrict__ vbuf, const Rhs& rh, int nr, int tid) {
+  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
+  map_ri<NR>(nr, M, tid, 256, [&](int r, int64_t i) { return i < ns ? x[r * rh.ldx + s.first + i] : 0.0; },
+             [&](int r, int64_t i, double val) { vbuf[r * rh.ldv + s.voff + i] = val; });
+  __syncthreads();
+  for (int c = s.chbeg; c < s.chend; ++c) {
+    const SNode ch = sn[chlist[c]];
+    const int32_t* rm = relmap + ch.rowptr;
+    // parent += child: both operands loaded per round (a child's relmap rows are distinct)
+    map_ri<NR>(nr, ch.nu, tid, 256,
+               [&](int r, int64_t i) {
+                 return vbuf[r * rh.ldv + s.voff + rm[i]] + vbuf[r * rh.ldv + ch.voff + ch.ns + i];
+               },
+               [&](int r, int64_t i, double val) { vbuf[r * rh.ldv + s.voff + rm[i]] = val; });
+    __syncthreads();
+  }
+  map_ri<NR>(nr, ns, tid, 256, [&](int r, int64_t i) { return vbuf[r * rh.ldv + s.voff + rowperm[s.first + i]]; },
+             [&](int r, int64_t i, double val) { x[r * rh.ldx + s.first + i] = val; });
+  __syncthreads();
+  map_ri<NR>(nr, ns, tid, 256, [&](int r, int64_t i) { return x[r * rh.ldx + s.first + i]; },
+             [&](int r, int64_t i, double val) { vbuf[r * rh.ldv + s.voff + i] = val; });
+}
+
+// v[i] -= sum_{j < bw} D[j*M + i] * xs[j][r] for every rhs r, rows i in [lo, hi): the old values
+// of all right-hand sides are loaded before the slab loop, stored after it.
+template <int NR>
+__device__ __forceinline__ void apply_block(const double* __restrict__ D, int64_t M, int bw, int64_t lo,
+                                            int64_t hi, const double (*xs)[NR], double* __restrict__ v,
+                                            const Rhs& rh, int nr, int tid) {
+  for (int64_t i = lo + tid; i < hi; i += 256) {
+    double acc[NR], o[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      acc[r] = 0.0;
+      o[r] = r < nr ? v[r * rh.ldv + i] : 0.0;
+    }
+#pragma unroll 1
+    for (int h = 0; h < 64; h += 32) {   // 32 slab values per memory round trip
+      double d[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) d[j] = h + j < bw ? D[(h + j) * M + i] : 0.0;
+#pragma unroll
+      for (int j = 0; j < 32; ++j) {
+        if (h + j < bw) {
+#pragma unroll
+          for (int r = 0; r < NR; ++r)
+            if (r < nr) acc[r] = fma(d[j], xs[h + j][r], acc[r]);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+      if (r < nr) v[r * rh.ldv + i] = o[r] - acc[r];
+  }
+}
+
+// Diagonal 64x64 block (staged in sD) solved for every rhs: waves take right-hand sides
+// round-robin; result into xs and v.
+template <bool UPPER, int NR>
+__device__ __forceinline__ void solve_block_lds(const double* __restrict__ sD, int64_t jb, int bw,
+                                                double (*xs)[NR], double* __restrict__ v, const Rhs& rh,
+                                                int nr, int lane, int wv) {
+  for (int r = wv; r < nr; r += 4) {
+    double* vr = v + r * rh.ldv;
+    double xi = lane < bw ? vr[jb + lane] : 0.0;
+    xi = tri_lds<UPPER>(xi, sD, bw, lane);
+    if (lane < bw) {
+      xs[lane][r] = xi;
+      vr[jb + lane] = xi;
+    }
+  }
+}
+
+template <int NR>
 __global__ __launch_bounds__(256) void k_fwd_front(const int32_t* __restrict__ list,
                                                    const SNode* __restrict__ sn,
                                                    const int32_t* __restrict__ chlist,
@@ -44,146 +158,133 @@ __global__ __launch_bounds__(256) void k_fwd_front(const int32_t* __restrict__ l
                                                    const int32_t* __restrict__ rowperm,
                                                    const double* __restrict__ store,
                                                    double* __restrict__ x,
-                                                   double* __restrict__ vbuf) {
-  __shared__ double xs[64];
+                                                   double* __restrict__ vbuf, Rhs rh) {
+  __shared__ double xs[64][NR];   // solved block, right-hand sides contiguous per column
   __shared__ double sD[64 * 65];
   const SNode s = sn[list[blockIdx.x]];
   const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
-  double* v = vbuf + s.voff;
-  double* xo = x + s.first;
+  const int nr = NR == 1 ? 1 : rh.n;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int64_t i = tid; i < M; i += 256) v[i] = i < ns ? xo[i] : 0.0;
-  __syncthreads();
-  for (int c = s.chbeg; c < s.chend; ++c) {
-    const SNode ch = sn[chlist[c]];
-    const double* u = vbuf + ch.voff + ch.ns;
-    const int32_t* rm = relmap + ch.rowptr;
-    for (int64_t i = tid; i < ch.nu; i += 256) v[rm[i]] += u[i];
-    __syncthreads();
-  }
-  // permuted diagonal-block right-hand side -> x positions (owned by this front)
-  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[rowperm[s.first + i]];
-  __syncthreads();
-  for (int64_t i = tid; i < ns; i += 256) v[i] = xo[i];
+  fwd_gather_front<NR>(s, sn, chlist, relmap, rowperm, x, vbuf, rh, nr, tid);
   __syncthreads();
   const double* Lp = store + s.Loff;
+  double* v = vbuf + s.voff;
   for (int64_t jb = 0; jb < ns; jb += 64) {
     const int bw = (int)min<int64_t>(64, ns - jb);
     stage_block(sD, Lp + jb * M + jb, M, bw, tid);
     __syncthreads();
-    if (wv == 0) {
-      double xi = lane < bw ? v[jb + lane] : 0.0;
-      xi = tri_lds<false>(xi, sD, bw, lane);
-      if (lane < bw) {
-        xs[lane] = xi;
-        v[jb + lane] = xi;
-      }
-    }
+    solve_block_lds<false, NR>(sD, jb, bw, xs, v, rh, nr, lane, wv);
     __syncthreads();
-    for (int64_t i = jb + bw + tid; i < M; i += 256) {
-      double acc = 0.0;
-#pragma unroll 8
-      for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
-      v[i] -= acc;
-    }
+    apply_block<NR>(Lp + jb * M, M, bw, jb + bw, M, xs, v, rh, nr, tid);
     __syncthreads();
   }
-  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[i];
+  map_ri<NR>(nr, ns, tid, 256, [&](int r, int64_t i) { return vbuf[r * rh.ldv + s.voff + i]; },
+             [&](int r, int64_t i, double val) { x[r * rh.ldx + s.first + i] = val; });
 }
 
 // Backward (U): x_s -= U12 * x[R_s]; then upper solve of the diagonal block from the bottom.
+template <int NR>
 __global__ __launch_bounds__(256) void k_bwd_front(const int32_t* __restrict__ list,
                                                    const SNode* __restrict__ sn,
                                                    const int32_t* __restrict__ rows,
                                                    const double* __restrict__ store,
                                                    double* __restrict__ x,
-                                                   double* __restrict__ vbuf) {
-  __shared__ double xs[64];
+                                                   double* __restrict__ vbuf, Rhs rh) {
+  __shared__ double xs[64][NR];   // solved block, right-hand sides contiguous per column
   __shared__ double sD[64 * 65];
   const SNode s = sn[list[blockIdx.x]];
   const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns, nu = s.nu;
-  double* v = vbuf + s.voff;
-  double* xo = x + s.first;
+  const int nr = NR == 1 ? 1 : rh.n;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int32_t* R = rows + s.rowptr;
-  for (int64_t i = tid; i < nu; i += 256) v[ns + i] = x[R[i]];
-  __syncthreads();
+  // x_s -= U12 x[R]: x[R] staged through LDS 64 columns at a time (xs doubles as the buffer)
   const double* U12 = store + s.Uoff;
-  for (int64_t i = tid; i < ns; i += 256) {
-    double acc = 0.0;
-#pragma unroll 8
-    for (int64_t j = 0; j < nu; ++j) acc = fma(U12[j * ns + i], v[ns + j], acc);
-    v[i] = xo[i] - acc;
+  for (int64_t i0 = 0; i0 < ns; i0 += 256) {
+    const int64_t i = i0 + tid;
+    double acc[NR], o[NR];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      acc[r] = 0.0;
+      o[r] = (i < ns && r < nr) ? x[r * rh.ldx + s.first + i] : 0.0;
+    }
+    for (int64_t jc = 0; jc < nu; jc += 64) {
+      const int cnt = (int)min<int64_t>(64, nu - jc);
+      __syncthreads();
+      map_ri<NR>(nr, cnt, tid, 256, [&](int r, int64_t j) { return x[r * rh.ldx + R[jc + j]]; },
+                 [&](int r, int64_t j, double val) { xs[j][r] = val; });
+      __syncthreads();
+      if (i < ns) {
+#pragma unroll 1
+        for (int h = 0; h < 64; h += 32) {   // 32 U12 values per memory round trip
+          double u[32];
+#pragma unroll
+          for (int j = 0; j < 32; ++j) u[j] = h + j < cnt ? U12[(jc + h + j) * ns + i] : 0.0;
+#pragma unroll
+          for (int j = 0; j < 32; ++j) {
+            if (h + j < cnt) {
+#pragma unroll
+              for (int r = 0; r < NR; ++r)
+                if (r < nr) acc[r] = fma(u[j], xs[h + j][r], acc[r]);
+            }
+          }
+        }
+      }
+    }
+    if (i < ns) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+        if (r < nr) vbuf[r * rh.ldv + s.voff + i] = o[r] - acc[r];
+    }
   }
-  __syncthreads();
+  __syncthreads();   // xs is reused by the diagonal sweep below
   const double* Lp = store + s.Loff;  // U11 in the upper triangle of the L panel
+  double* v = vbuf + s.voff;
   for (int64_t jb = ((ns - 1) / 64) * 64; jb >= 0; jb -= 64) {
     const int bw = (int)min<int64_t>(64, ns - jb);
     stage_block(sD, Lp + jb * M + jb, M, bw, tid);
     __syncthreads();
-    if (wv == 0) {
-      double xi = lane < bw ? v[jb + lane] : 0.0;
-      xi = tri_lds<true>(xi, sD, bw, lane);
-      if (lane < bw) {
-        xs[lane] = xi;
-        v[jb + lane] = xi;
-      }
-    }
+    solve_block_lds<true, NR>(sD, jb, bw, xs, v, rh, nr, lane, wv);
     __syncthreads();
-    for (int64_t i = tid; i < jb; i += 256) {
-      double acc = 0.0;
-#pragma unroll 8
-      for (int j = 0; j < bw; ++j) acc = fma(Lp[(jb + j) * M + i], xs[j], acc);
-      v[i] -= acc;
-    }
+    apply_block<NR>(Lp + jb * M, M, bw, 0, jb, xs, v, rh, nr, tid);
     __syncthreads();
   }
-  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[i];
+  map_ri<NR>(nr, ns, tid, 256, [&](int r, int64_t i) { return vbuf[r * rh.ldv + s.voff + i]; },
+             [&](int r, int64_t i, double val) { x[r * rh.ldx + s.first + i] = val; });
 }
 
 // ------------------------------------------------------------------------------------
 // Solves for large fronts (ns > 256): the diagonal block sweep is split over workgroups.
 // k_fwd_gather: front vector = own rows + children's update vectors, row permutation.
-// k_fwd_block (step t, jb = 64t): every workgroup re-solves the 64x64 unit-lower diagonal
-//   block from v (read-only in this launch), applies it to its 256-row chunk below; chunk 0
-//   publishes the solved block into x.  k_bwd_u12: x_s -= U12 x[R_s] by row chunks.
-// k_bwd_block: same as k_fwd_block for U11 from the bottom block up.
+// k_tri_block (step t): every workgroup re-solves the 64x64 diagonal block from v (read-only in
+//   this launch), applies it to its 256-row chunk; chunk 0 publishes the solved block into x.
+// k_bwd_u12: x_s -= U12 x[R_s] by row chunks.
 // ------------------------------------------------------------------------------------
+// One workgroup per (front, right-hand side): blockIdx.y selects the rhs.
 __global__ __launch_bounds__(256) void k_fwd_gather(const int32_t* __restrict__ list,
                                                     const SNode* __restrict__ sn,
                                                     const int32_t* __restrict__ chlist,
                                                     const int32_t* __restrict__ relmap,
                                                     const int32_t* __restrict__ rowperm,
-                                                    double* __restrict__ x, double* __restrict__ vbuf) {
+                                                    double* __restrict__ x, double* __restrict__ vbuf, Rhs rh) {
   const SNode s = sn[list[blockIdx.x]];
-  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
-  double* v = vbuf + s.voff;
-  double* xo = x + s.first;
-  const int tid = threadIdx.x;
-  for (int64_t i = tid; i < M; i += 256) v[i] = i < ns ? xo[i] : 0.0;
-  __syncthreads();
-  for (int c = s.chbeg; c < s.chend; ++c) {
-    const SNode ch = sn[chlist[c]];
-    const double* u = vbuf + ch.voff + ch.ns;
-    const int32_t* rm = relmap + ch.rowptr;
-    for (int64_t i = tid; i < ch.nu; i += 256) v[rm[i]] += u[i];
-    __syncthreads();
-  }
-  for (int64_t i = tid; i < ns; i += 256) xo[i] = v[rowperm[s.first + i]];
-  __syncthreads();
-  for (int64_t i = tid; i < ns; i += 256) v[i] = xo[i];
+  const int r = blockIdx.y;
+  fwd_gather_front<1>(s, sn, chlist, relmap, rowperm, x + r * rh.ldx, vbuf + r * rh.ldv, rh, 1, threadIdx.x);
 }
 
-// One 64-column step of a large front: wave 0 of every workgroup solves the 64x64 diagonal
-// block (tri64; each workgroup re-solves it, no inter-workgroup hand-off), waves 1-4 own one row
-// each of the workgroup's 256-row chunk and load that row's 64 slab values before the solved
-// block arrives (the two memory round trips overlap instead of following each other).
-template <bool UPPER>
-__global__ __launch_bounds__(320) void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step,
-                                                   const SNode* __restrict__ sn,
-                                                   const double* __restrict__ store,
-                                                   double* __restrict__ x, double* __restrict__ vbuf) {
-  __shared__ double xs[64];
+// One 64-column step of a large front: the first CW waves of every workgroup solve the 64x64
+// diagonal block for the right-hand sides (tri64, the diagonal block's rows loaded once per wave,
+// CW right-hand sides at a time; each workgroup re-solves it, no inter-workgroup hand-off); the
+// last four waves own one row each of the workgroup's 256-row chunk and load that row's 64 slab
+// values and its old values before the solved block arrives (the memory round trips overlap),
+// then apply the block to every right-hand side.  At most two waves per SIMD: d[64] and row[64]
+// keep 128 VGPRs live, so allow 256 rather than spill.
+template <bool UPPER, int NR>
+__global__ __launch_bounds__(NR == 1 ? 320 : 512) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step, const SNode* __restrict__ sn,
+                 const double* __restrict__ store, double* __restrict__ x, double* __restrict__ vbuf, Rhs rh) {
+  constexpr int CW = NR == 1 ? 1 : 4;        // chain waves
+  constexpr int PR = (NR + CW - 1) / CW;     // right-hand sides per chain wave
+  __shared__ double xs[64][NR];
   const int64_t b = blockIdx.x;
   const int fi = find_front_tile(ft, nft, b);
   const SNode s = sn[ft[fi].s];
@@ -192,15 +293,29 @@ __global__ __launch_bounds__(320) void k_tri_block(const FrontTile* __restrict__
   const int64_t nblk = (ns + 63) / 64;
   const int64_t jb = UPPER ? (nblk - 1 - step) * 64 : (int64_t)step * 64;
   const int bw = (int)min<int64_t>(64, ns - jb);
-  double* v = vbuf + s.voff;
+  const int nr = NR == 1 ? 1 : rh.n;
   const double* Lp = store + s.Loff;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (wv == 0) {
-    double xi = lane < bw ? v[jb + lane] : 0.0;
-    xi = tri64<UPPER>(xi, Lp + jb * M + jb, M, bw, lane);
-    if (lane < bw) {
-      xs[lane] = xi;
-      if (chunk == 0) x[s.first + jb + lane] = xi;
+  if (wv < CW) {
+    double xi[PR];
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+      const int r = wv + k * CW;
+      xi[k] = (r < nr && lane < bw) ? vbuf[r * rh.ldv + s.voff + jb + lane] : 0.0;
+    }
+    double row[64];   // the diagonal block's row `lane`, loaded once for all right-hand sides
+    load_row64(row, Lp + jb * M + jb, M, bw, lane);
+    const double dinv = UPPER ? diag_recip(Lp + jb * M + jb, M, bw, lane) : 1.0;
+#pragma unroll
+    for (int k = 0; k < PR; ++k) {
+      const int r = wv + k * CW;
+      if (r < nr) {
+        const double y = tri64_row<UPPER>(xi[k], row, dinv, bw, lane);
+        if (lane < bw) {
+          xs[lane][r] = y;
+          if (chunk == 0) x[r * rh.ldx + s.first + jb + lane] = y;
+        }
+      }
     }
     __syncthreads();
     return;
@@ -208,57 +323,89 @@ __global__ __launch_bounds__(320) void k_tri_block(const FrontTile* __restrict__
   // rows updated by this chunk: forward -> [jb+bw, M), backward -> [0, jb)
   const int64_t r0 = UPPER ? chunk * 256 : jb + bw + chunk * 256;
   const int64_t r1 = UPPER ? jb : M;
-  const int64_t i = r0 + tid - 64;
+  const int64_t i = r0 + tid - 64 * CW;
   const bool has = i < r1;
-  double d[64];
+  double d[64], o[NR];
 #pragma unroll
   for (int j = 0; j < 64; ++j) d[j] = (has && j < bw) ? Lp[(jb + j) * M + i] : 0.0;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) o[r] = (has && r < nr) ? vbuf[r * rh.ldv + s.voff + i] : 0.0;
   __syncthreads();
   if (has) {
-    double acc = 0.0;
 #pragma unroll
-    for (int j = 0; j < 64; ++j)
-      if (j < bw) acc = fma(d[j], xs[j], acc);
-    v[i] -= acc;
+    for (int r = 0; r < NR; ++r) {
+      if (r < nr) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < 64; ++j)
+          if (j < bw) acc = fma(d[j], xs[j][r], acc);
+        vbuf[r * rh.ldv + s.voff + i] = o[r] - acc;
+      }
+    }
   }
 }
 
-// x_s[i] (in v) = x[first+i] - sum_j U12[i,j] * x[R_j], 256 rows per workgroup
-// 64 rows per workgroup; wave w sums the columns [w*nu/4, (w+1)*nu/4) (x[R] staged in LDS
-// per 64-column chunk, 8 loads in flight), the four partial sums combined in wave order.
-__global__ __launch_bounds__(256) void k_bwd_u12(const FrontTile* __restrict__ ft, int nft,
+// x_s[i] (in v) = x[first+i] - sum_j U12[i,j] * x[R_j]: 64 rows per workgroup, 8 waves; wave w
+// sums the columns [w*nu/8, (w+1)*nu/8) 32 at a time, the 32 U12 loads of a chunk issued
+// together (8 waves x 32 x 512 B in flight per workgroup), x[R] staged per chunk in LDS; the
+// eight partial sums are combined in wave order; each U12 value is applied to every rhs.
+template <int NR>
+__global__ __launch_bounds__(512) void k_bwd_u12(const FrontTile* __restrict__ ft, int nft,
                                                  const SNode* __restrict__ sn,
                                                  const int32_t* __restrict__ rows,
                                                  const double* __restrict__ store,
                                                  const double* __restrict__ x,
-                                                 double* __restrict__ vbuf) {
-  __shared__ double xr[4][64];
-  __shared__ double part[4][64];
+                                                 double* __restrict__ vbuf, Rhs rh) {
+  constexpr int W = 8, JC = 32;
+  __shared__ double xr[W][JC][NR];
+  __shared__ double part[W][NR][64];
   const int64_t b = blockIdx.x;
   const int fi = find_front_tile(ft, nft, b);
   const SNode s = sn[ft[fi].s];
   const int64_t chunk = b - ft[fi].wg0;
   const int64_t ns = s.ns, nu = s.nu;
+  const int nr = NR == 1 ? 1 : rh.n;
   const int32_t* R = rows + s.rowptr;
   const double* U12 = store + s.Uoff;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t i = chunk * 64 + lane;
-  const int64_t j0 = nu * wv / 4, j1 = nu * (wv + 1) / 4;
-  double acc = 0.0;
-  for (int64_t jc = j0; jc < j1; jc += 64) {
-    const int cnt = (int)min<int64_t>(64, j1 - jc);
-    if (lane < cnt) xr[wv][lane] = x[R[jc + lane]];
+  const int64_t j0 = nu * wv / W, j1 = nu * (wv + 1) / W;
+  double acc[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) acc[r] = 0.0;
+  for (int64_t jc = j0; jc < j1; jc += JC) {
+    const int cnt = (int)min<int64_t>(JC, j1 - jc);
+    for (int e = lane; e < cnt * nr; e += 64) {
+      const int r = e / cnt, j = e - r * cnt;
+      xr[wv][j][r] = x[r * rh.ldx + R[jc + j]];
+    }
     wave_lds_sync();
     if (i < ns) {
-#pragma unroll 8
-      for (int j = 0; j < cnt; ++j) acc = fma(U12[(jc + j) * ns + i], xr[wv][j], acc);
+      double u[JC];
+#pragma unroll
+      for (int j = 0; j < JC; ++j) u[j] = j < cnt ? U12[(jc + j) * ns + i] : 0.0;
+#pragma unroll
+      for (int j = 0; j < JC; ++j) {
+        if (j < cnt) {
+#pragma unroll
+          for (int r = 0; r < NR; ++r)
+            if (r < nr) acc[r] = fma(u[j], xr[wv][j][r], acc[r]);
+        }
+      }
     }
     wave_lds_sync();   // every lane's reads of this chunk before the next chunk overwrites it
   }
-  part[wv][lane] = acc;
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (r < nr) part[wv][r][lane] = acc[r];
   __syncthreads();
   if (wv == 0 && i < ns)
-    vbuf[s.voff + i] = x[s.first + i] - (((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]);
+    for (int r = 0; r < nr; ++r) {
+      double t = part[0][r][lane];
+#pragma unroll
+      for (int w = 1; w < W; ++w) t += part[w][r][lane];
+      vbuf[r * rh.ldv + s.voff + i] = x[r * rh.ldx + s.first + i] - t;
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -298,20 +445,20 @@ __global__ void k_vcopy(const SNode* __restrict__ sn, int node, const double* __
   if (i < s.ns) vbuf[s.voff + i] = x[s.first + i];
 }
 
-// wrk[i] = Rs[p0[i]] * b[p0[i]]
+// wrk[r][i] = Rs[p0[i]] * b[r][p0[i]]   (blockIdx.y = right-hand side)
 __global__ void k_perm_in(int64_t n, const int64_t* __restrict__ p0, const double* __restrict__ Rs,
-                          const double* __restrict__ b, double* __restrict__ wrk) {
+                          const double* __restrict__ b, int64_t ldb, double* __restrict__ wrk, int64_t ldw) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) {
     int64_t r = p0[i];
-    wrk[i] = Rs[r] * b[r];
+    wrk[blockIdx.y * ldw + i] = Rs[r] * b[blockIdx.y * ldb + r];
   }
 }
-// x[q[i]] = wrk[i]
-__global__ void k_perm_out(int64_t n, const int64_t* __restrict__ q, const double* __restrict__ wrk,
-                           double* __restrict__ x) {
+// x[r][q[i]] = wrk[r][i]
+__global__ void k_perm_out(int64_t n, const int64_t* __restrict__ q, const double* __restrict__ wrk, int64_t ldw,
+                           double* __restrict__ x, int64_t ldx) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) x[q[i]] = wrk[i];
+  if (i < n) x[blockIdx.y * ldx + q[i]] = wrk[blockIdx.y * ldw + i];
 }
 // final order -> pre-swap positions: out[first + rowperm[first+i]] = in[first+i]
 __global__ void k_unswap(int64_t n, const int64_t* __restrict__ pos_first,
@@ -362,35 +509,57 @@ __global__ void k_axpy1(int64_t n, const double* __restrict__ d, double* __restr
 static inline unsigned nblk(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 hipError_t launch_fwd(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
                       const int32_t* chlist, const int32_t* relmap, const int32_t* rowperm,
-                      const double* store, double* x, double* vbuf) {
+                      const double* store, double* x, double* vbuf, Rhs rh) {
   if (cnt <= 0) return hipSuccess;
-  k_fwd_front<<<cnt, 256, 0, st>>>(list, sn, chlist, relmap, rowperm, store, x, vbuf);
+  if (rh.n < 1 || rh.n > kMaxRhs) return hipErrorInvalidValue;
+  if (rh.n == 1) k_fwd_front<1><<<cnt, 256, 0, st>>>(list, sn, chlist, relmap, rowperm, store, x, vbuf, rh);
+  else if (rh.n <= 4) k_fwd_front<4><<<cnt, 256, 0, st>>>(list, sn, chlist, relmap, rowperm, store, x, vbuf, rh);
+  else if (rh.n <= 8) k_fwd_front<8><<<cnt, 256, 0, st>>>(list, sn, chlist, relmap, rowperm, store, x, vbuf, rh);
+  else k_fwd_front<16><<<cnt, 256, 0, st>>>(list, sn, chlist, relmap, rowperm, store, x, vbuf, rh);
   return hipGetLastError();
 }
 hipError_t launch_bwd(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
-                      const int32_t* rows, const double* store, double* x, double* vbuf) {
+                      const int32_t* rows, const double* store, double* x, double* vbuf, Rhs rh) {
   if (cnt <= 0) return hipSuccess;
-  k_bwd_front<<<cnt, 256, 0, st>>>(list, sn, rows, store, x, vbuf);
+  if (rh.n < 1 || rh.n > kMaxRhs) return hipErrorInvalidValue;
+  if (rh.n == 1) k_bwd_front<1><<<cnt, 256, 0, st>>>(list, sn, rows, store, x, vbuf, rh);
+  else if (rh.n <= 4) k_bwd_front<4><<<cnt, 256, 0, st>>>(list, sn, rows, store, x, vbuf, rh);
+  else if (rh.n <= 8) k_bwd_front<8><<<cnt, 256, 0, st>>>(list, sn, rows, store, x, vbuf, rh);
+  else k_bwd_front<16><<<cnt, 256, 0, st>>>(list, sn, rows, store, x, vbuf, rh);
   return hipGetLastError();
 }
 hipError_t launch_fwd_gather(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
                              const int32_t* chlist, const int32_t* relmap, const int32_t* rowperm,
-                             double* x, double* vbuf) {
+                             double* x, double* vbuf, Rhs rh) {
   if (cnt <= 0) return hipSuccess;
-  k_fwd_gather<<<cnt, 256, 0, st>>>(list, sn, chlist, relmap, rowperm, x, vbuf);
+  if (rh.n < 1 || rh.n > kMaxRhs) return hipErrorInvalidValue;
+  k_fwd_gather<<<dim3((unsigned)cnt, (unsigned)rh.n), 256, 0, st>>>(list, sn, chlist, relmap, rowperm, x, vbuf, rh);
   return hipGetLastError();
 }
 hipError_t launch_tri_block(hipStream_t st, bool upper, int64_t nwg, const FrontTile* ft, int nft,
-                            int step, const SNode* sn, const double* store, double* x, double* vbuf) {
+                            int step, const SNode* sn, const double* store, double* x, double* vbuf, Rhs rh) {
   if (nwg <= 0) return hipSuccess;
-  if (upper) k_tri_block<true><<<(unsigned)nwg, 320, 0, st>>>(ft, nft, step, sn, store, x, vbuf);
-  else k_tri_block<false><<<(unsigned)nwg, 320, 0, st>>>(ft, nft, step, sn, store, x, vbuf);
+  if (rh.n < 1 || rh.n > kMaxRhs) return hipErrorInvalidValue;
+  // one chain wave for a single vector (320 threads), four for a batch (512)
+#define SMLU_TRI(NRV, THR)                                                                           \
+  (upper ? (k_tri_block<true, NRV><<<(unsigned)nwg, THR, 0, st>>>(ft, nft, step, sn, store, x, vbuf, rh)) \
+         : (k_tri_block<false, NRV><<<(unsigned)nwg, THR, 0, st>>>(ft, nft, step, sn, store, x, vbuf, rh)))
+  if (rh.n == 1) SMLU_TRI(1, 320);
+  else if (rh.n <= 4) SMLU_TRI(4, 512);
+  else if (rh.n <= 8) SMLU_TRI(8, 512);
+  else SMLU_TRI(16, 512);
+#undef SMLU_TRI
   return hipGetLastError();
 }
 hipError_t launch_bwd_u12(hipStream_t st, int64_t nwg, const FrontTile* ft, int nft, const SNode* sn,
-                          const int32_t* rows, const double* store, const double* x, double* vbuf) {
+                          const int32_t* rows, const double* store, const double* x, double* vbuf, Rhs rh) {
   if (nwg <= 0) return hipSuccess;
-  k_bwd_u12<<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sn, rows, store, x, vbuf);
+  if (rh.n < 1 || rh.n > kMaxRhs) return hipErrorInvalidValue;
+  // accumulators per right-hand side in registers: instantiate for the batch width
+  if (rh.n == 1) k_bwd_u12<1><<<(unsigned)nwg, 512, 0, st>>>(ft, nft, sn, rows, store, x, vbuf, rh);
+  else if (rh.n <= 4) k_bwd_u12<4><<<(unsigned)nwg, 512, 0, st>>>(ft, nft, sn, rows, store, x, vbuf, rh);
+  else if (rh.n <= 8) k_bwd_u12<8><<<(unsigned)nwg, 512, 0, st>>>(ft, nft, sn, rows, store, x, vbuf, rh);
+  else k_bwd_u12<16><<<(unsigned)nwg, 512, 0, st>>>(ft, nft, sn, rows, store, x, vbuf, rh);
   return hipGetLastError();
 }
 hipError_t launch_residual(hipStream_t st, int64_t n, const int64_t* rowptr, const int32_t* ent,
@@ -406,8 +575,8 @@ hipError_t launch_axpy1(hipStream_t st, int64_t n, const double* d, double* x) {
   return hipGetLastError();
 }
 hipError_t launch_perm_in(hipStream_t st, int64_t n, const int64_t* p0, const double* Rs,
-                          const double* b, double* wrk) {
-  k_perm_in<<<nblk(n, 256), 256, 0, st>>>(n, p0, Rs, b, wrk);
+                          const double* b, double* wrk, int nrhs, int64_t ldb, int64_t ldw) {
+  k_perm_in<<<dim3(nblk(n, 256), (unsigned)nrhs), 256, 0, st>>>(n, p0, Rs, b, ldb, wrk, ldw);
   return hipGetLastError();
 }
 hipError_t launch_segcopy(hipStream_t st, const SegDesc* d, int64_t nd) {
@@ -476,8 +645,9 @@ hipError_t launch_chunked_solve(hipStream_t st, bool upper, int64_t nchunk, cons
   return hipGetLastError();
 }
 
-hipError_t launch_perm_out(hipStream_t st, int64_t n, const int64_t* q, const double* wrk, double* x) {
-  k_perm_out<<<nblk(n, 256), 256, 0, st>>>(n, q, wrk, x);
+hipError_t launch_perm_out(hipStream_t st, int64_t n, const int64_t* q, const double* wrk, double* x, int nrhs,
+                           int64_t ldw, int64_t ldx) {
+  k_perm_out<<<dim3(nblk(n, 256), (unsigned)nrhs), 256, 0, st>>>(n, q, wrk, ldw, x, ldx);
   return hipGetLastError();
 }
 hipError_t launch_unswap(hipStream_t st, int64_t n, const int64_t* pos_first, const int32_t* rowperm,

@@ -157,6 +157,8 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
                              std::max<int64_t>(opt.grid[2], 1), opt.leaf_size);
   } else if (opt.ordering == 2) {
     return "geometric ND needs grid[] with prod(grid) == n";
+  } else if (opt.ordering == 5) {
+    ord = order_amd(g);
   } else {
     ord = order_graph_nd(g, opt.leaf_size);
   }

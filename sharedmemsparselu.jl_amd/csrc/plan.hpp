@@ -35,6 +35,7 @@ Graph build_sym_graph(int64_t n, const int64_t* colptr, const int32_t* rowval);
 // Orderings return perm (new -> old).
 std::vector<int64_t> order_geometric_nd(int64_t nx, int64_t ny, int64_t nz, int64_t leaf);
 std::vector<int64_t> order_graph_nd(const Graph& g, int64_t leaf);
+std::vector<int64_t> order_amd(const Graph& g);   // approximate minimum degree (amd.cpp)
 std::vector<int64_t> zero_free_diagonal(int64_t n, const int64_t* colptr, const int32_t* rowval,
                                         const double* a);
 

@@ -50,20 +50,21 @@ hipError_t launch_gemm(hipStream_t, int64_t, const GemmTask*, int, int, int64_t)
 hipError_t launch_gemm_g(hipStream_t, int64_t, const GemmTask*, int, int, int64_t, int32_t*, double*, double);
 hipError_t launch_tri_inv(hipStream_t, int, int, const int32_t*, const SNode*, double*, double*, double*);
 hipError_t launch_fwd_gather(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
-                             const int32_t*, double*, double*);
+                             const int32_t*, double*, double*, Rhs);
 hipError_t launch_tri_block(hipStream_t, bool, int64_t, const FrontTile*, int, int, const SNode*,
-                            const double*, double*, double*);
+                            const double*, double*, double*, Rhs);
 hipError_t launch_bwd_u12(hipStream_t, int64_t, const FrontTile*, int, const SNode*, const int32_t*,
-                          const double*, const double*, double*);
+                          const double*, const double*, double*, Rhs);
 hipError_t launch_fwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
-                      const int32_t*, const double*, double*, double*);
+                      const int32_t*, const double*, double*, double*, Rhs);
 hipError_t launch_bwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*,
-                      double*, double*);
+                      double*, double*, Rhs);
 hipError_t launch_residual(hipStream_t, int64_t, const int64_t*, const int32_t*, const int32_t*,
                            const double*, const double*, const double*, double*, double*);
 hipError_t launch_axpy1(hipStream_t, int64_t, const double*, double*);
-hipError_t launch_perm_in(hipStream_t, int64_t, const int64_t*, const double*, const double*, double*);
-hipError_t launch_perm_out(hipStream_t, int64_t, const int64_t*, const double*, double*);
+hipError_t launch_perm_in(hipStream_t, int64_t, const int64_t*, const double*, const double*, double*, int,
+                          int64_t, int64_t);
+hipError_t launch_perm_out(hipStream_t, int64_t, const int64_t*, const double*, double*, int, int64_t, int64_t);
 hipError_t launch_chunked_solve(hipStream_t, bool, int64_t, const ChunkDesc*, const double*, double*);
 hipError_t launch_segcopy(hipStream_t, const SegDesc*, int64_t);
 hipError_t launch_bwd_u12_cols(hipStream_t, const SNode*, int, int64_t, int64_t, int64_t, int, const int32_t*,
@@ -311,6 +312,7 @@ struct smlu_handle {
   bool given_Rs = false;
   // device buffers
   DBuf<double> A, Rs, store, scratch, wrk, wrk2, vbuf, growth;
+  DBuf<double> vbufm, wrkm, wrk2m;   // multi-RHS solve: kMultiRhs copies of vbuf / wrk / wrk2 (on first use)
   DBuf<double> tinv;   // per (front, sub-panel) slot: I - L_kk^-1 and I - U_kk^-1 (GEMM-form TRSM)
   // the reference's dense-chunk solve layout, rebuilt after each factorization
   DBuf<double> ch_data;
@@ -391,7 +393,7 @@ struct smlu_handle {
   void release_buffers() {
     if (stream) (void)hipSetDevice(device);
     release_graphs();
-    DBuf<double>* d[] = {&A, &Rs, &store, &scratch, &wrk, &wrk2, &vbuf, &growth, &ref_b, &ref_r, &ref_d, &ref_nrm,
+    DBuf<double>* d[] = {&A, &Rs, &store, &scratch, &wrk, &wrk2, &vbuf, &vbufm, &wrkm, &wrk2m, &growth, &ref_b, &ref_r, &ref_d, &ref_nrm,
                          &tinv, &ch_data};
     ch_desc.free();
     ch_p.free();
@@ -2384,6 +2386,7 @@ static void release_schedule(smlu_handle* h) {
   h->xcols.free();
   h->swaps.free();
   h->vbuf.free();
+  h->vbufm.free();
   h->tinv.free();
   h->stage_s.free();
   h->stage_r.free();
@@ -2428,26 +2431,28 @@ static int run_factor(smlu_handle* h) {
   return rc;
 }
 
-static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w) {
+// One solve launch for rh.n right-hand sides (x columns at w + r*rh.ldx, front vectors at
+// v + r*rh.ldv); the multi-GPU kinds (K_BWDU12C, K_VCOPY) are single-vector only.
+static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, double* v, Rhs rh) {
   hipStream_t st = h->stream;
   switch (L.kind) {
     case K_FWD:
       return launch_fwd(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->chlist.p, h->relmap.p,
-                        h->rowperm.p, h->store.p, w, h->vbuf.p);
+                        h->rowperm.p, h->store.p, w, v, rh);
     case K_BWD:
-      return launch_bwd(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->rows.p, h->store.p, w, h->vbuf.p);
+      return launch_bwd(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->rows.p, h->store.p, w, v, rh);
     case K_FWDG:
       return launch_fwd_gather(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->chlist.p, h->relmap.p,
-                               h->rowperm.p, w, h->vbuf.p);
+                               h->rowperm.p, w, v, rh);
     case K_TRIF:
       return launch_tri_block(st, false, L.nwg, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p,
-                              h->store.p, w, h->vbuf.p);
+                              h->store.p, w, v, rh);
     case K_TRIB:
       return launch_tri_block(st, true, L.nwg, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p,
-                              h->store.p, w, h->vbuf.p);
+                              h->store.p, w, v, rh);
     case K_BWDU:
-      return launch_bwd_u12(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->sn.p, h->rows.p, h->store.p, w,
-                            h->vbuf.p);
+      return launch_bwd_u12(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->sn.p, h->rows.p, h->store.p, w, v,
+                            rh);
     case K_BWDU12C:
       return launch_bwd_u12_cols(st, h->sn.p, L.node, h->hsn[L.node].ns, L.aux, L.aux2, (int)L.cnt, h->rows.p,
                                  h->store.p, w, h->vbuf.p);
@@ -2457,17 +2462,30 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w) {
   return hipErrorInvalidValue;
 }
 
-static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode) {
-  // mode 0: ldiv (b -> x); 1: lsolve in place on dx (final order); 2: rsolve in place
+static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode, int nrhs = 1, int64_t ldb = 0,
+                         int64_t ldx = 0) {
+  // mode 0: ldiv (b -> x); 1: lsolve in place on dx (final order); 2: rsolve in place.
+  // nrhs > 1 (mode 0, one GPU): columns of db / dx with leading dimensions ldb / ldx.
   Plan& P = h->plan;
   if (h->nranks > 1 && mode != 0) return fail(h, SMLU_ERR_STATE, "lsolve!/rsolve! are single-GPU only");
+  if (nrhs > 1 && (mode != 0 || h->nranks > 1 || nrhs > kMultiRhs))
+    return fail(h, SMLU_ERR_STATE, "batched right-hand sides: ldiv on one GPU only");
   hipStream_t st = h->stream;
   auto t0 = std::chrono::steady_clock::now();
   Timer tm(h);
   hipEvent_t stop;
   HIPCHK(tm.begin(K_FWD, &stop, h->stream));
   double* w = h->wrk.p;
-  if (mode == 0) HIPCHK(launch_perm_in(st, P.n, h->p0.p, h->Rs.p, db, w));
+  double* v = h->vbuf.p;
+  Rhs rh{1, (int64_t)P.n, (int64_t)h->vbuf.n};
+  if (nrhs > 1) {
+    if (!h->vbufm.p) HIPCHK(h->vbufm.alloc(h->vbuf.n * kMultiRhs));
+    if (!h->wrkm.p) HIPCHK(h->wrkm.alloc((size_t)P.n * kMultiRhs));
+    w = h->wrkm.p;
+    v = h->vbufm.p;
+    rh.n = nrhs;
+  }
+  if (mode == 0) HIPCHK(launch_perm_in(st, P.n, h->p0.p, h->Rs.p, db, w, nrhs, ldb > 0 ? ldb : P.n, rh.ldx));
   if (mode == 1) HIPCHK(launch_unswap(st, P.n, h->posfirst.p, h->rowperm.p, dx, w));
   if (mode == 2) HIPCHK(hipMemcpyAsync(w, dx, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st));
   // launches between communication steps (one GPU: a single segment each)
@@ -2478,7 +2496,7 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode)
         if (rc != SMLU_OK) return rc;
       }
       const size_t hi = k + 1 < seg.size() ? seg[k + 1] : seq.size();
-      for (size_t i = seg[k]; i < hi; ++i) HIPCHK(run_solve_launch(h, seq[i], w));
+      for (size_t i = seg[k]; i < hi; ++i) HIPCHK(run_solve_launch(h, seq[i], w, v, rh));
     }
     return (int)SMLU_OK;
   };
@@ -2490,7 +2508,7 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode)
     int rc = run_seq(h->bwd, h->bwd_seg, h->bwd_comm);
     if (rc != SMLU_OK) return rc;
   }
-  if (mode == 0) HIPCHK(launch_perm_out(st, P.n, h->q.p, w, dx));
+  if (mode == 0) HIPCHK(launch_perm_out(st, P.n, h->q.p, w, dx, nrhs, rh.ldx, ldx > 0 ? ldx : P.n));
   else HIPCHK(hipMemcpyAsync(dx, w, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st));
   HIPCHK(tm.end(stop));
   HIPCHK(hipStreamSynchronize(st));
@@ -2812,7 +2830,34 @@ int smlu_solve(smlu_handle* h, const double* b, double* x) {
   return SMLU_OK;
 }
 
-// Multiple right-hand sides: one solve per column, reusing the captured solve schedule.
+// Multiple right-hand sides.  One GPU without refinement: batches of up to kMultiRhs columns go
+// through the solve kernels together (each factor value read once per batch, not per column);
+// otherwise (refinement, several GPUs) one refined solve per column.  d_B may alias d_X when
+// ldb == ldx (the batch is permuted into the work buffer before x is written).
+static int solve_multi_dev(smlu_handle* h, int64_t nrhs, const double* d_B, int64_t ldb, double* d_X,
+                           int64_t ldx) {
+  const int steps = h->opts.refine < 0 ? (h->weak > 0 ? 3 : 0) : h->opts.refine;
+  const bool batched = steps == 0 && h->nranks == 1 && nrhs > 1 && !std::getenv("SMLU_NO_MULTI_RHS");
+  if (!batched) {
+    for (int64_t j = 0; j < nrhs; ++j) {
+      int rc = solve_refined(h, d_B + j * ldb, d_X + j * ldx);
+      if (rc != SMLU_OK) return rc;
+    }
+    return SMLU_OK;
+  }
+  h->refine_steps = 0;
+  h->refine_resid = -1;
+  double ms = 0;
+  for (int64_t j = 0; j < nrhs; j += kMultiRhs) {
+    const int nb = (int)std::min<int64_t>(kMultiRhs, nrhs - j);
+    int rc = run_solve_dev(h, d_B + j * ldb, d_X + j * ldx, 0, nb, ldb, ldx);
+    if (rc != SMLU_OK) return rc;
+    ms += h->solve_ms;
+  }
+  h->solve_ms = ms;
+  return SMLU_OK;
+}
+
 int smlu_solve_multi_device(smlu_handle* h, int64_t nrhs, const double* d_B, int64_t ldb, double* d_X,
                             int64_t ldx) {
   if (!h || nrhs < 0 || (nrhs > 0 && (!d_B || !d_X))) return fail(h, SMLU_ERR_ARG, "invalid arguments");
@@ -2820,11 +2865,7 @@ int smlu_solve_multi_device(smlu_handle* h, int64_t nrhs, const double* d_B, int
   const int64_t n = h->plan.n;
   if (ldb < n || ldx < n) return fail(h, SMLU_ERR_ARG, "leading dimension smaller than n");
   HIPCHK(hipSetDevice(h->device));
-  for (int64_t j = 0; j < nrhs; ++j) {
-    int rc = solve_refined(h, d_B + j * ldb, d_X + j * ldx);
-    if (rc != SMLU_OK) return rc;
-  }
-  return SMLU_OK;
+  return solve_multi_dev(h, nrhs, d_B, ldb, d_X, ldx);
 }
 
 int smlu_solve_multi(smlu_handle* h, int64_t nrhs, const double* B, int64_t ldb, double* X, int64_t ldx) {
@@ -2833,6 +2874,21 @@ int smlu_solve_multi(smlu_handle* h, int64_t nrhs, const double* B, int64_t ldb,
   const int64_t n = h->plan.n;
   if (ldb < n || ldx < n) return fail(h, SMLU_ERR_ARG, "leading dimension smaller than n");
   HIPCHK(hipSetDevice(h->device));
+  if (nrhs > 1 && h->nranks == 1 && (h->opts.refine == 0 || (h->opts.refine < 0 && h->weak == 0))) {
+    if (!h->wrk2m.p) HIPCHK(h->wrk2m.alloc((size_t)n * kMultiRhs));
+    double* d = h->wrk2m.p;
+    for (int64_t j = 0; j < nrhs; j += kMultiRhs) {
+      const int64_t nb = std::min<int64_t>(kMultiRhs, nrhs - j);
+      HIPCHK(hipMemcpy2DAsync(d, sizeof(double) * n, B + j * ldb, sizeof(double) * ldb, sizeof(double) * n, nb,
+                              hipMemcpyHostToDevice, h->stream));
+      int rc = solve_multi_dev(h, nb, d, n, d, n);
+      if (rc != SMLU_OK) return rc;
+      HIPCHK(hipMemcpy2DAsync(X + j * ldx, sizeof(double) * ldx, d, sizeof(double) * n, sizeof(double) * n, nb,
+                              hipMemcpyDeviceToHost, h->stream));
+    }
+    HIPCHK(hipStreamSynchronize(h->stream));
+    return SMLU_OK;
+  }
   for (int64_t j = 0; j < nrhs; ++j) {
     HIPCHK(hipMemcpyAsync(h->wrk2.p, B + j * ldb, sizeof(double) * n, hipMemcpyHostToDevice, h->stream));
     int rc = solve_refined(h, h->wrk2.p, h->wrk2.p);
@@ -3226,10 +3282,10 @@ int smlu_chunked_ldiv_device(smlu_handle* h, const double* d_b, double* d_x) {
   hipStream_t st = h->stream;
   const int64_t n = h->plan.n;
   double* w = h->wrk.p;
-  HIPCHK(launch_perm_in(st, n, h->ch_p.p, h->Rs.p, d_b, w));
+  HIPCHK(launch_perm_in(st, n, h->ch_p.p, h->Rs.p, d_b, w, 1, n, n));
   HIPCHK(launch_chunked_solve(st, false, h->ch_T, h->ch_desc.p, h->ch_data.p, w));
   HIPCHK(launch_chunked_solve(st, true, h->ch_T, h->ch_desc.p + h->ch_T, h->ch_data.p, w));
-  HIPCHK(launch_perm_out(st, n, h->ch_q.p, w, d_x));
+  HIPCHK(launch_perm_out(st, n, h->ch_q.p, w, d_x, 1, n, n));
   HIPCHK(hipStreamSynchronize(st));
   return SMLU_OK;
 }

@@ -30,7 +30,7 @@ SMLU_ERR_HIP = -4
 SMLU_ERR_NODEVICE = -5
 SMLU_ERR_STATE = -6
 
-ORDER_AUTO, ORDER_NATURAL, ORDER_GEOMETRIC_ND, ORDER_GRAPH_ND, ORDER_GIVEN = range(5)
+ORDER_AUTO, ORDER_NATURAL, ORDER_GEOMETRIC_ND, ORDER_GRAPH_ND, ORDER_GIVEN, ORDER_AMD = range(6)
 
 
 class SmluOpts(ctypes.Structure):

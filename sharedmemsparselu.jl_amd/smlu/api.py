@@ -74,7 +74,7 @@ class ParallelSparseLU:
             chunk_size = 8                       # :67-70
         chunk_size = min(int(chunk_size), n)     # :72
         order = {"auto": C.ORDER_AUTO, "natural": C.ORDER_NATURAL, "nd": C.ORDER_GRAPH_ND,
-                 "geometric": C.ORDER_GEOMETRIC_ND, "given": C.ORDER_GIVEN}[ordering]
+                 "geometric": C.ORDER_GEOMETRIC_ND, "amd": C.ORDER_AMD, "given": C.ORDER_GIVEN}[ordering]
         kw = dict(chunk_size=chunk_size, index_base=0, ordering=order, device=device,
                   profile=1 if profile else 0, relax=1 if relax else 0)
         if grid is not None:
@@ -178,6 +178,16 @@ class ParallelSparseLU:
         pb = d_b.data_ptr() if hasattr(d_b, "data_ptr") else int(d_b)
         return _check(C.lib().smlu_solve_device(self._h, ctypes.c_void_p(pb), ctypes.c_void_p(px)),
                       self._h)
+
+    def solve_multi_device(self, d_X, d_B):
+        """ldiv! for several right-hand sides on the device: d_B, d_X are (nrhs, n) contiguous
+        torch tensors (column r = row r, i.e. column-major n x nrhs).  One GPU: batches of up to
+        16 columns go through the solve kernels together."""
+        nrhs, n = d_B.shape
+        if n != self.n or tuple(d_X.shape) != (nrhs, n):
+            raise DimensionMismatch(f"B has shape {tuple(d_B.shape)}, X has shape {tuple(d_X.shape)}, n={self.n}")
+        return _check(C.lib().smlu_solve_multi_device(self._h, nrhs, ctypes.c_void_p(d_B.data_ptr()), n,
+                                                      ctypes.c_void_p(d_X.data_ptr()), n), self._h)
 
     def close(self):
         h = getattr(self, "_h", None)

@@ -104,7 +104,7 @@ class DistributedSparseLU:
         A = _csc(A)
         self.n = A.shape[0]
         order = {"auto": C.ORDER_AUTO, "natural": C.ORDER_NATURAL, "nd": C.ORDER_GRAPH_ND,
-                 "geometric": C.ORDER_GEOMETRIC_ND}[ordering]
+                 "geometric": C.ORDER_GEOMETRIC_ND, "amd": C.ORDER_AMD}[ordering]
         o = C.default_opts(index_base=0, ordering=order, device=self.device.index, **opts)
         self._colptr = np.ascontiguousarray(A.indptr, dtype=np.int64)
         self._rowval = np.ascontiguousarray(A.indices, dtype=np.int64)

@@ -18,7 +18,7 @@ class Plan:
         A.sum_duplicates()
         n = A.shape[0]
         order = {"auto": C.ORDER_AUTO, "natural": C.ORDER_NATURAL, "nd": C.ORDER_GRAPH_ND,
-                 "geometric": C.ORDER_GEOMETRIC_ND}[ordering]
+                 "geometric": C.ORDER_GEOMETRIC_ND, "amd": C.ORDER_AMD}[ordering]
         kw = dict(index_base=0, ordering=order, relax=1 if relax else 0)
         if grid is not None:
             kw["grid"] = grid

@@ -39,6 +39,21 @@ def test_poisson3d_factors(gpu, N, grid):
     assert isapprox(x, spla.spsolve(A, b), TOL, TOL)
 
 
+@pytest.mark.parametrize("make", [lambda: mats.poisson2d(30), lambda: mats.poisson3d(12),
+                                  lambda: O.test_matrix(np.random.default_rng(3), 57, 5)],
+                         ids=["poisson2d_30", "poisson3d_12", "fe_57"])
+def test_amd_ordering_factors(gpu, make):
+    # SMLU_ORDER_AMD: factors against the oracle on the same (p, q), solve against SuperLU
+    A = sp.csc_matrix(make())
+    F = smlu.ParallelSparseLU(A, ordering="amd")
+    factor_parity(A, F, rtol=1e-10)
+    assert F.stat("nnzLU") > 0
+    b = np.random.default_rng(2).random(A.shape[0])
+    x = np.empty_like(b)
+    smlu.ldiv_(x, F, b)
+    assert isapprox(x, spla.spsolve(A, b), TOL, TOL)
+
+
 @pytest.mark.parametrize("nel", [1, 2, 3, 7, 20, 57, 200])
 def test_fe_matrix_ldiv(gpu, nel):
     rng = np.random.default_rng(47 + nel)
@@ -206,6 +221,29 @@ def test_solve_multiple_rhs(gpu):
         assert isapprox(xj, spla.spsolve(A, B[:, j]), TOL, TOL)
     with pytest.raises(smlu.DimensionMismatch):
         smlu.ldiv_(np.empty((n, 4)), F, B)
+
+
+@pytest.mark.parametrize("k,nrhs", [(20, 3), (24, 20)])
+def test_solve_multiple_rhs_batched(gpu, k, nrhs):
+    # batched multi-RHS kernels (16 columns per launch) on 3D Poisson with large fronts (the
+    # 64-column block steps): every column bitwise equal to its single-vector solve; host and
+    # device entry points agree; nrhs=20 spans two batches.
+    import torch
+    A = mats.poisson3d(k)
+    n = A.shape[0]
+    F = smlu.ParallelSparseLU(A)
+    B = np.random.default_rng(9).random((n, nrhs))
+    X = np.empty((n, nrhs))
+    smlu.ldiv_(X, F, B)
+    dB = torch.from_numpy(np.ascontiguousarray(B.T)).cuda()
+    dX = torch.empty_like(dB)
+    F.solve_multi_device(dX, dB)
+    assert np.array_equal(dX.cpu().numpy().T, X)
+    for j in range(nrhs):
+        xj = np.empty(n)
+        smlu.ldiv_(xj, F, B[:, j])
+        assert np.array_equal(xj, X[:, j]), j
+    assert isapprox(X[:, -1], spla.spsolve(A, B[:, -1]), TOL, TOL)
 
 
 def test_int32_indices(gpu):
