@@ -129,6 +129,30 @@ int smlu_solve_multi_device(smlu_handle* h, int64_t nrhs, const double* d_B, int
 int smlu_create_i32(int64_t n, const int32_t* colptr, const int32_t* rowval, const double* nzval,
                     const smlu_opts* opts, smlu_handle** out);
 
+/* ParallelSparseLU(A::SparseMatrixCSC{ComplexF64}) — the reference is generic in Tf
+ * (src/SharedMemSparseLU.jl:43, :64, :286).  nzval holds 2*nnz doubles,
+ * interleaved (re, im) per entry (Julia's ComplexF64 / C99 double complex layout).
+ * The handle factors the real-equivalent K (2n x 2n, entry x+iy -> block [[x,-y],[y,x]] at rows
+ * 2i,2i+1 / columns 2j,2j+1) on the real GPU path, so on a complex handle:
+ *   - smlu_solve[_device], smlu_solve_multi[_device], smlu_residual_device, smlu_lsolve/rsolve
+ *     and smlu_chunked_* take complex vectors as 2n interleaved doubles (ldb/ldx in doubles);
+ *   - smlu_get_sizes / smlu_get_factors describe K's factors (n reported as 2n);
+ *   - smlu_last_error_col reports the complex column;  smlu_stat(h, "complex") == 1.
+ * The column order is computed on the complex pattern (opts.ordering; SMLU_ORDER_GIVEN is
+ * refused) and kept pairwise, so each 2x2 block stays in one front. */
+int smlu_create_z(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
+                  const smlu_opts* opts, smlu_handle** out);
+
+/* lu!(F, A) for a complex handle (same pattern; host values, 2*nnz doubles interleaved). */
+int smlu_refactor_z(smlu_handle* h, const double* nzval);
+
+/* Same, complex values already in device memory (16-byte aligned); expanded into K on the GPU. */
+int smlu_refactor_z_device(smlu_handle* h, const double* d_nzval);
+
+/* lu!(F, A) for a complex handle where the pattern may differ (re-analysis, :252-273). */
+int smlu_refactor_csc_z(smlu_handle* h, int64_t n, const int64_t* colptr, const int64_t* rowval,
+                        const double* nzval);
+
 /* lsolve!(F, x) — src/SharedMemSparseLU.jl:349-367: in place L \ x on an already
  * row-permuted and scaled host vector (x in the reference's F.p order). */
 int smlu_lsolve(smlu_handle* h, double* x);

@@ -14,6 +14,12 @@ Contents
   ``fill_chunks!`` (:180-243, rectangular chunks store the NEGATED values), ``lsolve!``
   (:349-367, ``trsv!('L','N','U')`` + ``gemm!`` with alpha = beta = 1) and ``rsolve!``
   (:374-392, chunks walked from the back).
+* :func:`real_equivalent` — ComplexF64 (the reference is generic in ``Tf``,
+  src/SharedMemSparseLU.jl:43,:64,:286): the real 2n x 2n matrix K in which a complex entry
+  x + iy is the block [[x, -y], [y, x]] at rows 2i, 2i+1 / columns 2j, 2j+1.  An LU of K is an
+  LU of the complex operator; interleaved complex vectors are vectors of K.  The oracle's LU of
+  K is the checker of the library's complex path; the complex solutions are pinned against
+  scipy's complex SuperLU (tests/test_oracle.py).
 * :func:`test_matrix` — the reference's FE-like fixture generator (test/runtests.jl:12-21),
   restated over a numpy Generator (Julia's MersenneTwister stream is not reproduced).
 
@@ -260,3 +266,34 @@ def test_matrix(rng, nel=6, ngr=5):
         imax = iel * (ngr - 1) + 1
         mat[imin - 1:imax, imin - 1:imax] = rng.random((ngr, ngr))
     return sp.csc_matrix(mat)
+
+
+def real_equivalent(A):
+    """ComplexF64 A (n x n) -> its real-equivalent K (2n x 2n CSC, sorted): entry a_ij = x + iy
+    becomes K[2i, 2j] = x, K[2i+1, 2j] = y, K[2i, 2j+1] = -y, K[2i+1, 2j+1] = x.  Every stored
+    complex entry gives four stored entries (zeros included), so K's pattern is value-independent.
+    Interleaved complex vectors (re, im, ...) -- ``z.view(np.float64)`` -- are vectors of K."""
+    A = sp.csc_matrix(A, dtype=np.complex128)
+    A.sort_indices()
+    n = A.shape[0]
+    cp, ri = A.indptr.astype(np.int64), A.indices.astype(np.int64)
+    nnz = cp[-1]
+    Kp = np.zeros(2 * n + 1, np.int64)
+    Ki = np.empty(4 * nnz, np.int64)
+    Kx = np.empty(4 * nnz)
+    for j in range(n):
+        c0, c = cp[j], cp[j + 1] - cp[j]
+        k0 = 4 * c0
+        Kp[2 * j + 1] = k0 + 2 * c
+        Kp[2 * j + 2] = k0 + 4 * c
+        r = ri[c0:c0 + c]
+        v = A.data[c0:c0 + c]
+        Ki[k0:k0 + 2 * c:2] = 2 * r
+        Ki[k0 + 1:k0 + 2 * c:2] = 2 * r + 1
+        Kx[k0:k0 + 2 * c:2] = v.real
+        Kx[k0 + 1:k0 + 2 * c:2] = v.imag
+        Ki[k0 + 2 * c:k0 + 4 * c:2] = 2 * r
+        Ki[k0 + 2 * c + 1:k0 + 4 * c:2] = 2 * r + 1
+        Kx[k0 + 2 * c:k0 + 4 * c:2] = -v.imag
+        Kx[k0 + 2 * c + 1:k0 + 4 * c:2] = v.real
+    return sp.csc_matrix((Kx, Ki, Kp), shape=(2 * n, 2 * n))

@@ -502,6 +502,18 @@ __global__ void k_axpy1(int64_t n, const double* __restrict__ d, double* __restr
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] += d[i];
 }
+// ComplexF64 values (interleaved re, im per entry of A's CSC) -> the real-equivalent K's values:
+// entry e of complex column j lands as (re, im) at dst[e] (column 2j) and as (-im, re) at
+// dst[e] + off[e] (column 2j+1).  One lane per complex entry, 16-byte loads, two 16-byte stores.
+__global__ void k_expand_z(int64_t nnz, const double2* __restrict__ z, const int64_t* __restrict__ dst,
+                           const int32_t* __restrict__ off, double* __restrict__ K) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nnz) return;
+  const double2 v = z[e];
+  const int64_t d = dst[e];
+  *reinterpret_cast<double2*>(K + d) = v;
+  *reinterpret_cast<double2*>(K + d + off[e]) = make_double2(-v.y, v.x);
+}
 
 // ------------------------------------------------------------------------------------
 // Host-side launch wrappers (called from smlu.cpp)
@@ -572,6 +584,12 @@ hipError_t launch_residual(hipStream_t st, int64_t n, const int64_t* rowptr, con
 hipError_t launch_axpy1(hipStream_t st, int64_t n, const double* d, double* x) {
   if (n <= 0) return hipSuccess;
   k_axpy1<<<nblk(n, 256), 256, 0, st>>>(n, d, x);
+  return hipGetLastError();
+}
+hipError_t launch_expand_z(hipStream_t st, int64_t nnz, const double* z, const int64_t* dst, const int32_t* off,
+                           double* K) {
+  if (nnz <= 0) return hipSuccess;
+  k_expand_z<<<nblk(nnz, 256), 256, 0, st>>>(nnz, reinterpret_cast<const double2*>(z), dst, off, K);
   return hipGetLastError();
 }
 hipError_t launch_perm_in(hipStream_t st, int64_t n, const int64_t* p0, const double* Rs,

@@ -82,7 +82,32 @@ std::vector<int64_t> postorder(const std::vector<int64_t>& parent) {
   return post;
 }
 
+std::vector<int64_t> order_on_graph(int64_t n, const Graph& g, const PlanOptions& opt, std::string& err) {
+  std::vector<int64_t> ord;
+  if (opt.ordering == 1) {
+    ord.resize(n);
+    std::iota(ord.begin(), ord.end(), 0);
+  } else if ((opt.ordering == 0 || opt.ordering == 2) && opt.grid[0] > 0 &&
+             opt.grid[0] * std::max<int64_t>(opt.grid[1], 1) * std::max<int64_t>(opt.grid[2], 1) == n) {
+    ord = order_geometric_nd(opt.grid[0], std::max<int64_t>(opt.grid[1], 1),
+                             std::max<int64_t>(opt.grid[2], 1), opt.leaf_size);
+  } else if (opt.ordering == 2) {
+    err = "geometric ND needs grid[] with prod(grid) == n";
+  } else if (opt.ordering == 5) {
+    ord = order_amd(g);
+  } else {
+    ord = order_graph_nd(g, opt.leaf_size);
+  }
+  return ord;
+}
+
 }  // namespace
+
+std::vector<int64_t> compute_order(int64_t n, const int64_t* colptr, const int32_t* rowval,
+                                   const PlanOptions& opt, std::string& err) {
+  Graph g = build_sym_graph(n, colptr, rowval);
+  return order_on_graph(n, g, opt, err);
+}
 
 std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval, int base,
                         const PlanOptions& opt, const int64_t* pgiven, const int64_t* qgiven,
@@ -148,19 +173,12 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
   if (given_order) {
     ord.resize(n);
     for (int64_t k = 0; k < n; ++k) ord[k] = qgiven[k] - base;
-  } else if (opt.ordering == 1) {
-    ord.resize(n);
-    std::iota(ord.begin(), ord.end(), 0);
-  } else if ((opt.ordering == 0 || opt.ordering == 2) && opt.grid[0] > 0 &&
-             opt.grid[0] * std::max<int64_t>(opt.grid[1], 1) * std::max<int64_t>(opt.grid[2], 1) == n) {
-    ord = order_geometric_nd(opt.grid[0], std::max<int64_t>(opt.grid[1], 1),
-                             std::max<int64_t>(opt.grid[2], 1), opt.leaf_size);
-  } else if (opt.ordering == 2) {
-    return "geometric ND needs grid[] with prod(grid) == n";
-  } else if (opt.ordering == 5) {
-    ord = order_amd(g);
+  } else if (!opt.preorder.empty()) {
+    ord = opt.preorder;
   } else {
-    ord = order_graph_nd(g, opt.leaf_size);
+    std::string err;
+    ord = order_on_graph(n, g, opt, err);
+    if (!err.empty()) return err;
   }
   if ((int64_t)ord.size() != n) return "ordering is not a permutation";
   {

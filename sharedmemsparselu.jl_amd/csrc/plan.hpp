@@ -22,6 +22,10 @@ struct PlanOptions {
   int64_t grid[3] = {0, 0, 0};
   int relax = 1;
   int64_t leaf_size = 64;
+  // Column order to use instead of computing one (new -> old, 0-based; empty = compute).
+  // Pivoting stays on, unlike a given (p, q).  Used by the ComplexF64 path: the order is
+  // computed on the complex pattern and expanded to the real-equivalent 2x2 blocks.
+  std::vector<int64_t> preorder;
 };
 
 // Symmetric adjacency (A + A'), no diagonal, deduplicated, CSR.
@@ -36,6 +40,10 @@ Graph build_sym_graph(int64_t n, const int64_t* colptr, const int32_t* rowval);
 std::vector<int64_t> order_geometric_nd(int64_t nx, int64_t ny, int64_t nz, int64_t leaf);
 std::vector<int64_t> order_graph_nd(const Graph& g, int64_t leaf);
 std::vector<int64_t> order_amd(const Graph& g);   // approximate minimum degree (amd.cpp)
+// The ordering Plan::build would compute for the pattern (0-based CSC) under `opt`
+// (natural / geometric ND / AMD / graph ND); empty with `err` set on a bad option.
+std::vector<int64_t> compute_order(int64_t n, const int64_t* colptr, const int32_t* rowval,
+                                   const PlanOptions& opt, std::string& err);
 std::vector<int64_t> zero_free_diagonal(int64_t n, const int64_t* colptr, const int32_t* rowval,
                                         const double* a);
 

@@ -62,6 +62,7 @@ hipError_t launch_bwd(hipStream_t, int, const int32_t*, const SNode*, const int3
 hipError_t launch_residual(hipStream_t, int64_t, const int64_t*, const int32_t*, const int32_t*,
                            const double*, const double*, const double*, double*, double*);
 hipError_t launch_axpy1(hipStream_t, int64_t, const double*, double*);
+hipError_t launch_expand_z(hipStream_t, int64_t, const double*, const int64_t*, const int32_t*, double*);
 hipError_t launch_perm_in(hipStream_t, int64_t, const int64_t*, const double*, const double*, double*, int,
                           int64_t, int64_t);
 hipError_t launch_perm_out(hipStream_t, int64_t, const int64_t*, const double*, double*, int, int64_t, int64_t);
@@ -389,6 +390,14 @@ struct smlu_handle {
   int64_t vendor_calls = 0;   // rocBLAS dgemm calls per factorization
   int vendor_kinds = 3;       // launch kinds routed to rocBLAS: 1 F22, 2 trailing, 4 U rows, 8 in-block (SMLU_ROCBLAS_KINDS)
   std::vector<GemmTask> hgt;  // host copy of the GEMM tasks (rocBLAS calls read their operands from it)
+  // ComplexF64 handle (smlu_create_z): the plan and factors are those of the real-equivalent K
+  bool zc = false;
+  int64_t zn = 0, znnz = 0;          // complex n and nnz(A)
+  std::vector<int64_t> zdst;         // per complex entry: K position of its (re, im) in column 2j
+  std::vector<int32_t> zoff;         // ... and the distance to its (-im, re) in column 2j+1
+  std::vector<int64_t> zcolptr, zrowval;   // complex pattern (0-based), for pattern checks
+  DBuf<int64_t> d_zdst;
+  DBuf<int32_t> d_zoff;
   ~smlu_handle() { release_all(); }
   void release_buffers() {
     if (stream) (void)hipSetDevice(device);
@@ -406,6 +415,8 @@ struct smlu_handle {
     DBuf<int32_t>* i[] = {&Arow_ent, &Arow, &rows, &relmap, &chlist, &ilist, &rowperm, &rowperm0, &info, &swaps};
     for (auto* b : i) b->free();
     sn.free();
+    d_zdst.free();
+    d_zoff.free();
     xtasks.free();
     aents.free();
     ftiles.free();
@@ -2568,7 +2579,7 @@ static std::vector<int64_t> diagonal_match(int64_t n, const int64_t* colptr, con
 static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
                        const int64_t* p, const int64_t* q, const double* Rs, const smlu_opts* opts,
                        smlu_handle** out, int rank = 0, int nranks = 1, const smlu_transport* tr = nullptr,
-                       RcclState* rccl = nullptr) {
+                       RcclState* rccl = nullptr, const std::vector<int64_t>* preorder = nullptr) {
   std::unique_ptr<RcclState> rccl_own(rccl);   // owned by the handle once it exists
   if (!out) return fail(nullptr, SMLU_ERR_ARG, "out is NULL");
   *out = nullptr;
@@ -2589,7 +2600,9 @@ static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, 
     std::vector<int64_t> match;
     if (!p && h->opts.ordering != SMLU_ORDER_GIVEN)
       match = diagonal_match(n, colptr, rowval, nzval, h->opts.index_base);
-    e = h->plan.build(n, colptr, rowval, h->opts.index_base, plan_opts(h->opts), p, q,
+    PlanOptions po = plan_opts(h->opts);
+    if (preorder) po.preorder = *preorder;
+    e = h->plan.build(n, colptr, rowval, h->opts.index_base, po, p, q,
                       match.empty() ? nullptr : match.data());
   } catch (const std::bad_alloc&) {
     return fail(nullptr, SMLU_ERR_ALLOC, "host allocation failed during analysis");
@@ -2702,9 +2715,20 @@ int smlu_refactor_device(smlu_handle* h, const double* d_nzval) {
   return run_factor(h);
 }
 
+static int refactor_csc_impl(smlu_handle* h, int64_t n, const int64_t* colptr, const int64_t* rowval,
+                             const double* nzval, const std::vector<int64_t>* preorder);
+
 int smlu_refactor_csc(smlu_handle* h, int64_t n, const int64_t* colptr, const int64_t* rowval,
                       const double* nzval) {
   if (!h || !colptr || !rowval || !nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  if (h->zc) return fail(h, SMLU_ERR_ARG, "complex handle: use smlu_refactor_csc_z");
+  return refactor_csc_impl(h, n, colptr, rowval, nzval, nullptr);
+}
+
+}  // extern "C"
+
+static int refactor_csc_impl(smlu_handle* h, int64_t n, const int64_t* colptr, const int64_t* rowval,
+                             const double* nzval, const std::vector<int64_t>* preorder) {
   if (h->nranks > 1) return fail(h, SMLU_ERR_STATE, "partitioned handle: create a new one for a new pattern");
   const Plan& P = h->plan;
   int base = h->opts.index_base;
@@ -2721,7 +2745,9 @@ int smlu_refactor_csc(smlu_handle* h, int64_t n, const int64_t* colptr, const in
   std::string e;
   try {
     std::vector<int64_t> match = diagonal_match(n, colptr, rowval, nzval, base);
-    e = h->plan.build(n, colptr, rowval, base, plan_opts(h->opts), nullptr, nullptr,
+    PlanOptions po = plan_opts(h->opts);
+    if (preorder) po.preorder = *preorder;
+    e = h->plan.build(n, colptr, rowval, base, po, nullptr, nullptr,
                       match.empty() ? nullptr : match.data());
   } catch (const std::bad_alloc&) {
     return fail(h, SMLU_ERR_ALLOC, "host allocation failed during analysis");
@@ -2734,6 +2760,181 @@ int smlu_refactor_csc(smlu_handle* h, int64_t n, const int64_t* colptr, const in
   HIPCHK(hipMemcpyAsync(h->A.p, nzval, sizeof(double) * h->plan.nnzA, hipMemcpyHostToDevice, h->stream));
   return run_factor(h);
 }
+
+extern "C" {
+
+}  // extern "C"
+
+// ---- ComplexF64 (the reference is generic in Tf, src/SharedMemSparseLU.jl:43,64,286)
+// A complex A is factored as its real-equivalent K (2n x 2n): the entry a_ij = x + iy becomes the
+// 2x2 block [[x, -y], [y, x]] at rows 2i, 2i+1 and columns 2j, 2j+1.  K = L U with threshold
+// pivoting is an LU of the complex operator, so every kernel of the real path (MFMA Schur
+// updates included) runs unchanged, and an interleaved complex vector (re, im, re, im, ...) IS a
+// vector of K: the solve entry points take complex buffers as 2n doubles.  Column 2j of K holds
+// complex column j's values verbatim, column 2j+1 the pairs (-y, x).  The column order is
+// computed on the complex pattern and expanded to (2k, 2k+1) pairs, so each 2x2 block stays
+// inside one front.  Cost: 2x the flops and factor bytes of a native complex LU.
+namespace {
+struct ZExpand {
+  std::vector<int64_t> colptr, rowval;   // K's pattern, in the caller's index base
+  std::vector<int64_t> dst;
+  std::vector<int32_t> off;
+  std::vector<int64_t> zcolptr, zrowval; // the complex pattern, 0-based
+  std::vector<int64_t> preorder;         // K column order (pairs)
+};
+
+std::string z_expand(int64_t n, const int64_t* colptr, const int64_t* rowval, int base, const smlu_opts& o,
+                     ZExpand& Z) {
+  if (n <= 0 || n >= (int64_t)INT32_MAX / 2) return "invalid n for a complex matrix";
+  if (colptr[0] != base) return "colptr[0] must equal index_base";
+  const int64_t nnz = colptr[n] - base;
+  if (nnz < 0 || nnz > (int64_t)INT32_MAX) return "invalid nnz";
+  Z.zcolptr.resize(n + 1);
+  Z.zrowval.resize(nnz);
+  std::vector<int32_t> r32(nnz);
+  for (int64_t j = 0; j <= n; ++j) {
+    Z.zcolptr[j] = colptr[j] - base;
+    if (j > 0 && Z.zcolptr[j] < Z.zcolptr[j - 1]) return "colptr not monotone";
+  }
+  if (Z.zcolptr[n] != nnz) return "colptr not monotone";
+  for (int64_t e = 0; e < nnz; ++e) {
+    const int64_t r = rowval[e] - base;
+    if (r < 0 || r >= n) return "row index out of range";
+    Z.zrowval[e] = r;
+    r32[e] = (int32_t)r;
+  }
+  Z.colptr.assign(2 * n + 1, base);
+  Z.rowval.resize(4 * nnz);
+  Z.dst.resize(nnz);
+  Z.off.resize(nnz);
+  for (int64_t j = 0; j < n; ++j) {
+    const int64_t c0 = Z.zcolptr[j], c = Z.zcolptr[j + 1] - c0, k0 = 4 * c0;
+    Z.colptr[2 * j + 1] = base + k0 + 2 * c;
+    Z.colptr[2 * j + 2] = base + k0 + 4 * c;
+    for (int64_t t = 0; t < c; ++t) {
+      const int64_t r = Z.zrowval[c0 + t];
+      Z.rowval[k0 + 2 * t] = Z.rowval[k0 + 2 * c + 2 * t] = base + 2 * r;
+      Z.rowval[k0 + 2 * t + 1] = Z.rowval[k0 + 2 * c + 2 * t + 1] = base + 2 * r + 1;
+      Z.dst[c0 + t] = k0 + 2 * t;
+      Z.off[c0 + t] = (int32_t)(2 * c);
+    }
+  }
+  std::string err;
+  std::vector<int64_t> ord;
+  if (o.ordering == SMLU_ORDER_GIVEN) return "complex handles compute their own order";
+  ord = compute_order(n, Z.zcolptr.data(), r32.data(), plan_opts(o), err);
+  if (!err.empty()) return err;
+  if ((int64_t)ord.size() != n) return "ordering is not a permutation";
+  Z.preorder.resize(2 * n);
+  for (int64_t k = 0; k < n; ++k) {
+    Z.preorder[2 * k] = 2 * ord[k];
+    Z.preorder[2 * k + 1] = 2 * ord[k] + 1;
+  }
+  return "";
+}
+
+void z_values(const std::vector<int64_t>& dst, const std::vector<int32_t>& off, const double* z, double* K) {
+  const int64_t nnz = (int64_t)dst.size();
+  for (int64_t e = 0; e < nnz; ++e) {
+    const double x = z[2 * e], y = z[2 * e + 1];
+    const int64_t d = dst[e];
+    K[d] = x;
+    K[d + 1] = y;
+    K[d + off[e]] = -y;
+    K[d + off[e] + 1] = x;
+  }
+}
+
+void z_adopt(smlu_handle* h, int64_t n, ZExpand& Z) {
+  h->zc = true;
+  h->zn = n;
+  h->znnz = (int64_t)Z.dst.size();
+  h->zdst.swap(Z.dst);
+  h->zoff.swap(Z.off);
+  h->zcolptr.swap(Z.zcolptr);
+  h->zrowval.swap(Z.zrowval);
+  h->d_zdst.free();
+  h->d_zoff.free();
+}
+}  // namespace
+
+extern "C" {
+
+int smlu_create_z(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
+                  const smlu_opts* opts, smlu_handle** out) {
+  if (!out) return fail(nullptr, SMLU_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  if (n <= 0 || !colptr || !nzval) return fail(nullptr, SMLU_ERR_ARG, "invalid matrix arguments");
+  smlu_opts o;
+  if (opts) o = *opts;
+  else smlu_default_opts(&o);
+  if (!valid_opts(&o)) return fail(nullptr, SMLU_ERR_ARG, "index_base must be 0 or 1");
+  if (colptr[n] - o.index_base > 0 && !rowval) return fail(nullptr, SMLU_ERR_ARG, "invalid matrix arguments");
+  ZExpand Z;
+  std::vector<double> K;
+  try {
+    std::string e = z_expand(n, colptr, rowval, o.index_base, o, Z);
+    if (!e.empty()) return fail(nullptr, SMLU_ERR_ARG, e);
+    K.resize(Z.rowval.size());
+    z_values(Z.dst, Z.off, nzval, K.data());
+  } catch (const std::bad_alloc&) {
+    return fail(nullptr, SMLU_ERR_ALLOC, "host allocation failed");
+  }
+  if (o.chunk_size > 0) o.chunk_size = std::min<int64_t>(2 * o.chunk_size, 2 * n);
+  int rc = create_impl(2 * n, Z.colptr.data(), Z.rowval.data(), K.data(), nullptr, nullptr, nullptr, &o, out,
+                       0, 1, nullptr, nullptr, &Z.preorder);
+  if (*out) z_adopt(*out, n, Z);
+  return rc;
+}
+
+int smlu_refactor_z(smlu_handle* h, const double* nzval) {
+  if (!h || !nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  if (!h->zc) return fail(h, SMLU_ERR_ARG, "not a complex handle (smlu_create_z)");
+  std::vector<double> K(h->plan.nnzA);
+  z_values(h->zdst, h->zoff, nzval, K.data());
+  return smlu_refactor(h, K.data());
+}
+
+int smlu_refactor_z_device(smlu_handle* h, const double* d_nzval) {
+  if (!h || !d_nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  if (!h->zc) return fail(h, SMLU_ERR_ARG, "not a complex handle (smlu_create_z)");
+  if (reinterpret_cast<uintptr_t>(d_nzval) % 16) return fail(h, SMLU_ERR_ARG, "complex values must be 16-byte aligned");
+  HIPCHK(hipSetDevice(h->device));
+  if (!h->d_zdst.p) {
+    HIPCHK(h->d_zdst.upload(h->zdst.data(), h->zdst.size(), h->stream));
+    HIPCHK(h->d_zoff.upload(h->zoff.data(), h->zoff.size(), h->stream));
+  }
+  HIPCHK(launch_expand_z(h->stream, h->znnz, d_nzval, h->d_zdst.p, h->d_zoff.p, h->A.p));
+  return run_factor(h);
+}
+
+int smlu_refactor_csc_z(smlu_handle* h, int64_t n, const int64_t* colptr, const int64_t* rowval,
+                        const double* nzval) {
+  if (!h || !colptr || !rowval || !nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  if (!h->zc) return fail(h, SMLU_ERR_ARG, "not a complex handle (smlu_create_z)");
+  const int base = h->opts.index_base;
+  bool same = (n == h->zn) && colptr[n] - base == h->znnz;
+  for (int64_t j = 0; same && j <= n; ++j) same = (colptr[j] - base == h->zcolptr[j]);
+  for (int64_t e = 0; same && e < h->znnz; ++e) same = (rowval[e] - base == h->zrowval[e]);
+  if (same) return smlu_refactor_z(h, nzval);
+  ZExpand Z;
+  std::vector<double> K;
+  try {
+    std::string e = z_expand(n, colptr, rowval, base, h->opts, Z);
+    if (!e.empty()) return fail(h, SMLU_ERR_ARG, e);
+    K.resize(Z.rowval.size());
+    z_values(Z.dst, Z.off, nzval, K.data());
+  } catch (const std::bad_alloc&) {
+    return fail(h, SMLU_ERR_ALLOC, "host allocation failed");
+  }
+  const std::vector<int64_t> pre = Z.preorder;
+  z_adopt(h, n, Z);
+  return refactor_csc_impl(h, 2 * n, Z.colptr.data(), Z.rowval.data(), K.data(), &pre);
+}
+
+}  // extern "C"
+
+extern "C" {
 
 // ldiv! plus iterative refinement on the original (unscaled) A: x <- x + A \ (b - A x).  The
 // diagonal-tile pivoting of large fronts cannot always keep growth below 1/pivot_tol; when a
@@ -3310,7 +3511,10 @@ const char* smlu_last_error_string(const smlu_handle* h) {
   return g_last_error.c_str();
 }
 
-int64_t smlu_last_error_col(const smlu_handle* h) { return h ? h->errcol : -1; }
+int64_t smlu_last_error_col(const smlu_handle* h) {
+  if (!h) return -1;
+  return (h->zc && h->errcol >= 0) ? h->errcol / 2 : h->errcol;   // complex handle: column of A
+}
 
 static double plan_stat(const Plan& P, const std::string& k) {
   if (k == "n") return (double)P.n;
@@ -3342,6 +3546,7 @@ static double plan_stat(const Plan& P, const std::string& k) {
 double smlu_stat(const smlu_handle* h, const char* key) {
   if (!h || !key) return std::numeric_limits<double>::quiet_NaN();
   std::string k(key);
+  if (k == "complex") return h->zc ? 1.0 : 0.0;
   if (k == "launches") return (double)h->nlaunch;
   if (k == "refactor_ms_last") return h->refactor_ms;
   if (k == "solve_ms_last") return h->solve_ms;

@@ -3,10 +3,13 @@ module SharedMemSparseLU
 
 export ParallelSparseLU, cleanup_ParallelSparseLU!, allocate_shared
 
-using LinearAlgebra, SparseArrays
+using LinearAlgebra, SparseArrays, Libdl
 import LinearAlgebra: ldiv!, lu!
 
 const libsmlu = get(ENV, "SMLU_LIB", joinpath(@__DIR__, "..", "deps", "libsmlu.so"))
+
+# entry point chosen at run time (ccall's literal (name, lib) form needs a constant name)
+fnptr(name::Symbol) = Libdl.dlsym(Libdl.dlopen(libsmlu), name)
 
 # must match `smlu_opts` in include/smlu.h field for field
 mutable struct SmluOpts
@@ -38,15 +41,37 @@ mutable struct ParallelSparseLU{Tf,Ti}
     chunk_size::Ti
 end
 
-function ParallelSparseLU(A::SparseMatrixCSC{Float64,Int64}, chunk_size=nothing)
+# Tf in (Float64, ComplexF64), Ti in (Int64, Int32): the reference is generic in both
+# (src/SharedMemSparseLU.jl:43, :64; SURVEY §8f-4).  Int32 indices go through smlu_create_i32
+# (real) or are widened here (complex); complex values go through smlu_create_z as interleaved
+# (re, im) doubles -- the memory layout of Vector{ComplexF64}.
+const SmluFloat = Union{Float64,ComplexF64}
+const SmluInt = Union{Int64,Int32}
+
+function ParallelSparseLU(A::SparseMatrixCSC{Tf,Ti}, chunk_size=nothing) where {Tf<:SmluFloat,Ti<:SmluInt}
     chunk_size = min(something(chunk_size, 8), A.n)           # :67-72
     o = default_opts(); o.chunk_size = chunk_size
     h = Ref{Ptr{Cvoid}}(C_NULL)
-    rc = ccall((:smlu_create, libsmlu), Int32,
-               (Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Ref{SmluOpts}, Ref{Ptr{Cvoid}}),
-               A.n, A.colptr, A.rowval, A.nzval, o, h)
+    if Tf === ComplexF64
+        rc = ccall((:smlu_create_z, libsmlu), Int32,
+                   (Int64, Ptr{Int64}, Ptr{Int64}, Ptr{ComplexF64}, Ref{SmluOpts}, Ref{Ptr{Cvoid}}),
+                   A.n, Vector{Int64}(A.colptr), Vector{Int64}(A.rowval), A.nzval, o, h)
+    elseif Ti === Int32
+        rc = ccall((:smlu_create_i32, libsmlu), Int32,
+                   (Int64, Ptr{Int32}, Ptr{Int32}, Ptr{Float64}, Ref{SmluOpts}, Ref{Ptr{Cvoid}}),
+                   A.n, A.colptr, A.rowval, A.nzval, o, h)
+    else
+        rc = ccall((:smlu_create, libsmlu), Int32,
+                   (Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Ref{SmluOpts}, Ref{Ptr{Cvoid}}),
+                   A.n, A.colptr, A.rowval, A.nzval, o, h)
+    end
+    if rc == 1 && h[] != C_NULL                   # singular: free the handle, then throw
+        col = ccall((:smlu_last_error_col, libsmlu), Int64, (Ptr{Cvoid},), h[])
+        ccall((:smlu_destroy, libsmlu), Cvoid, (Ptr{Cvoid},), h[])
+        throw(SingularException(col + 1))
+    end
     check(rc, h[])
-    F = ParallelSparseLU{Float64,Int64}(A.m, A.n, h[], copy(A.colptr), copy(A.rowval), chunk_size)
+    F = ParallelSparseLU{Tf,Ti}(A.m, A.n, h[], copy(A.colptr), copy(A.rowval), chunk_size)
     finalizer(cleanup_ParallelSparseLU!, F)
     return F
 end
@@ -60,43 +85,71 @@ function ParallelSparseLU_umfpack(A::SparseMatrixCSC{Float64,Int64})
                 Ptr{Float64}, Ref{SmluOpts}, Ref{Ptr{Cvoid}}),
                A.n, A.colptr, A.rowval, A.nzval, U.p, U.q, U.Rs, o, h)
     check(rc, h[])
-    return ParallelSparseLU{Float64,Int64}(A.m, A.n, h[], copy(A.colptr), copy(A.rowval), 8)
+    F = ParallelSparseLU{Float64,Int64}(A.m, A.n, h[], copy(A.colptr), copy(A.rowval), 8)
+    finalizer(cleanup_ParallelSparseLU!, F)
+    return F
 end
 
 function lu!(F::ParallelSparseLU{Tf,Ti}, A::SparseMatrixCSC{Tf,Ti}) where {Tf,Ti}   # :245-279
+    z = Tf === ComplexF64
     if A.colptr == F.colptr && A.rowval == F.rowval
-        rc = ccall((:smlu_refactor, libsmlu), Int32, (Ptr{Cvoid}, Ptr{Float64}), F.handle, A.nzval)
+        rc = ccall(fnptr(z ? :smlu_refactor_z : :smlu_refactor), Int32, (Ptr{Cvoid}, Ptr{Tf}),
+                   F.handle, A.nzval)
     else                                                                          # :265-273
-        rc = ccall((:smlu_refactor_csc, libsmlu), Int32,
-                   (Ptr{Cvoid}, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}),
-                   F.handle, A.n, A.colptr, A.rowval, A.nzval)
+        rc = ccall(fnptr(z ? :smlu_refactor_csc_z : :smlu_refactor_csc), Int32,
+                   (Ptr{Cvoid}, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Tf}),
+                   F.handle, A.n, Vector{Int64}(A.colptr), Vector{Int64}(A.rowval), A.nzval)
         F.colptr = copy(A.colptr); F.rowval = copy(A.rowval)
     end
     check(rc, F.handle)
     return nothing
 end
 
-function ldiv!(x::AbstractVector, F::ParallelSparseLU, b::AbstractVector)        # :286-342
+function ldiv!(x::AbstractVecOrMat, F::ParallelSparseLU{Tf}, b::AbstractVecOrMat) where {Tf}   # :286-342
     @boundscheck F.m == F.n || throw(DimensionMismatch("`F` is not square: F.m=$(F.m), F.n=$(F.n)"))
-    @boundscheck length(x) == F.n || throw(DimensionMismatch("`x` does not have same size as F: length(x)=$(length(x)), F.n=$(F.n)"))
-    @boundscheck length(b) == F.n || throw(DimensionMismatch("`b` does not have same size as F: length(b)=$(length(b)), F.n=$(F.n)"))
-    bb = b isa Vector{Float64} ? b : Vector{Float64}(b)
-    xx = x isa Vector{Float64} ? x : similar(bb)
-    check(ccall((:smlu_solve, libsmlu), Int32, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}),
-                F.handle, bb, xx), F.handle)
+    @boundscheck size(x, 1) == F.n || throw(DimensionMismatch("`x` does not have same size as F: length(x)=$(length(x)), F.n=$(F.n)"))
+    @boundscheck size(b, 1) == F.n || throw(DimensionMismatch("`b` does not have same size as F: length(b)=$(length(b)), F.n=$(F.n)"))
+    bb = b isa Array{Tf} ? b : Array{Tf}(b)
+    xx = x isa Array{Tf} ? x : similar(bb)
+    if ndims(b) == 1
+        check(ccall((:smlu_solve, libsmlu), Int32, (Ptr{Cvoid}, Ptr{Tf}, Ptr{Tf}), F.handle, bb, xx), F.handle)
+    else                                       # several right-hand sides: one batched call
+        ld = (Tf === ComplexF64 ? 2 : 1) * F.n  # leading dimension in doubles
+        check(ccall((:smlu_solve_multi, libsmlu), Int32,
+                    (Ptr{Cvoid}, Int64, Ptr{Tf}, Int64, Ptr{Tf}, Int64),
+                    F.handle, size(b, 2), bb, ld, xx, ld), F.handle)
+    end
     xx === x || copyto!(x, xx)
     return x
 end
 
-lsolve!(F::ParallelSparseLU, x) = (check(ccall((:smlu_lsolve, libsmlu), Int32,
-    (Ptr{Cvoid}, Ptr{Float64}), F.handle, x), F.handle); nothing)                   # :349
-rsolve!(F::ParallelSparseLU, x) = (check(ccall((:smlu_rsolve, libsmlu), Int32,
-    (Ptr{Cvoid}, Ptr{Float64}), F.handle, x), F.handle); nothing)                   # :374
+function _trisolve!(name, F::ParallelSparseLU{Tf}, x::AbstractVector) where {Tf}
+    xx = x isa Vector{Tf} ? x : Vector{Tf}(x)
+    check(ccall(fnptr(name), Int32, (Ptr{Cvoid}, Ptr{Tf}), F.handle, xx), F.handle)
+    xx === x || copyto!(x, xx)
+    return nothing
+end
+lsolve!(F::ParallelSparseLU, x) = _trisolve!(:smlu_lsolve, F, x)                   # :349
+rsolve!(F::ParallelSparseLU, x) = _trisolve!(:smlu_rsolve, F, x)                   # :374
+
+# Optional parity mode: the reference's own dense-chunk layout (:101-243) on the GPU, refilled
+# after each lu! (:265-276); ldiv! through it runs lsolve!/rsolve! chunk by chunk (:349-392).
+chunked_setup!(F::ParallelSparseLU) = check(ccall((:smlu_chunked_setup, libsmlu), Int32,
+    (Ptr{Cvoid}, Int64), F.handle, F.chunk_size), F.handle)
+function chunked_ldiv!(x::AbstractVector, F::ParallelSparseLU{Tf}, b::AbstractVector) where {Tf}
+    length(x) == length(b) == F.n || throw(DimensionMismatch("x, b and F sizes differ"))
+    bb = Vector{Tf}(b); xx = Vector{Tf}(undef, F.n)
+    check(ccall((:smlu_chunked_ldiv, libsmlu), Int32, (Ptr{Cvoid}, Ptr{Tf}, Ptr{Tf}),
+                F.handle, bb, xx), F.handle)
+    copyto!(x, xx)
+end
 
 function Base.getproperty(F::ParallelSparseLU, s::Symbol)                           # :45-52
     s in (:L, :U, :p, :q, :Rs) || return getfield(F, s)
-    n = getfield(F, :n); nl = Ref{Int64}(0); nu = Ref{Int64}(0)
     h = getfield(F, :handle)
+    n = Int64(getfield(F, :n)); nl = Ref{Int64}(0); nu = Ref{Int64}(0)
+    # a ComplexF64 handle exports the factors of its real-equivalent 2n x 2n matrix (smlu.h)
+    ccall((:smlu_stat, libsmlu), Float64, (Ptr{Cvoid}, Cstring), h, "complex") == 1 && (n *= 2)
     check(ccall((:smlu_get_sizes, libsmlu), Int32, (Ptr{Cvoid}, Ptr{Int64}, Ref{Int64}, Ref{Int64}),
                 h, C_NULL, nl, nu), h)
     Lp = Vector{Int64}(undef, n + 1); Li = Vector{Int64}(undef, nl[]); Lx = Vector{Float64}(undef, nl[])

@@ -68,6 +68,10 @@ SIGNATURES = {
     "smlu_solve_multi": (i32, [vp, i64, vp, i64, vp, i64]),
     "smlu_solve_multi_device": (i32, [vp, i64, vp, i64, vp, i64]),
     "smlu_create_i32": (i32, [i64, vp, vp, vp, ctypes.POINTER(SmluOpts), ctypes.POINTER(vp)]),
+    "smlu_create_z": (i32, [i64, vp, vp, vp, ctypes.POINTER(SmluOpts), ctypes.POINTER(vp)]),
+    "smlu_refactor_z": (i32, [vp, vp]),
+    "smlu_refactor_z_device": (i32, [vp, vp]),
+    "smlu_refactor_csc_z": (i32, [vp, i64, vp, vp, vp]),
     "smlu_lsolve": (i32, [vp, vp]),
     "smlu_rsolve": (i32, [vp, vp]),
     "smlu_chunked_setup": (i32, [vp, i64]),

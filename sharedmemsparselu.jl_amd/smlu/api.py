@@ -11,6 +11,11 @@ cleanup_ParallelSparseLU!(F)        cleanup_ParallelSparseLU_(F)  :31 (exported,
 DimensionMismatch                   DimensionMismatch             :288-290
 SingularException (UMFPACK)         SingularException             :74 / :247
 
+Tf = ComplexF64 (the reference is generic in Tf, :43, :64, :286): pass a complex matrix and
+complex vectors to the same functions; the library factors the real-equivalent 2n x 2n matrix
+(``smlu_create_z``, include/smlu.h), so F.L / F.U / F.p / F.q / F.Rs of a complex F are those
+of that real-equivalent matrix (2n rows).
+
 All numerics run on the MI355X through libsmlu.so; nothing here computes factors or solves.
 """
 from __future__ import annotations
@@ -40,9 +45,11 @@ class SmluError(RuntimeError):
 
 
 def _csc(A):
+    dt = np.complex128 if (np.iscomplexobj(A.data) if sp.issparse(A) else np.iscomplexobj(A)) \
+        else np.float64
     if not sp.issparse(A):
-        A = sp.csc_matrix(np.asarray(A, dtype=np.float64))
-    A = sp.csc_matrix(A, dtype=np.float64)
+        A = sp.csc_matrix(np.asarray(A, dtype=dt))
+    A = sp.csc_matrix(A, dtype=dt)
     if not A.has_sorted_indices:
         A = A.sorted_indices()
     A.sum_duplicates()
@@ -94,12 +101,19 @@ class ParallelSparseLU:
         self._opts = C.default_opts(**kw)
         self.m, self.n = m, n
         self.chunk_size = chunk_size
+        self.is_complex = A.dtype == np.complex128
+        self._dt = A.dtype
         self._colptr = np.ascontiguousarray(A.indptr, dtype=np.int64)
         self._rowval = np.ascontiguousarray(A.indices, dtype=np.int64)
-        vals = np.ascontiguousarray(A.data, dtype=np.float64)
+        vals = np.ascontiguousarray(A.data, dtype=self._dt)
         h = ctypes.c_void_p()
         L = C.lib()
-        if p is not None or q is not None:
+        if self.is_complex:
+            if p is not None or q is not None or int32_indices:
+                raise ValueError("complex matrices take neither a given (p, q) nor Int32 indices")
+            rc = L.smlu_create_z(n, C.ptr(self._colptr), C.ptr(self._rowval), C.ptr(vals),
+                                 ctypes.byref(self._opts), ctypes.byref(h))
+        elif p is not None or q is not None:
             pp = np.ascontiguousarray(p, dtype=np.int64)
             qq = np.ascontiguousarray(q, dtype=np.int64)
             rs = None if Rs is None else np.ascontiguousarray(Rs, dtype=np.float64)
@@ -128,7 +142,7 @@ class ParallelSparseLU:
     def _download(self):
         if self._factors is None:
             L = C.lib()
-            n = self.n
+            n = 2 * self.n if self.is_complex else self.n   # complex: the real-equivalent matrix
             nl, nu = ctypes.c_int64(), ctypes.c_int64()
             _check(L.smlu_get_sizes(self._h, None, ctypes.byref(nl), ctypes.byref(nu)), self._h)
             Lp = np.empty(n + 1, np.int64); Li = np.empty(nl.value, np.int64); Lx = np.empty(nl.value)
@@ -165,9 +179,11 @@ class ParallelSparseLU:
 
     # ---- device-resident entry points (values / vectors already in HBM) ----
     def refactor_device(self, d_values):
-        """lu! with values already on the device (torch tensor or raw pointer int)."""
+        """lu! with values already on the device (torch tensor or raw pointer int; complex
+        handles take interleaved complex values, e.g. a complex128 tensor)."""
         ptr = d_values.data_ptr() if hasattr(d_values, "data_ptr") else int(d_values)
-        rc = _check(C.lib().smlu_refactor_device(self._h, ctypes.c_void_p(ptr)), self._h)
+        fn = C.lib().smlu_refactor_z_device if self.is_complex else C.lib().smlu_refactor_device
+        rc = _check(fn(self._h, ctypes.c_void_p(ptr)), self._h)
         self._factors = None
         if rc == C.SMLU_SINGULAR:
             raise SingularException(C.lib().smlu_last_error_col(self._h))
@@ -186,8 +202,9 @@ class ParallelSparseLU:
         nrhs, n = d_B.shape
         if n != self.n or tuple(d_X.shape) != (nrhs, n):
             raise DimensionMismatch(f"B has shape {tuple(d_B.shape)}, X has shape {tuple(d_X.shape)}, n={self.n}")
-        return _check(C.lib().smlu_solve_multi_device(self._h, nrhs, ctypes.c_void_p(d_B.data_ptr()), n,
-                                                      ctypes.c_void_p(d_X.data_ptr()), n), self._h)
+        ld = 2 * n if self.is_complex else n     # leading dimension in doubles
+        return _check(C.lib().smlu_solve_multi_device(self._h, nrhs, ctypes.c_void_p(d_B.data_ptr()), ld,
+                                                      ctypes.c_void_p(d_X.data_ptr()), ld), self._h)
 
     def close(self):
         h = getattr(self, "_h", None)
@@ -211,16 +228,19 @@ def lu_(F: ParallelSparseLU, A):
     A = _csc(A)
     if A.shape != (F.m, F.n):
         raise DimensionMismatch(f"A has size {A.shape}, F has size {(F.m, F.n)}")
-    vals = np.ascontiguousarray(A.data, dtype=np.float64)
+    if A.dtype == np.complex128 and not F.is_complex:
+        raise TypeError("complex values for a real factorization (create it from a complex matrix)")
+    vals = np.ascontiguousarray(A.data, dtype=F._dt)   # real values into a complex F are promoted
     L = C.lib()
     same = (A.nnz == F._rowval.size and np.array_equal(A.indptr, F._colptr)
             and np.array_equal(A.indices, F._rowval))
     if same:
-        rc = L.smlu_refactor(F._h, C.ptr(vals))
+        rc = (L.smlu_refactor_z if F.is_complex else L.smlu_refactor)(F._h, C.ptr(vals))
     else:
         F._colptr = np.ascontiguousarray(A.indptr, dtype=np.int64)
         F._rowval = np.ascontiguousarray(A.indices, dtype=np.int64)
-        rc = L.smlu_refactor_csc(F._h, F.n, C.ptr(F._colptr), C.ptr(F._rowval), C.ptr(vals))
+        fn = L.smlu_refactor_csc_z if F.is_complex else L.smlu_refactor_csc
+        rc = fn(F._h, F.n, C.ptr(F._colptr), C.ptr(F._rowval), C.ptr(vals))
     F._factors = None
     _check(rc, F._h)
     if rc == C.SMLU_SINGULAR:
@@ -236,21 +256,25 @@ def ldiv_(x, F: ParallelSparseLU, b):
         raise DimensionMismatch(f"`x` does not have same size as F: length(x)={len(x)}, F.n={F.n}")
     if len(b) != F.n:
         raise DimensionMismatch(f"`b` does not have same size as F: length(b)={len(b)}, F.n={F.n}")
+    if not F.is_complex and (np.iscomplexobj(b) or np.iscomplexobj(x)):
+        raise TypeError("complex vectors need a factorization of a complex matrix")
     if np.ndim(b) == 2 or np.ndim(x) == 2:
         # several right-hand sides (columns), SURVEY §8f-4: one C-ABI call, column-major buffers
         if np.shape(x) != np.shape(b):
             raise DimensionMismatch(f"`x` has size {np.shape(x)}, `b` has size {np.shape(b)}")
         nrhs = np.shape(b)[1]
-        bb = np.asfortranarray(b, dtype=np.float64)
-        xx = x if (isinstance(x, np.ndarray) and x.dtype == np.float64 and x.flags.f_contiguous) \
-            else np.empty((F.n, nrhs), order="F")
-        _check(C.lib().smlu_solve_multi(F._h, nrhs, C.ptr(bb), F.n, C.ptr(xx), F.n), F._h)
+        dt = F._dt
+        bb = np.asfortranarray(b, dtype=dt)
+        xx = x if (isinstance(x, np.ndarray) and x.dtype == dt and x.flags.f_contiguous) \
+            else np.empty((F.n, nrhs), dtype=dt, order="F")
+        ld = 2 * F.n if F.is_complex else F.n   # leading dimension in doubles
+        _check(C.lib().smlu_solve_multi(F._h, nrhs, C.ptr(bb), ld, C.ptr(xx), ld), F._h)
         if xx is not x:
             x[:, :] = xx
         return x
-    bb = np.ascontiguousarray(b, dtype=np.float64)
-    xx = x if (isinstance(x, np.ndarray) and x.dtype == np.float64 and x.flags.c_contiguous) \
-        else np.empty(F.n)
+    bb = np.ascontiguousarray(b, dtype=F._dt)
+    xx = x if (isinstance(x, np.ndarray) and x.dtype == F._dt and x.flags.c_contiguous) \
+        else np.empty(F.n, dtype=F._dt)
     _check(C.lib().smlu_solve(F._h, C.ptr(bb), C.ptr(xx)), F._h)
     if xx is not x:
         x[:] = xx
@@ -260,8 +284,8 @@ def ldiv_(x, F: ParallelSparseLU, b):
 def _tri(F, x, which):
     if len(x) != F.n:
         raise DimensionMismatch(f"`x` does not have same size as F: length(x)={len(x)}, F.n={F.n}")
-    xx = x if (isinstance(x, np.ndarray) and x.dtype == np.float64 and x.flags.c_contiguous) \
-        else np.ascontiguousarray(x, dtype=np.float64)
+    xx = x if (isinstance(x, np.ndarray) and x.dtype == F._dt and x.flags.c_contiguous) \
+        else np.ascontiguousarray(x, dtype=F._dt)
     fn = C.lib().smlu_lsolve if which == "L" else C.lib().smlu_rsolve
     _check(fn(F._h, C.ptr(xx)), F._h)
     if xx is not x:
@@ -291,8 +315,8 @@ def chunked_ldiv_(x, F: ParallelSparseLU, b):
     chunk on the GPU.  Same DimensionMismatch checks as ldiv_; x may be b."""
     if len(x) != F.n or len(b) != F.n:
         raise DimensionMismatch(f"x and b must have length F.n={F.n}: {len(x)}, {len(b)}")
-    bb = np.ascontiguousarray(b, dtype=np.float64)
-    xx = np.empty(F.n)
+    bb = np.ascontiguousarray(b, dtype=F._dt)
+    xx = np.empty(F.n, dtype=F._dt)
     _check(C.lib().smlu_chunked_ldiv(F._h, C.ptr(bb), C.ptr(xx)), F._h)
     x[:] = xx
     return x

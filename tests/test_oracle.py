@@ -182,3 +182,47 @@ def test_reference_suite_sparse(nel):
     F.ldiv(x, b)
     t = ctol(A2, TOL)
     assert isapprox(x, spla.spsolve(A2, b), t, t)
+
+
+def complex_fe(rng, nel, ngr=5):
+    """The reference's FE fixture (test/runtests.jl:12-21) with complex values on its pattern."""
+    A = O.test_matrix(rng, nel, ngr).tocsc()
+    A.sort_indices()
+    Z = A.astype(np.complex128)
+    Z.data = Z.data + 1j * (rng.random(A.nnz) - 0.5)
+    return Z
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_real_equivalent_embedding(seed):
+    """K (oracle.real_equivalent) acts on interleaved vectors exactly as A on complex ones."""
+    rng = np.random.default_rng(seed)
+    A = complex_fe(rng, 7)
+    n = A.shape[0]
+    K = O.real_equivalent(A)
+    assert K.shape == (2 * n, 2 * n) and K.nnz == 4 * A.nnz and K.has_sorted_indices
+    x = rng.random(n) + 1j * rng.random(n)
+    assert np.allclose(K @ x.view(np.float64), (A @ x).view(np.float64), rtol=0, atol=1e-14)
+
+
+@pytest.mark.parametrize("nel", [1, 4, 12])
+def test_oracle_complex_solve_vs_superlu(nel):
+    """The oracle's LU of K with a pairwise column order solves the complex system: pinned
+    against scipy's complex SuperLU at the reference's sparse tolerance (1e-12)."""
+    rng = np.random.default_rng(100 + nel)
+    A = complex_fe(rng, nel)
+    n = A.shape[0]
+    K = O.real_equivalent(A)
+    order = np.argsort(rng.random(n))            # any complex order, expanded to pairs
+    q = np.empty(2 * n, np.int64)
+    q[0::2], q[1::2] = 2 * order, 2 * order + 1
+    Rs = O.rowscale(K)
+    assert np.allclose(Rs[0::2], Rs[1::2], rtol=1e-15, atol=0)   # SUM scaling: |x| + |y| per entry
+    ref = O.OracleLU(K, q, q, Rs)
+    assert ref.status == 0
+    b = rng.random(n) + 1j * rng.random(n)
+    xr = np.empty(2 * n)
+    ref.ldiv(xr, b.view(np.float64).copy())
+    x = xr.view(np.complex128)
+    xs = spla.spsolve(A.tocsc(), b)
+    assert np.linalg.norm(x - xs) <= 1e-12 * max(np.linalg.norm(x), 1.0) * max(1.0, np.linalg.cond(A.toarray()) / 1e3)

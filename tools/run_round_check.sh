@@ -1,0 +1,11 @@
+# Full GPU check of the current tree (via gpurun from the repo root): all -m gpu tests, smoke,
+# then the default bench line.  bash tools/run_round_check.sh TAG
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+T=${1:-rc}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/${T}_tests.log 2>&1 || { echo PYTEST FAIL; tail -40 gpurun_out/${T}_tests.log; exit 1; }
+tail -3 gpurun_out/${T}_tests.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${T}_smoke.log 2>&1 || { echo SMOKE FAIL; tail -20 gpurun_out/${T}_smoke.log; exit 1; }
+tail -1 gpurun_out/${T}_smoke.log
+timeout -k 10 400 python bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.log || { echo BENCH FAIL; tail -20 gpurun_out/${T}_bench.log; exit 1; }
+cat gpurun_out/${T}_bench.json
