@@ -96,6 +96,9 @@ const char* kKindName[K_NKIND] = {"memset", "memset", "assemble", "assemble", "s
                                   "trsm", "trsm", "gemm", "solve", "solve", "solve", "solve",
                                   "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "sync", "sync", "trsm", "solve", "solve"};
 constexpr int kSolveBigNs = 256;  // fronts with more pivots use the multi-workgroup solve
+// ... and so do fronts whose L panel (M x ns entries) exceeds this: one workgroup streams a
+// tall panel at single-CU bandwidth (a 10^4-row front with 200 pivots took ~350 us per sweep)
+constexpr int64_t kSolveBigWork = 1 << 16;
 
 struct Launch {
   int kind = 0;
@@ -348,7 +351,7 @@ struct smlu_handle {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   std::vector<int> ev_kind;
   int32_t* hinfo = nullptr;  // pinned
-  hipGraphExec_t sol_exec = nullptr;
+  std::vector<std::pair<int, hipGraphExec_t>> sol_execs;   // captured solve sweeps, keyed by mode/rhs count
   std::vector<hipGraphExec_t> fac_execs;   // one captured graph per factor segment
   int fac_exec_profile = -1;
   std::vector<std::pair<size_t, size_t>> seg_events;   // profile events of each captured segment
@@ -436,8 +439,9 @@ struct smlu_handle {
     for (auto& g : fac_execs)
       if (g) (void)hipGraphExecDestroy(g);
     fac_execs.clear();
-    if (sol_exec) (void)hipGraphExecDestroy(sol_exec);
-    sol_exec = nullptr;
+    for (auto& g : sol_execs)
+      if (g.second) (void)hipGraphExecDestroy(g.second);
+    sol_execs.clear();
     fac_exec_profile = -1;
   }
   void release_all() {
@@ -1633,11 +1637,17 @@ static int build_schedule(smlu_handle* h) {
     add_comm(seq, seg, cm, std::move(op));
   };
   auto holder = [&](int64_t c) { return P.dist(c) ? P.blk_owner(c, P.npblk(c) - 1) : P.owner[c]; };
+  static const int64_t big_work = [] {
+    const char* e = std::getenv("SMLU_SOLVE_BIGWORK");   // dev knob (sweeps)
+    return e ? std::atoll(e) : kSolveBigWork;
+  }();
   for (int l = 0; l < P.nlevels; ++l) {
     std::vector<int64_t> small, bigs;
     for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {
       int64_t s = LS[k];
-      (h->hsn[s].ns > kSolveBigNs ? bigs : small).push_back(s);
+      const SNode& r = h->hsn[s];
+      const bool big = r.ns > kSolveBigNs || (int64_t)r.ns * ((int64_t)r.ns + r.nu) > big_work;
+      (big ? bigs : small).push_back(s);
     }
     std::vector<Launch> bl;
     if (!small.empty()) {
@@ -2511,12 +2521,48 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
     }
     return (int)SMLU_OK;
   };
-  if (mode != 2) {
-    int rc = run_seq(h->fwd, h->fwd_seg, h->fwd_comm);
-    if (rc != SMLU_OK) return rc;
-  }
-  if (mode != 1) {
-    int rc = run_seq(h->bwd, h->bwd_seg, h->bwd_comm);
+  auto sweeps = [&]() {
+    if (mode != 2) {
+      int rc = run_seq(h->fwd, h->fwd_seg, h->fwd_comm);
+      if (rc != SMLU_OK) return rc;
+    }
+    if (mode != 1) {
+      int rc = run_seq(h->bwd, h->bwd_seg, h->bwd_comm);
+      if (rc != SMLU_OK) return rc;
+    }
+    return (int)SMLU_OK;
+  };
+  // One GPU: the forward and backward sweeps (~1,400 launches at 128^3, fixed pointers: the
+  // handle's wrk / vbuf) are captured once per (mode, rhs count) into a hipGraph and replayed;
+  // only the permutation kernels see the caller's b and x.
+  static const bool nograph = std::getenv("SMLU_NO_GRAPH") != nullptr;
+  if (h->nranks == 1 && !nograph && !h->graph_failed) {
+    const int key = mode * 256 + rh.n;
+    hipGraphExec_t ex = nullptr;
+    for (auto& g : h->sol_execs)
+      if (g.first == key) ex = g.second;
+    if (!ex) {
+      hipGraph_t g = nullptr;
+      HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+      int rc = sweeps();
+      hipError_t ec = hipStreamEndCapture(st, &g);
+      if (rc == SMLU_OK && ec == hipSuccess && g) ec = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+      if (g) (void)hipGraphDestroy(g);
+      if (rc != SMLU_OK || ec != hipSuccess || !ex) {
+        (void)hipGetLastError();
+        h->graph_failed = true;
+        ex = nullptr;
+      } else {
+        h->sol_execs.push_back({key, ex});
+      }
+    }
+    if (ex) HIPCHK(hipGraphLaunch(ex, st));
+    else {
+      int rc = sweeps();
+      if (rc != SMLU_OK) return rc;
+    }
+  } else {
+    int rc = sweeps();
     if (rc != SMLU_OK) return rc;
   }
   if (mode == 0) HIPCHK(launch_perm_out(st, P.n, h->q.p, w, dx, nrhs, rh.ldx, ldx > 0 ? ldx : P.n));

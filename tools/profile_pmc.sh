@@ -6,6 +6,6 @@ N=${1:-128}
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 export SMLU_NO_GRAPH=1
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 500 rocprofv3 --pmc $c --kernel-include-regex "k_gemm" -d gpurun_out/pmc_${c}_$N -o pmc \
+  timeout -k 10 500 rocprofv3 --pmc $c --kernel-include-regex "k_gemm|Cijk" -d gpurun_out/pmc_${c}_$N -o pmc \
     --output-format csv -- python3 tools/pmc_factor.py $N > gpurun_out/pmc_${c}_$N.log 2>&1 || exit 1
 done

@@ -9,7 +9,7 @@ timeout -k 10 300 python bench.py > gpurun_out/p_bench.json 2> gpurun_out/p_benc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/p_kt -o kt --output-format csv -- python3 bench.py --no-cpu --steps 2 --warmup 1 > gpurun_out/p_kt.json 2> gpurun_out/p_kt.log || exit 1
 export SMLU_NO_GRAPH=1
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex "k_gemm" -d gpurun_out/pmc_${c}_$N -o pmc \
+  timeout -k 10 300 rocprofv3 --pmc $c --kernel-include-regex "k_gemm|Cijk" -d gpurun_out/pmc_${c}_$N -o pmc \
     --output-format csv -- python3 tools/pmc_factor.py $N > gpurun_out/pmc_${c}_$N.log 2>&1 || exit 1
 done
 # the same two counters over every kernel of the factorization: whole-refactor HBM bytes
