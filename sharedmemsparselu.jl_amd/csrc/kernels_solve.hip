@@ -252,6 +252,121 @@ __global__ __launch_bounds__(256) void k_bwd_front(const int32_t* __restrict__ l
              [&](int r, int64_t i, double val) { x[r * rh.ldx + s.first + i] = val; });
 }
 
+// Tiny fronts (M <= 64: the leaves of the assembly tree, 257k fronts of M = 7 at 128^3): one
+// wave per front, four fronts per workgroup, lane i owns row i of the front -- no workgroup
+// barriers, the factor rows are loaded once into registers and applied to every right-hand
+// side.  Same operations in the same order as k_fwd_front / k_bwd_front (bitwise identical):
+// forward, the pivot rows run the unit-lower chain and the update rows accumulate
+// sum_j L[i,j] x_j then subtract it; backward, x_s - U12 x[R] then the upper chain.
+template <int NR>
+__global__ __launch_bounds__(256) void k_fwd_tiny(const int32_t* __restrict__ list, int cnt,
+                                                  const SNode* __restrict__ sn, const int32_t* __restrict__ chlist,
+                                                  const int32_t* __restrict__ relmap,
+                                                  const int32_t* __restrict__ rowperm,
+                                                  const double* __restrict__ store, double* __restrict__ x,
+                                                  double* __restrict__ vbuf, Rhs rh) {
+  __shared__ double sv[4][64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t f = (int64_t)blockIdx.x * 4 + wv;
+  if (f >= cnt) return;   // the whole wave: no workgroup barriers below
+  const SNode s = sn[list[f]];
+  const int ns = s.ns, M = ns + s.nu;
+  const int nr = NR == 1 ? 1 : rh.n;
+  const double* Lp = store + s.Loff;
+  double l[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) l[j] = (lane < M && j < ns) ? Lp[(int64_t)j * M + lane] : 0.0;
+  const int pr = lane < ns ? rowperm[s.first + lane] : lane;
+  for (int r = 0; r < nr; ++r) {
+    double* xr = x + r * rh.ldx;
+    double* vr = vbuf + r * rh.ldv;
+    sv[wv][lane] = lane < ns ? xr[s.first + lane] : 0.0;
+    wave_lds_sync();
+    for (int c = s.chbeg; c < s.chend; ++c) {   // parent += child, children in order
+      const SNode ch = sn[chlist[c]];
+      if (lane < ch.nu) {
+        const int t = relmap[ch.rowptr + lane];
+        sv[wv][t] = sv[wv][t] + vr[ch.voff + ch.ns + lane];
+      }
+      wave_lds_sync();
+    }
+    double val = lane < M ? sv[wv][pr] : 0.0;   // pivot rows in the front's pivot order
+    wave_lds_sync();                            // every lane read before the next rhs overwrites
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      if (j < ns) {
+        const double xj = readlane_f64(val, j);
+        if (lane > j && lane < ns) val = fma(-l[j], xj, val);
+        else if (lane >= ns) acc = fma(l[j], xj, acc);
+      }
+    }
+    if (lane < ns) {
+      xr[s.first + lane] = val;
+      vr[s.voff + lane] = val;
+    } else if (lane < M) {
+      vr[s.voff + lane] = val - acc;
+    }
+  }
+}
+
+template <int NR>
+__global__ __launch_bounds__(256) void k_bwd_tiny(const int32_t* __restrict__ list, int cnt,
+                                                  const SNode* __restrict__ sn, const int32_t* __restrict__ rows,
+                                                  const double* __restrict__ store, double* __restrict__ x,
+                                                  double* __restrict__ vbuf, Rhs rh) {
+  __shared__ double sv[4][NR][64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t f = (int64_t)blockIdx.x * 4 + wv;
+  if (f >= cnt) return;
+  const SNode s = sn[list[f]];
+  const int ns = s.ns, nu = s.nu;
+  const int64_t M = (int64_t)ns + nu;
+  const int nr = NR == 1 ? 1 : rh.n;
+  {   // x_s - U12 x[R]: U12 row `lane` in registers, x[R_j] broadcast from lane j
+    const double* U12 = store + s.Uoff;
+    double u[64];
+#pragma unroll
+    for (int j = 0; j < 64; ++j) u[j] = (lane < ns && j < nu) ? U12[(int64_t)j * ns + lane] : 0.0;
+    const int32_t rj = lane < nu ? rows[s.rowptr + lane] : 0;
+    for (int r = 0; r < nr; ++r) {
+      const double* xr = x + r * rh.ldx;
+      const double xR = lane < nu ? xr[rj] : 0.0;
+      const double o = lane < ns ? xr[s.first + lane] : 0.0;
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < 64; ++j) {
+        if (j < nu) {
+          const double xj = readlane_f64(xR, j);
+          acc = fma(u[j], xj, acc);
+        }
+      }
+      sv[wv][r][lane] = o - acc;
+    }
+  }
+  wave_lds_sync();
+  const double* Lp = store + s.Loff;   // U11 in the upper triangle of the L panel
+  double l[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) l[j] = (lane < ns && j < ns) ? Lp[(int64_t)j * M + lane] : 0.0;
+  const double dinv = lane < ns ? recip(Lp[(int64_t)lane * M + lane]) : 1.0;
+  for (int r = 0; r < nr; ++r) {
+    double val = lane < ns ? sv[wv][r][lane] : 0.0;
+#pragma unroll
+    for (int j = 63; j >= 0; --j) {
+      if (j < ns) {
+        if (lane == j) val = val * dinv;
+        const double xj = readlane_f64(val, j);
+        if (lane < j) val = fma(-l[j], xj, val);
+      }
+    }
+    if (lane < ns) {
+      x[r * rh.ldx + s.first + lane] = val;
+      vbuf[r * rh.ldv + s.voff + lane] = val;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Solves for large fronts (ns > 256): the diagonal block sweep is split over workgroups.
 // k_fwd_gather: front vector = own rows + children's update vectors, row permutation.
@@ -538,6 +653,26 @@ hipError_t launch_bwd(hipStream_t st, int cnt, const int32_t* list, const SNode*
   else if (rh.n <= 4) k_bwd_front<4><<<cnt, 256, 0, st>>>(list, sn, rows, store, x, vbuf, rh);
   else if (rh.n <= 8) k_bwd_front<8><<<cnt, 256, 0, st>>>(list, sn, rows, store, x, vbuf, rh);
   else k_bwd_front<16><<<cnt, 256, 0, st>>>(list, sn, rows, store, x, vbuf, rh);
+  return hipGetLastError();
+}
+hipError_t launch_fwd_tiny(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
+                           const int32_t* chlist, const int32_t* relmap, const int32_t* rowperm,
+                           const double* store, double* x, double* vbuf, Rhs rh) {
+  if (cnt <= 0) return hipSuccess;
+  if (rh.n < 1 || rh.n > kMaxRhs) return hipErrorInvalidValue;
+  const unsigned g = nblk(cnt, 4);
+  if (rh.n == 1) k_fwd_tiny<1><<<g, 256, 0, st>>>(list, cnt, sn, chlist, relmap, rowperm, store, x, vbuf, rh);
+  else k_fwd_tiny<kMaxRhs><<<g, 256, 0, st>>>(list, cnt, sn, chlist, relmap, rowperm, store, x, vbuf, rh);
+  return hipGetLastError();
+}
+hipError_t launch_bwd_tiny(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
+                           const int32_t* rows, const double* store, double* x, double* vbuf, Rhs rh) {
+  if (cnt <= 0) return hipSuccess;
+  if (rh.n < 1 || rh.n > kMaxRhs) return hipErrorInvalidValue;
+  const unsigned g = nblk(cnt, 4);
+  if (rh.n == 1) k_bwd_tiny<1><<<g, 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf, rh);
+  else if (rh.n <= 4) k_bwd_tiny<4><<<g, 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf, rh);
+  else k_bwd_tiny<kMaxRhs><<<g, 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf, rh);
   return hipGetLastError();
 }
 hipError_t launch_fwd_gather(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,

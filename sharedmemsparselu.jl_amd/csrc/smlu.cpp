@@ -49,6 +49,10 @@ hipError_t launch_trsm_u(hipStream_t, int64_t, const FrontTile*, int, int, int, 
 hipError_t launch_gemm(hipStream_t, int64_t, const GemmTask*, int, int, int64_t);
 hipError_t launch_gemm_g(hipStream_t, int64_t, const GemmTask*, int, int, int64_t, int32_t*, double*, double);
 hipError_t launch_tri_inv(hipStream_t, int, int, const int32_t*, const SNode*, double*, double*, double*);
+hipError_t launch_fwd_tiny(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
+                           const int32_t*, const double*, double*, double*, Rhs);
+hipError_t launch_bwd_tiny(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*, double*,
+                           double*, Rhs);
 hipError_t launch_fwd_gather(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                              const int32_t*, double*, double*, Rhs);
 hipError_t launch_tri_block(hipStream_t, bool, int64_t, const FrontTile*, int, int, const SNode*,
@@ -90,15 +94,17 @@ thread_local std::string g_last_error;
 enum Kind : int {
   K_MEMSET_STORE, K_MEMSET_SCRATCH, K_SCATTER, K_EXTADD, K_FRONT_LDS, K_PANEL, K_TRSMU, K_TRSML,
   K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_GEMM22, K_LASWP, K_STEPTRSM, K_GEMMU,
-  K_GEMMO, K_FORK, K_JOIN, K_TRIINV, K_BWDU12C, K_VCOPY, K_NKIND
+  K_GEMMO, K_FORK, K_JOIN, K_TRIINV, K_BWDU12C, K_VCOPY, K_FWDT, K_BWDT, K_NKIND
 };
 const char* kKindName[K_NKIND] = {"memset", "memset", "assemble", "assemble", "small", "panel",
                                   "trsm", "trsm", "gemm", "solve", "solve", "solve", "solve",
-                                  "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "sync", "sync", "trsm", "solve", "solve"};
+                                  "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "sync", "sync", "trsm", "solve", "solve",
+                                  "solve", "solve"};
 constexpr int kSolveBigNs = 256;  // fronts with more pivots use the multi-workgroup solve
 // ... and so do fronts whose L panel (M x ns entries) exceeds this: one workgroup streams a
 // tall panel at single-CU bandwidth (a 10^4-row front with 200 pivots took ~350 us per sweep)
 constexpr int64_t kSolveBigWork = 1 << 16;
+constexpr int kSolveTinyM = 64;   // fronts with M <= 64 rows: one wave each (k_fwd_tiny / k_bwd_tiny)
 
 struct Launch {
   int kind = 0;
@@ -1637,19 +1643,30 @@ static int build_schedule(smlu_handle* h) {
     add_comm(seq, seg, cm, std::move(op));
   };
   auto holder = [&](int64_t c) { return P.dist(c) ? P.blk_owner(c, P.npblk(c) - 1) : P.owner[c]; };
+  static const bool no_tiny = std::getenv("SMLU_NO_TINY_SOLVE") != nullptr;   // dev knob
   static const int64_t big_work = [] {
     const char* e = std::getenv("SMLU_SOLVE_BIGWORK");   // dev knob (sweeps)
     return e ? std::atoll(e) : kSolveBigWork;
   }();
   for (int l = 0; l < P.nlevels; ++l) {
-    std::vector<int64_t> small, bigs;
+    std::vector<int64_t> tiny, small, bigs;
     for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {
       int64_t s = LS[k];
       const SNode& r = h->hsn[s];
       const bool big = r.ns > kSolveBigNs || (int64_t)r.ns * ((int64_t)r.ns + r.nu) > big_work;
-      (big ? bigs : small).push_back(s);
+      (big ? bigs : (int64_t)r.ns + r.nu <= kSolveTinyM && !no_tiny ? tiny : small).push_back(s);
     }
     std::vector<Launch> bl;
+    if (!tiny.empty()) {   // one wave per front
+      Launch L;
+      L.kind = K_FWDT;
+      L.off = (int64_t)ilist.size();
+      for (auto s : tiny) ilist.push_back((int32_t)s);
+      L.cnt = (int64_t)tiny.size();
+      h->fwd.push_back(L);
+      L.kind = K_BWDT;
+      bl.push_back(L);
+    }
     if (!small.empty()) {
       Launch L;
       L.kind = K_FWD;
@@ -2462,6 +2479,11 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, d
                         h->rowperm.p, h->store.p, w, v, rh);
     case K_BWD:
       return launch_bwd(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->rows.p, h->store.p, w, v, rh);
+    case K_FWDT:
+      return launch_fwd_tiny(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->chlist.p, h->relmap.p, h->rowperm.p,
+                             h->store.p, w, v, rh);
+    case K_BWDT:
+      return launch_bwd_tiny(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->rows.p, h->store.p, w, v, rh);
     case K_FWDG:
       return launch_fwd_gather(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->chlist.p, h->relmap.p,
                                h->rowperm.p, w, v, rh);
