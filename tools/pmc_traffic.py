@@ -19,13 +19,22 @@ out_dir = sys.argv[2]
 base = "gpurun_out"
 
 
+def short(name):
+    """rocBLAS/Tensile kernel names are several hundred characters: keep the macro tile and WGM."""
+    if name.startswith("Cijk_"):
+        mt = re.search(r"_MT(\w+?)_", name)
+        wg = re.search(r"_WGM(\d+)", name)
+        return f"rocblas dgemm MT{mt.group(1) if mt else '?'} WGM{wg.group(1) if wg else '?'}"
+    return name
+
+
 def load(counter):
     """Per-kernel totals of the Schur-update GEMMs (the <false> instantiations; the <true> ones
     are the GEMM-form triangular solves, accounted as "trsm")."""
     path = os.path.join(base, f"pmc_{counter}_{N}", "pmc_counter_collection.csv")
     per = {}
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0]
+        name = short(r["Kernel_Name"].split("(")[0])
         if "<true>" in name:
             continue
         d = per.setdefault(name, [0, 0.0])
@@ -65,7 +74,7 @@ if os.path.exists(os.path.join(base, f"pmcall_FETCH_SIZE_{N}", "pmc_counter_coll
         per = {}
         path = os.path.join(base, f"pmcall_{counter}_{N}", "pmc_counter_collection.csv")
         for r in csv.DictReader(open(path)):
-            name = r["Kernel_Name"].split("(")[0]
+            name = short(r["Kernel_Name"].split("(")[0])
             per[name] = per.get(name, 0.0) + float(r["Counter_Value"])
         return per
     fa, wa = load_all("FETCH_SIZE"), load_all("WRITE_SIZE")
