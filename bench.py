@@ -114,6 +114,25 @@ def cpu_baseline(N_head, upd_head, nnz_head, ordering, grid_hint, samples=(24, 3
     return res
 
 
+def ordering_compare(N):
+    """nnz(L+U) and upd = sum_k |L_k||U_k| of the native orderings on the headline config (C3) and
+    on C2 (2D 512^2): graph nested dissection (the default) against SMLU_ORDER_AMD, the
+    minimum-degree ordering of UMFPACK's symmetric strategy.  Host symbolic
+    analysis only, outside the timed region."""
+    import smlu
+    from smlu import matrices as mats
+    out = {}
+    for name, A in ((f"c3_poisson3d_{N}", mats.poisson3d(N)), ("c2_poisson2d_512", mats.poisson2d(512))):
+        row = {}
+        for o in ("nd", "amd"):
+            t0 = time.perf_counter()
+            P = smlu.Plan(A, ordering=o)
+            row[o] = {"nnzLU": P.stat("nnzLU"), "upd": P.stat("upd"),
+                      "analysis_s": round(time.perf_counter() - t0, 2)}
+        out[name] = row
+    return out
+
+
 def kernel_source_sha():
     """Hash of the library sources: a committed PMC profile applies to this build only if its
     recorded hash matches (otherwise its traffic numbers are stale and are not reported)."""
@@ -349,6 +368,8 @@ def main():
             "create_s": t_create,
         }
         if not args.no_cpu and world == 1:
+            log("ordering comparison (host symbolic analysis) ...")
+            res["config"]["ordering_compare"] = ordering_compare(N)
             log("cpu baseline ...")
             res["cpu_baseline"] = cpu_baseline(N, upd, nnzLU, args.ordering, args.ordering == "geometric")
         print(json.dumps(res), flush=True)
