@@ -335,7 +335,7 @@ def main():
                        "dense_flops": dense_flops, "ordering": args.ordering,
                        "parallelism": (f"tree-partition{world} (proportional mapping, RCCL p2p)"
                                        if partitioned else f"replicas{world}" if world > 1 else "single")},
-            "roofline": {"bound": "mfma", "kernel": "k_gemm128_mfma + k_gemm (fp64 Schur-complement updates)",
+            "roofline": {"bound": "mfma", "kernel": "Schur-complement GEMM group: rocBLAS dgemm (large plain updates) + k_gemm128_mfma + k_gemm_k64 + k_gemm (fp64)",
                          "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic,
