@@ -1,6 +1,7 @@
 """CPU tests of the host symbolic analysis (no GPU): the plan's L pattern is exactly the
 structural fill of (Rs.*A)[q,q] computed independently by the oracle, for structurally
 symmetric inputs; a superset for unsymmetric ones; supernode/level invariants hold."""
+import os
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -133,3 +134,20 @@ def test_amd_fill_close_to_minimum_degree(make):
     nat = smlu.Plan(A, ordering="natural", relax=False)
     assert nnz_amd <= 1.15 * nnz_mmd, (nnz_amd, nnz_mmd)
     assert nnz_amd < 2 * nat.stat("nnzL") - n
+
+
+def test_bench_ordering_compare():
+    """bench.py's config.ordering_compare: ND and AMD statistics from the host analysis, the
+    numbers DESIGN.md §1 quotes (ND fills less than AMD on 3D grids)."""
+    import importlib
+    import sys as _sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in _sys.path:
+        _sys.path.insert(0, root)
+    bench = importlib.import_module("bench")
+    out = bench.ordering_compare(14)
+    c3, c2 = out["c3_poisson3d_14"], out["c2_poisson2d_512"]
+    for row in (c3, c2):
+        for o in ("nd", "amd"):
+            assert row[o]["nnzLU"] > 0 and row[o]["upd"] > 0
+    assert c3["nd"]["upd"] < c3["amd"]["upd"]
