@@ -252,12 +252,13 @@ __global__ __launch_bounds__(256) void k_bwd_front(const int32_t* __restrict__ l
              [&](int r, int64_t i, double val) { x[r * rh.ldx + s.first + i] = val; });
 }
 
-// Tiny fronts (M <= 64: the leaves of the assembly tree, 257k fronts of M = 7 at 128^3): one
-// wave per front, four fronts per workgroup, lane i owns row i of the front -- no workgroup
-// barriers, the factor rows are loaded once into registers and applied to every right-hand
-// side.  Same operations in the same order as k_fwd_front / k_bwd_front (bitwise identical):
-// forward, the pivot rows run the unit-lower chain and the update rows accumulate
-// sum_j L[i,j] x_j then subtract it; backward, x_s - U12 x[R] then the upper chain.
+// Tiny fronts (M <= 128 rows, ns <= 64 pivots: the leaves of the assembly tree -- 257k fronts of
+// M = 7 at 128^3 -- and most of the next four levels): one wave per front, four fronts per
+// workgroup, lane i owns rows i and i + 64 of the front -- no workgroup barriers, the factor rows
+// are loaded once into registers and applied to every right-hand side.  Same operations in the
+// same order as k_fwd_front / k_bwd_front (bitwise identical): forward, the pivot rows run the
+// unit-lower chain and the update rows accumulate sum_j L[i,j] x_j then subtract it; backward,
+// x_s - U12 x[R] (columns in order, 64 at a time) then the upper chain.
 template <int NR>
 __global__ __launch_bounds__(256) void k_fwd_tiny(const int32_t* __restrict__ list, int cnt,
                                                   const SNode* __restrict__ sn, const int32_t* __restrict__ chlist,
@@ -265,7 +266,9 @@ __global__ __launch_bounds__(256) void k_fwd_tiny(const int32_t* __restrict__ li
                                                   const int32_t* __restrict__ rowperm,
                                                   const double* __restrict__ store, double* __restrict__ x,
                                                   double* __restrict__ vbuf, Rhs rh) {
-  __shared__ double sv[4][64];
+  __shared__ double sv[4][128];
+  __shared__ double sx[4][NR][64];   // solved pivot values, for rows 64..127
+  __shared__ double s2[4][NR][64];   // gathered values of rows 64..127
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t f = (int64_t)blockIdx.x * 4 + wv;
   if (f >= cnt) return;   // the whole wave: no workgroup barriers below
@@ -273,40 +276,58 @@ __global__ __launch_bounds__(256) void k_fwd_tiny(const int32_t* __restrict__ li
   const int ns = s.ns, M = ns + s.nu;
   const int nr = NR == 1 ? 1 : rh.n;
   const double* Lp = store + s.Loff;
-  double l[64];
+  {
+    double l[64];
 #pragma unroll
-  for (int j = 0; j < 64; ++j) l[j] = (lane < M && j < ns) ? Lp[(int64_t)j * M + lane] : 0.0;
-  const int pr = lane < ns ? rowperm[s.first + lane] : lane;
-  for (int r = 0; r < nr; ++r) {
-    double* xr = x + r * rh.ldx;
-    double* vr = vbuf + r * rh.ldv;
-    sv[wv][lane] = lane < ns ? xr[s.first + lane] : 0.0;
-    wave_lds_sync();
-    for (int c = s.chbeg; c < s.chend; ++c) {   // parent += child, children in order
-      const SNode ch = sn[chlist[c]];
-      if (lane < ch.nu) {
-        const int t = relmap[ch.rowptr + lane];
-        sv[wv][t] = sv[wv][t] + vr[ch.voff + ch.ns + lane];
-      }
+    for (int j = 0; j < 64; ++j) l[j] = (lane < M && j < ns) ? Lp[(int64_t)j * M + lane] : 0.0;
+    const int pr = lane < ns ? rowperm[s.first + lane] : lane;
+    for (int r = 0; r < nr; ++r) {
+      double* xr = x + r * rh.ldx;
+      double* vr = vbuf + r * rh.ldv;
+      sv[wv][lane] = lane < ns ? xr[s.first + lane] : 0.0;
+      sv[wv][64 + lane] = 0.0;
       wave_lds_sync();
+      for (int c = s.chbeg; c < s.chend; ++c) {   // parent += child, children in order
+        const SNode ch = sn[chlist[c]];
+        for (int q = lane; q < ch.nu; q += 64) {   // a child's target rows are distinct
+          const int t = relmap[ch.rowptr + q];
+          sv[wv][t] = sv[wv][t] + vr[ch.voff + ch.ns + q];
+        }
+        wave_lds_sync();
+      }
+      double val = lane < M ? sv[wv][pr] : 0.0;   // pivot rows in the front's pivot order
+      if (M > 64) s2[wv][r][lane] = 64 + lane < M ? sv[wv][64 + lane] : 0.0;
+      wave_lds_sync();                            // every lane read before the next rhs overwrites
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < 64; ++j) {
+        if (j < ns) {
+          const double xj = readlane_f64(val, j);
+          if (lane > j && lane < ns) val = fma(-l[j], xj, val);
+          else if (lane >= ns) acc = fma(l[j], xj, acc);
+        }
+      }
+      if (lane < ns) {
+        xr[s.first + lane] = val;
+        vr[s.voff + lane] = val;
+        if (M > 64) sx[wv][r][lane] = val;
+      } else if (lane < M) {
+        vr[s.voff + lane] = val - acc;
+      }
     }
-    double val = lane < M ? sv[wv][pr] : 0.0;   // pivot rows in the front's pivot order
-    wave_lds_sync();                            // every lane read before the next rhs overwrites
+  }
+  if (M <= 64) return;
+  wave_lds_sync();
+  // rows 64..127 (update rows: ns <= 64): sum_j L[64+lane, j] x_j, then subtract
+  double l2[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) l2[j] = (64 + lane < M && j < ns) ? Lp[(int64_t)j * M + 64 + lane] : 0.0;
+  for (int r = 0; r < nr; ++r) {
     double acc = 0.0;
 #pragma unroll
-    for (int j = 0; j < 64; ++j) {
-      if (j < ns) {
-        const double xj = readlane_f64(val, j);
-        if (lane > j && lane < ns) val = fma(-l[j], xj, val);
-        else if (lane >= ns) acc = fma(l[j], xj, acc);
-      }
-    }
-    if (lane < ns) {
-      xr[s.first + lane] = val;
-      vr[s.voff + lane] = val;
-    } else if (lane < M) {
-      vr[s.voff + lane] = val - acc;
-    }
+    for (int j = 0; j < 64; ++j)
+      if (j < ns) acc = fma(l2[j], sx[wv][r][j], acc);
+    if (64 + lane < M) vbuf[r * rh.ldv + s.voff + 64 + lane] = s2[wv][r][lane] - acc;
   }
 }
 
@@ -323,28 +344,36 @@ __global__ __launch_bounds__(256) void k_bwd_tiny(const int32_t* __restrict__ li
   const int ns = s.ns, nu = s.nu;
   const int64_t M = (int64_t)ns + nu;
   const int nr = NR == 1 ? 1 : rh.n;
-  {   // x_s - U12 x[R]: U12 row `lane` in registers, x[R_j] broadcast from lane j
+  {   // x_s - U12 x[R]: U12 row `lane` in registers 64 columns at a time, x[R_j] from lane j
     const double* U12 = store + s.Uoff;
-    double u[64];
+#pragma unroll 1
+    for (int jb = 0; jb < nu; jb += 64) {
+      __builtin_amdgcn_sched_barrier(0);   // one 64-column slab live at a time
+      double u[64];
 #pragma unroll
-    for (int j = 0; j < 64; ++j) u[j] = (lane < ns && j < nu) ? U12[(int64_t)j * ns + lane] : 0.0;
-    const int32_t rj = lane < nu ? rows[s.rowptr + lane] : 0;
-    for (int r = 0; r < nr; ++r) {
-      const double* xr = x + r * rh.ldx;
-      const double xR = lane < nu ? xr[rj] : 0.0;
-      const double o = lane < ns ? xr[s.first + lane] : 0.0;
-      double acc = 0.0;
+      for (int j = 0; j < 64; ++j) u[j] = (lane < ns && jb + j < nu) ? U12[(int64_t)(jb + j) * ns + lane] : 0.0;
+      const int32_t rj = jb + lane < nu ? rows[s.rowptr + jb + lane] : 0;
+      for (int r = 0; r < nr; ++r) {
+        const double* xr = x + r * rh.ldx;
+        const double xR = jb + lane < nu ? xr[rj] : 0.0;
+        double acc = jb == 0 ? 0.0 : sv[wv][r][lane];
 #pragma unroll
-      for (int j = 0; j < 64; ++j) {
-        if (j < nu) {
-          const double xj = readlane_f64(xR, j);
-          acc = fma(u[j], xj, acc);
+        for (int j = 0; j < 64; ++j) {
+          if (jb + j < nu) {
+            const double xj = readlane_f64(xR, j);
+            acc = fma(u[j], xj, acc);
+          }
         }
+        sv[wv][r][lane] = acc;
       }
-      sv[wv][r][lane] = o - acc;
+    }
+    for (int r = 0; r < nr; ++r) {
+      const double o = lane < ns ? x[r * rh.ldx + s.first + lane] : 0.0;
+      sv[wv][r][lane] = o - (nu > 0 ? sv[wv][r][lane] : 0.0);
     }
   }
   wave_lds_sync();
+  __builtin_amdgcn_sched_barrier(0);   // the U12 slab dies before the U11 rows are loaded
   const double* Lp = store + s.Loff;   // U11 in the upper triangle of the L panel
   double l[64];
 #pragma unroll
@@ -670,8 +699,9 @@ hipError_t launch_bwd_tiny(hipStream_t st, int cnt, const int32_t* list, const S
   if (cnt <= 0) return hipSuccess;
   if (rh.n < 1 || rh.n > kMaxRhs) return hipErrorInvalidValue;
   const unsigned g = nblk(cnt, 4);
-  if (rh.n == 1) k_bwd_tiny<1><<<g, 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf, rh);
-  else if (rh.n <= 4) k_bwd_tiny<4><<<g, 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf, rh);
+  // the <4> instance also for a single rhs: <1> lets the compiler keep the U12 and U11 slabs live
+  // together (256 VGPRs)
+  if (rh.n <= 4) k_bwd_tiny<4><<<g, 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf, rh);
   else k_bwd_tiny<kMaxRhs><<<g, 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf, rh);
   return hipGetLastError();
 }

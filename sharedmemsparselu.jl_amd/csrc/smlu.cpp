@@ -104,7 +104,7 @@ constexpr int kSolveBigNs = 256;  // fronts with more pivots use the multi-workg
 // ... and so do fronts whose L panel (M x ns entries) exceeds this: one workgroup streams a
 // tall panel at single-CU bandwidth (a 10^4-row front with 200 pivots took ~350 us per sweep)
 constexpr int64_t kSolveBigWork = 1 << 16;
-constexpr int kSolveTinyM = 64;   // fronts with M <= 64 rows: one wave each (k_fwd_tiny / k_bwd_tiny)
+constexpr int kSolveTinyM = 128;   // fronts with M <= 128 rows and ns <= 64: one wave each (k_fwd_tiny / k_bwd_tiny)
 
 struct Launch {
   int kind = 0;
@@ -1654,7 +1654,8 @@ static int build_schedule(smlu_handle* h) {
       int64_t s = LS[k];
       const SNode& r = h->hsn[s];
       const bool big = r.ns > kSolveBigNs || (int64_t)r.ns * ((int64_t)r.ns + r.nu) > big_work;
-      (big ? bigs : (int64_t)r.ns + r.nu <= kSolveTinyM && !no_tiny ? tiny : small).push_back(s);
+      const bool tiny_front = (int64_t)r.ns + r.nu <= kSolveTinyM && r.ns <= 64 && !no_tiny;
+      (big ? bigs : tiny_front ? tiny : small).push_back(s);
     }
     std::vector<Launch> bl;
     if (!tiny.empty()) {   // one wave per front
