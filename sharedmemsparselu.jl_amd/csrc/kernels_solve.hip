@@ -642,6 +642,35 @@ __global__ __launch_bounds__(256) void k_residual(int64_t n, const int64_t* __re
   const double m = wave_max(fabs(ri));
   if ((threadIdx.x & 63) == 0 && m > 0.0) atomic_max_pos(nrm, m);
 }
+// Diagonal dominance of A's current values in HBM (the device twin of smlu.cpp's host
+// diagonally_dominant(), for smlu_refactor_device): thread i sums |column i| in CSC order and
+// |row i| over its entries in column order (Arow_ent), the host's summation order, so both take
+// the same decision; flags[0] / flags[1] are cleared when some column / row is not dominant.
+__global__ __launch_bounds__(256) void k_dominance(int64_t n, const int64_t* __restrict__ colptr,
+                                                   const int32_t* __restrict__ arow,
+                                                   const int64_t* __restrict__ rowptr,
+                                                   const int32_t* __restrict__ ent,
+                                                   const int32_t* __restrict__ acol,
+                                                   const double* __restrict__ a, int32_t* __restrict__ flags) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double d = 0.0, off = 0.0;
+  for (int64_t e = colptr[i]; e < colptr[i + 1]; ++e) {
+    const double v = fabs(a[e]);
+    if (arow[e] == i) d += v;
+    else off += v;
+  }
+  if (!(d > 0.0 && d >= off)) flags[0] = 0;
+  d = 0.0;
+  off = 0.0;
+  for (int64_t t = rowptr[i]; t < rowptr[i + 1]; ++t) {
+    const int32_t e = ent[t];
+    const double v = fabs(a[e]);
+    if (acol[e] == i) d += v;
+    else off += v;
+  }
+  if (!(d > 0.0 && d >= off)) flags[1] = 0;
+}
 __global__ void k_axpy1(int64_t n, const double* __restrict__ d, double* __restrict__ x) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] += d[i];
@@ -745,6 +774,17 @@ hipError_t launch_residual(hipStream_t st, int64_t n, const int64_t* rowptr, con
   if (n <= 0) return hipSuccess;
   k_residual<<<nblk(n, 256), 256, 0, st>>>(n, rowptr, ent, acol, a, x, b, r, nrm);
   return hipGetLastError();
+}
+hipError_t launch_dominance(hipStream_t st, int64_t n, const int64_t* colptr, const int32_t* arow,
+                            const int64_t* rowptr, const int32_t* ent, const int32_t* acol, const double* a,
+                            int32_t* dflags, int32_t* hflags) {
+  static const int32_t ones[2] = {1, 1};
+  hipError_t e = hipMemcpyAsync(dflags, ones, sizeof(ones), hipMemcpyHostToDevice, st);
+  if (e != hipSuccess) return e;
+  if (n > 0) k_dominance<<<nblk(n, 256), 256, 0, st>>>(n, colptr, arow, rowptr, ent, acol, a, dflags);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return hipMemcpyAsync(hflags, dflags, sizeof(ones), hipMemcpyDeviceToHost, st);
 }
 hipError_t launch_axpy1(hipStream_t st, int64_t n, const double* d, double* x) {
   if (n <= 0) return hipSuccess;

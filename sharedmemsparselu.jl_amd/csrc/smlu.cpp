@@ -66,6 +66,8 @@ hipError_t launch_bwd(hipStream_t, int, const int32_t*, const SNode*, const int3
 hipError_t launch_residual(hipStream_t, int64_t, const int64_t*, const int32_t*, const int32_t*,
                            const double*, const double*, const double*, double*, double*);
 hipError_t launch_axpy1(hipStream_t, int64_t, const double*, double*);
+hipError_t launch_dominance(hipStream_t, int64_t, const int64_t*, const int32_t*, const int64_t*, const int32_t*,
+                            const int32_t*, const double*, int32_t*, int32_t*);
 hipError_t launch_expand_z(hipStream_t, int64_t, const double*, const int64_t*, const int32_t*, double*);
 hipError_t launch_perm_in(hipStream_t, int64_t, const int64_t*, const double*, const double*, double*, int,
                           int64_t, int64_t);
@@ -270,11 +272,13 @@ int rccl_exchange(void* ctx, int32_t npeer, const int32_t* peer, void* const* sb
   auto* S = static_cast<RcclState*>(ctx);
   hipStream_t st = (hipStream_t)stream;
   if (R->GroupStart() != ncclSuccess) return 1;
-  for (int32_t i = 0; i < npeer; ++i) {
-    if (sbytes[i] > 0 && R->Send(sbuf[i], (size_t)sbytes[i], ncclUint8, peer[i], S->comm, st) != ncclSuccess) return 2;
-    if (rbytes[i] > 0 && R->Recv(rbuf[i], (size_t)rbytes[i], ncclUint8, peer[i], S->comm, st) != ncclSuccess) return 3;
+  int rc = 0;   // on a failed send/recv the group is still closed, so the communicator stays usable
+  for (int32_t i = 0; i < npeer && rc == 0; ++i) {
+    if (sbytes[i] > 0 && R->Send(sbuf[i], (size_t)sbytes[i], ncclUint8, peer[i], S->comm, st) != ncclSuccess) rc = 2;
+    else if (rbytes[i] > 0 && R->Recv(rbuf[i], (size_t)rbytes[i], ncclUint8, peer[i], S->comm, st) != ncclSuccess) rc = 3;
   }
-  return R->GroupEnd() == ncclSuccess ? 0 : 4;
+  const bool ended = R->GroupEnd() == ncclSuccess;
+  return rc != 0 ? rc : ended ? 0 : 4;
 }
 
 // broadcast inside a rank group as root -> member sends (the group is a subset of the ranks)
@@ -284,13 +288,15 @@ int rccl_bcast(void* ctx, void* buf, int64_t bytes, int32_t root, int32_t gsize,
   hipStream_t st = (hipStream_t)stream;
   if (bytes <= 0) return 0;
   if (R->GroupStart() != ncclSuccess) return 1;
+  int rc = 0;   // GroupEnd runs on the error path too
   if (S->rank == root) {
-    for (int32_t i = 0; i < gsize; ++i)
-      if (group[i] != root && R->Send(buf, (size_t)bytes, ncclUint8, group[i], S->comm, st) != ncclSuccess) return 2;
+    for (int32_t i = 0; i < gsize && rc == 0; ++i)
+      if (group[i] != root && R->Send(buf, (size_t)bytes, ncclUint8, group[i], S->comm, st) != ncclSuccess) rc = 2;
   } else if (R->Recv(buf, (size_t)bytes, ncclUint8, root, S->comm, st) != ncclSuccess) {
-    return 3;
+    rc = 3;
   }
-  return R->GroupEnd() == ncclSuccess ? 0 : 4;
+  const bool ended = R->GroupEnd() == ncclSuccess;
+  return rc != 0 ? rc : ended ? 0 : 4;
 }
 
 int rccl_allreduce_max(void* ctx, double* buf, int32_t count) {
@@ -331,7 +337,9 @@ struct smlu_handle {
   int64_t ch_T = 0, ch_size = 0, ch_version = -1;
   int64_t nfactor = 0;       // completed numeric factorizations
   DBuf<double> ref_b, ref_r, ref_d, ref_nrm;   // iterative refinement (allocated on first use)
-  DBuf<int32_t> Acol;                          // column of each A entry (residuals)
+  DBuf<int32_t> Acol;                          // column of each A entry (residuals, dominance check)
+  DBuf<int64_t> Acolp;                         // A's colptr (device dominance check)
+  DBuf<int32_t> domflag;
   int refine_steps = 0;
   double refine_resid = -1;
   DBuf<int64_t> Arowptr, p0, q, posfirst;
@@ -418,6 +426,8 @@ struct smlu_handle {
     ch_q.free();
     ch_version = -1;
     Acol.free();
+    Acolp.free();
+    domflag.free();
     for (auto* b : d) b->free();
     DBuf<int64_t>* l[] = {&Arowptr, &p0, &q, &posfirst};
     for (auto* b : l) b->free();
@@ -2121,7 +2131,7 @@ static int setup_device(smlu_handle* h) {
   HIPCHK(init_kernel_attributes());
   if (h->hinfo) HIPCHK(hipHostFree(h->hinfo));
   h->hinfo = nullptr;
-  HIPCHK(hipHostMalloc((void**)&h->hinfo, sizeof(int32_t) * std::max<int64_t>(nnodes, 1), 0));
+  HIPCHK(hipHostMalloc((void**)&h->hinfo, sizeof(int32_t) * std::max<int64_t>(nnodes, 2), 0));   // >= 2: dominance flags
   return build_schedule(h);
 }
 
@@ -2751,29 +2761,53 @@ int smlu_create_with_pivots(int64_t n, const int64_t* colptr, const int64_t* row
   return create_impl(n, colptr, rowval, nzval, p, q, Rs, opts, out);
 }
 
+static int ensure_residual(smlu_handle* h);
+
+// Pivoting mode per refactor: dominant values take the diagonal-tile path for
+// the mid-size fronts; a handle left in full-candidate mode by a re-pivoting refactor returns to
+// the fast schedule once the values are dominant again.  Every rank of a partitioned handle sees
+// the same values and takes the same decision.
+static int apply_dominance(smlu_handle* h, bool dom) {
+  bool changed = false;
+  if (dom != h->dominant) {
+    h->dominant = dom;
+    changed = h->pivmode == 0;
+  }
+  if (dom && h->pivmode == 1) {
+    h->pivmode = 0;
+    changed = true;
+  }
+  return changed ? rebuild_schedule(h) : SMLU_OK;
+}
+
+// The same dominance test on values already in HBM (k_dominance: one thread per column and row,
+// the host's summation order), for device-only callers.
+static int device_dominant(smlu_handle* h, bool* dom) {
+  const Plan& P = h->plan;
+  hipStream_t st = h->stream;
+  if (!h->Acolp.p) {
+    HIPCHK(h->Acolp.upload(P.Acolptr.data(), P.Acolptr.size(), st));
+    HIPCHK(h->domflag.alloc(2));
+  }
+  int rc = ensure_residual(h);   // the column of every A entry
+  if (rc != SMLU_OK) return rc;
+  HIPCHK(launch_dominance(st, P.n, h->Acolp.p, h->Arow.p, h->Arowptr.p, h->Arow_ent.p, h->Acol.p, h->A.p,
+                          h->domflag.p, h->hinfo));
+  HIPCHK(hipStreamSynchronize(st));
+  *dom = h->hinfo[0] != 0 || h->hinfo[1] != 0;
+  return SMLU_OK;
+}
+
 int smlu_refactor(smlu_handle* h, const double* nzval) {
   if (!h || !nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
-  if (h->nranks > 1) return fail(h, SMLU_ERR_STATE, "partitioned handle: use smlu_dist_set_values");
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipMemcpyAsync(h->A.p, nzval, sizeof(double) * h->plan.nnzA, hipMemcpyHostToDevice, h->stream));
   if (!h->plan.given_order && !h->plan.matched) {   // pivoting mode per refactor: re-check dominance
     const Plan& P = h->plan;
-    const bool dom = diagonally_dominant(P.n, P.Acolptr.data(), P.Arow.data(), nzval, 0);
-    bool changed = false;
-    if (dom != h->dominant) {
-      h->dominant = dom;
-      changed = h->pivmode == 0;
-    }
-    if (dom && h->pivmode == 1) {
-      h->pivmode = 0;
-      changed = true;
-    }
-    if (changed) {
-      int rc = rebuild_schedule(h);
-      if (rc != SMLU_OK) return rc;
-    }
+    int rc = apply_dominance(h, diagonally_dominant(P.n, P.Acolptr.data(), P.Arow.data(), nzval, 0));
+    if (rc != SMLU_OK) return rc;
   }
-  return run_factor(h);
+  return run_factor(h);   // collective on a partitioned handle
 }
 
 int smlu_refactor_device(smlu_handle* h, const double* d_nzval) {
@@ -2781,6 +2815,12 @@ int smlu_refactor_device(smlu_handle* h, const double* d_nzval) {
   HIPCHK(hipSetDevice(h->device));
   if (d_nzval != h->A.p)
     HIPCHK(hipMemcpyAsync(h->A.p, d_nzval, sizeof(double) * h->plan.nnzA, hipMemcpyDeviceToDevice, h->stream));
+  if (!h->plan.given_order && !h->plan.matched && !h->zc) {
+    bool dom = false;
+    int rc = device_dominant(h, &dom);
+    if (rc == SMLU_OK) rc = apply_dominance(h, dom);
+    if (rc != SMLU_OK) return rc;
+  }
   return run_factor(h);
 }
 

@@ -1,10 +1,13 @@
-# Julia ccall shim over libsmlu.so (untested here: no Julia in the image). See INTEGRATION.md.
+# Julia ccall shim over libsmlu.so.  No Julia in the image: tests/test_julia_shim.py checks it
+# statically against include/smlu.h (struct layout, constructor arity, every ccall'd symbol and
+# its argument count).  See INTEGRATION.md.
 module SharedMemSparseLU
 
 export ParallelSparseLU, cleanup_ParallelSparseLU!, allocate_shared
 
 using LinearAlgebra, SparseArrays, Libdl
 import LinearAlgebra: ldiv!, lu!
+import MPI                                     # declared by the reference (Project.toml:8)
 
 const libsmlu = get(ENV, "SMLU_LIB", joinpath(@__DIR__, "..", "deps", "libsmlu.so"))
 
@@ -18,7 +21,7 @@ mutable struct SmluOpts
     device::Int32; profile::Int32; leaf_size::Int64; use_mfma::Int32; refine::Int32; vendor_gemm::Int32
 end
 function default_opts()
-    o = SmluOpts(0, 0, 0, (0, 0, 0), 0, 0, 0.0, 0.0, 0, 0, 0, 0, 0)
+    o = SmluOpts(0, 0, 0, (0, 0, 0), 0, 0, 0.0, 0.0, 0, 0, 0, 0, 0, 0)
     ccall((:smlu_default_opts, libsmlu), Cvoid, (Ref{SmluOpts},), o)
     return o                                   # index_base = 1: Julia's 1-based CSC as is
 end
@@ -76,16 +79,41 @@ function ParallelSparseLU(A::SparseMatrixCSC{Tf,Ti}, chunk_size=nothing) where {
     return F
 end
 
-# Optional: hand UMFPACK's own analysis over so that pivot order matches it by construction.
-function ParallelSparseLU_umfpack(A::SparseMatrixCSC{Float64,Int64})
+# Optional: hand UMFPACK's own analysis over so that pivot order matches it by construction
+# (SURVEY §8f-1): the reference's lu(A) (:74) and its p, q, Rs extraction (:75-77, :93-94).
+function ParallelSparseLU_umfpack(A::SparseMatrixCSC{Float64,Ti}, chunk_size=nothing) where {Ti<:SmluInt}
     U = lu(A)
-    o = default_opts(); h = Ref{Ptr{Cvoid}}(C_NULL)
+    o = default_opts(); o.chunk_size = min(something(chunk_size, 8), A.n); h = Ref{Ptr{Cvoid}}(C_NULL)
     rc = ccall((:smlu_create_with_pivots, libsmlu), Int32,
                (Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Ptr{Int64}, Ptr{Int64},
                 Ptr{Float64}, Ref{SmluOpts}, Ref{Ptr{Cvoid}}),
-               A.n, A.colptr, A.rowval, A.nzval, U.p, U.q, U.Rs, o, h)
+               A.n, Vector{Int64}(A.colptr), Vector{Int64}(A.rowval), A.nzval,
+               Vector{Int64}(U.p), Vector{Int64}(U.q), U.Rs, o, h)
     check(rc, h[])
-    F = ParallelSparseLU{Float64,Int64}(A.m, A.n, h[], copy(A.colptr), copy(A.rowval), 8)
+    F = ParallelSparseLU{Float64,Ti}(A.m, A.n, h[], copy(A.colptr), copy(A.rowval), o.chunk_size)
+    finalizer(cleanup_ParallelSparseLU!, F)
+    return F
+end
+
+# One process per GPU (the rank split the reference only sketches, :107, :128; MPI is its declared
+# dependency, Project.toml:8).  Collective over `comm`: rank 0 creates the RCCL unique id, MPI
+# broadcasts the 128 bytes, every rank builds its part of the partition on its node-local GPU and
+# the library moves the blocks itself over RCCL/xGMI.  lu! and ldiv! below are then collective too
+# (every rank calls them with the same values / right-hand side; x comes back complete everywhere).
+function ParallelSparseLU(A::SparseMatrixCSC{Float64,Int64}, comm::MPI.Comm, chunk_size=nothing)
+    rank = MPI.Comm_rank(comm); nranks = MPI.Comm_size(comm)
+    id = zeros(UInt8, 128)
+    rank == 0 && check(ccall((:smlu_rccl_unique_id, libsmlu), Int32, (Ptr{UInt8},), id), C_NULL)
+    MPI.Bcast!(id, 0, comm)
+    o = default_opts(); o.chunk_size = min(something(chunk_size, 8), A.n)
+    o.device = MPI.Comm_rank(MPI.Comm_split_type(comm, MPI.COMM_TYPE_SHARED, rank))   # node-local GPU
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    rc = ccall((:smlu_dist_create_rccl, libsmlu), Int32,
+               (Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Ref{SmluOpts}, Int32, Int32, Ptr{UInt8},
+                Ref{Ptr{Cvoid}}),
+               A.n, A.colptr, A.rowval, A.nzval, o, rank, nranks, id, h)
+    check(rc, h[])
+    F = ParallelSparseLU{Float64,Int64}(A.m, A.n, h[], copy(A.colptr), copy(A.rowval), o.chunk_size)
     finalizer(cleanup_ParallelSparseLU!, F)
     return F
 end
@@ -123,14 +151,15 @@ function ldiv!(x::AbstractVecOrMat, F::ParallelSparseLU{Tf}, b::AbstractVecOrMat
     return x
 end
 
-function _trisolve!(name, F::ParallelSparseLU{Tf}, x::AbstractVector) where {Tf}
+function _trisolve!(upper::Bool, F::ParallelSparseLU{Tf}, x::AbstractVector) where {Tf}
     xx = x isa Vector{Tf} ? x : Vector{Tf}(x)
-    check(ccall(fnptr(name), Int32, (Ptr{Cvoid}, Ptr{Tf}), F.handle, xx), F.handle)
+    check(ccall(fnptr(upper ? :smlu_rsolve : :smlu_lsolve), Int32, (Ptr{Cvoid}, Ptr{Tf}), F.handle, xx),
+          F.handle)
     xx === x || copyto!(x, xx)
     return nothing
 end
-lsolve!(F::ParallelSparseLU, x) = _trisolve!(:smlu_lsolve, F, x)                   # :349
-rsolve!(F::ParallelSparseLU, x) = _trisolve!(:smlu_rsolve, F, x)                   # :374
+lsolve!(F::ParallelSparseLU, x) = _trisolve!(false, F, x)                          # :349
+rsolve!(F::ParallelSparseLU, x) = _trisolve!(true, F, x)                           # :374
 
 # Optional parity mode: the reference's own dense-chunk layout (:101-243) on the GPU, refilled
 # after each lu! (:265-276); ldiv! through it runs lsolve!/rsolve! chunk by chunk (:349-392).
@@ -144,7 +173,7 @@ function chunked_ldiv!(x::AbstractVector, F::ParallelSparseLU{Tf}, b::AbstractVe
     copyto!(x, xx)
 end
 
-function Base.getproperty(F::ParallelSparseLU, s::Symbol)                           # :45-52
+function Base.getproperty(F::ParallelSparseLU{Tf,Ti}, s::Symbol) where {Tf,Ti}     # :45-52
     s in (:L, :U, :p, :q, :Rs) || return getfield(F, s)
     h = getfield(F, :handle)
     n = Int64(getfield(F, :n)); nl = Ref{Int64}(0); nu = Ref{Int64}(0)
@@ -161,8 +190,8 @@ function Base.getproperty(F::ParallelSparseLU, s::Symbol)                       
                 h, Lp, Li, Lx, Up, Ui, Ux, p, q, Rs), h)
     s === :L && return SparseMatrixCSC(n, n, Lp, Li, Lx)
     s === :U && return SparseMatrixCSC(n, n, Up, Ui, Ux)
-    s === :p && return p
-    s === :q && return q
+    s === :p && return Vector{Ti}(p)           # p::Vector{Ti}, q::Vector{Ti} as the reference (:49-50)
+    s === :q && return Vector{Ti}(q)
     return Rs
 end
 

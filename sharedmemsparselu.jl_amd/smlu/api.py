@@ -258,6 +258,7 @@ def ldiv_(x, F: ParallelSparseLU, b):
         raise DimensionMismatch(f"`b` does not have same size as F: length(b)={len(b)}, F.n={F.n}")
     if not F.is_complex and (np.iscomplexobj(b) or np.iscomplexobj(x)):
         raise TypeError("complex vectors need a factorization of a complex matrix")
+    _need_complex_x(F, x)
     if np.ndim(b) == 2 or np.ndim(x) == 2:
         # several right-hand sides (columns), SURVEY §8f-4: one C-ABI call, column-major buffers
         if np.shape(x) != np.shape(b):
@@ -281,7 +282,15 @@ def ldiv_(x, F: ParallelSparseLU, b):
     return x
 
 
+def _need_complex_x(F, x):
+    """A complex factorization writes a complex solution: a real x would silently drop the
+    imaginary part (Julia raises InexactError there), so it is refused."""
+    if F.is_complex and not np.iscomplexobj(x):
+        raise TypeError("the solution of a complex factorization needs a complex x")
+
+
 def _tri(F, x, which):
+    _need_complex_x(F, x)
     if len(x) != F.n:
         raise DimensionMismatch(f"`x` does not have same size as F: length(x)={len(x)}, F.n={F.n}")
     xx = x if (isinstance(x, np.ndarray) and x.dtype == F._dt and x.flags.c_contiguous) \
@@ -315,6 +324,7 @@ def chunked_ldiv_(x, F: ParallelSparseLU, b):
     chunk on the GPU.  Same DimensionMismatch checks as ldiv_; x may be b."""
     if len(x) != F.n or len(b) != F.n:
         raise DimensionMismatch(f"x and b must have length F.n={F.n}: {len(x)}, {len(b)}")
+    _need_complex_x(F, x)
     bb = np.ascontiguousarray(b, dtype=F._dt)
     xx = np.empty(F.n, dtype=F._dt)
     _check(C.lib().smlu_chunked_ldiv(F._h, C.ptr(bb), C.ptr(xx)), F._h)

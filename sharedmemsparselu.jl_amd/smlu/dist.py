@@ -102,6 +102,8 @@ class DistributedSparseLU:
         backend = dist.get_backend(group)
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         A = _csc(A)
+        if np.iscomplexobj(A.data):   # the partitioned path is real-only; never drop the imaginary part
+            raise TypeError("DistributedSparseLU factors real matrices only (ComplexF64: one GPU)")
         self.n = A.shape[0]
         order = {"auto": C.ORDER_AUTO, "natural": C.ORDER_NATURAL, "nd": C.ORDER_GRAPH_ND,
                  "geometric": C.ORDER_GEOMETRIC_ND, "amd": C.ORDER_AMD}[ordering]
@@ -145,6 +147,15 @@ class DistributedSparseLU:
     @property
     def refine_steps(self):
         return int(self.stat("refine_steps"))
+
+    def refactor(self, values):
+        """lu!(F, A) with host values (A's CSC order, float64); collective (smlu_refactor)."""
+        v = np.ascontiguousarray(values, dtype=np.float64)
+        rc = _check(C.lib().smlu_refactor(self._h, C.ptr(v)), self._h)
+        self.status = rc
+        if rc == C.SMLU_SINGULAR:
+            raise SingularException(C.lib().smlu_last_error_col(self._h))
+        return rc
 
     def refactor_device(self, d_values):
         """lu!(F, A) with values already in HBM (A's CSC order); collective."""

@@ -32,6 +32,15 @@ def _matrix(which):
     return sp.csc_matrix(mats.random_dominant(3000, 0.003, seed=5))
 
 
+def _values3(A):
+    A3 = A.copy()
+    A3.setdiag(A3.diagonal() * 2.0 + 1.0)
+    import scipy.sparse as sp
+    A3 = sp.csc_matrix(A3)
+    A3.sort_indices()
+    return A3.data
+
+
 def _worker(rank, world, port, which, ob, q, transport="auto"):
     try:
         import scipy.sparse as sp
@@ -60,9 +69,13 @@ def _worker(rank, world, port, which, ob, q, transport="auto"):
         F.refactor_device(torch.from_numpy(np.ascontiguousarray(A2.data)).cuda())
         F.solve_device(dx, db)
         x2 = dx.cpu().numpy()
+        # lu! with host values on the partitioned handle (smlu_refactor, collective)
+        F.refactor(_values3(A))
+        F.solve_device(dx, db)
+        x3 = dx.cpu().numpy()
         info = {k: F.stat(k) for k in ("shared_fronts", "owned_blocks", "comm_steps")}
         info["transport"] = F.transport
-        q.put((rank, x1, x2, info, None))
+        q.put((rank, (x1, x3), x2, info, None))
         F.close()
         dist.destroy_process_group()
     except Exception:  # report instead of hanging the parent
@@ -100,12 +113,18 @@ def test_dist_factor_solve_matches_single_gpu(world, which, ob):
     smlu.lu_(F, A2)
     xs2 = np.empty(n)
     smlu.ldiv_(xs2, F, b)
+    A3 = A.copy()
+    A3.data = _values3(A)
+    smlu.lu_(F, A3)
+    xs3 = np.empty(n)
+    smlu.ldiv_(xs3, F, b)
     F.close()
     # the partition really shares fronts between ranks and moves data
     assert max(r[3]["shared_fronts"] for r in res) >= 1
     assert all(r[3]["comm_steps"] >= 1 for r in res)
-    for rank, x1, x2, _, _ in res:
+    for rank, (x1, x3), x2, _, _ in res:
         # every rank holds the full solution
+        assert np.allclose(x3, xs3, rtol=1e-11, atol=1e-13), (rank, np.abs(x3 - xs3).max())
         assert np.allclose(x1, xs1, rtol=1e-11, atol=1e-13), (rank, np.abs(x1 - xs1).max())
         assert np.allclose(x2, xs2, rtol=1e-11, atol=1e-13), (rank, np.abs(x2 - xs2).max())
         r1 = np.abs(A @ x1 - b).max() / np.abs(b).max()
@@ -198,7 +217,7 @@ def test_dist_rccl_transport_single_rank():
     port = _free_port()
     p = ctx.Process(target=_worker, args=(0, 1, port, "poisson", 0, q, "rccl"))
     p.start()
-    rank, x1, x2, info, err = q.get(timeout=240)
+    rank, x13, x2, info, err = q.get(timeout=240)
     p.join(timeout=120)
     assert err is None, err
     assert p.exitcode == 0
@@ -210,4 +229,4 @@ def test_dist_rccl_transport_single_rank():
     xs1 = np.empty(n)
     smlu.ldiv_(xs1, F, b)
     F.close()
-    assert np.allclose(x1, xs1, rtol=1e-11, atol=1e-13)
+    assert np.allclose(x13[0], xs1, rtol=1e-11, atol=1e-13)

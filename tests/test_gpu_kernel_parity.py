@@ -303,3 +303,38 @@ def test_lu_pattern_change(gpu):
     smlu.lu_(F, A)
     smlu.ldiv_(x, F, b)
     assert isapprox(x, spla.spsolve(A, b), TOL, TOL)
+
+
+def test_refactor_device_redecides_pivoting_mode(gpu):
+    # the device-only lu! (values already in HBM, the bench's usage) re-checks dominance on the
+    # GPU (k_dominance) like the host lu! does: after a re-pivoting refactor left the handle in
+    # full-candidate mode, dominant values bring the fast diagonal-tile schedule back
+    import torch
+    n = 700
+    Dd = _dominant_dense(n, 41)
+    A = sp.csc_matrix(Dd)
+    F = smlu.ParallelSparseLU(A)
+    assert F.stat("dominant") == 1.0 and F.stat("pivmode") == 0
+    m2 = F.stat("fronts_mode2")
+    assert m2 > 0
+
+    def dev(D):
+        return torch.tensor(sp.csc_matrix(D).data, dtype=torch.float64, device="cuda")
+
+    Dw = _weak_tile_matrix(n, 42)
+    F.refactor_device(dev(Dw))
+    assert F.stat("dominant") == 0.0
+    assert F.stat("repivots") == 1 and F.stat("pivmode") == 1 and F.stat("weak") == 0
+    b = np.random.default_rng(5).random(n)
+    x = np.empty(n)
+    smlu.ldiv_(x, F, b)
+    ctol = max(DENSE_TOL, 8 * np.finfo(float).eps * np.linalg.cond(Dw))
+    assert isapprox(x, np.linalg.solve(Dw, b), ctol, ctol)
+    factor_parity(sp.csc_matrix(Dw), F, rtol=1e-10)
+    Dd2 = _dominant_dense(n, 43)
+    F.refactor_device(dev(Dd2))
+    assert F.stat("dominant") == 1.0 and F.stat("pivmode") == 0
+    assert F.stat("fronts_mode2") == m2 and F.stat("repivots") == 1
+    smlu.ldiv_(x, F, b)
+    assert isapprox(x, np.linalg.solve(Dd2, b), DENSE_TOL, DENSE_TOL)
+    factor_parity(sp.csc_matrix(Dd2), F, rtol=1e-11)
