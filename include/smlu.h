@@ -183,6 +183,18 @@ int smlu_get_factors(smlu_handle* h, int64_t* Lcolptr, int64_t* Lrowval, double*
                      int64_t* Ucolptr, int64_t* Urowval, double* Unzval,
                      int64_t* p, int64_t* q, double* Rs);
 
+/* The assembly tree of the handle's analysis (diagnostic: the tests' pivot-rule oracle replays
+ * the GPU's pivot decisions on it).  first[nsup+1]: first column (pivot position) of each front;
+ * parent[nsup] (-1: root; parents follow their children); rowptr[nsup+1] / rows[rowptr[nsup]]:
+ * the update rows of each front (sorted positions); p0[n]: the row order before pivoting (new ->
+ * old, 0-based: q, or q composed with the zero-free-diagonal transversal); mode[nsup]: pivot
+ * candidates of the current schedule (0: small front, every fully-summed row; 1: blocked front,
+ * every fully-summed row; 2: blocked front, the rows of the 64 x 64 diagonal tile).  The final row
+ * order is p[k] = p0[first[s] + rowperm_s[k - first[s]]] for the pivot sequence chosen per front.
+ * nsup = smlu_stat(h, "nsuper"); NULL pointers are skipped. */
+int smlu_get_fronts(smlu_handle* h, int64_t* first, int64_t* parent, int64_t* rowptr, int64_t* rows,
+                    int64_t* p0, int32_t* mode);
+
 /* cleanup_ParallelSparseLU!(F) — exported but undefined in the reference
  * (src/SharedMemSparseLU.jl:31): frees device memory, stream and host plan. */
 void smlu_destroy(smlu_handle* h);
@@ -209,6 +221,9 @@ int  smlu_plan_pattern(const smlu_plan* plan, int64_t* q, int64_t* Lcolptr, int6
 /* Supernode partition: first column of each supernode (nsuper+1 entries), parent
  * supernode (-1 for roots) and level; NULL pointers are skipped. */
 int  smlu_plan_supernodes(const smlu_plan* plan, int64_t* first, int64_t* parent, int64_t* level);
+/* Update rows of every front (rowptr[nsup+1], rows[rowptr[nsup]], sorted positions) and the
+ * row pre-order p0 (new -> old) of a host-only plan; NULL pointers are skipped. */
+int  smlu_plan_fronts(const smlu_plan* plan, int64_t* rowptr, int64_t* rows, int64_t* p0);
 void smlu_plan_destroy(smlu_plan* plan);
 
 /* ---- multi-GPU partition ---------------------------------------------------

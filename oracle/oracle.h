@@ -28,6 +28,21 @@ int oracle_rsolve(int64_t n, const int64_t* Up, const int64_t* Ui, const double*
 int oracle_ldiv(const oracle_lu* F, const double* Rs, const int64_t* p, const int64_t* q,
                 const double* b, double* x);
 
+/* mf.c: multifrontal restatement of the GPU's pivot rule (and the multi-core CPU baseline).
+ * p0, q: row pre-order and column order (new -> old); the assembly tree: first[nsup+1],
+ * parent[nsup] (postorder: parent > child, -1 root), update rows rowptr[nsup+1] / rows (sorted
+ * global positions); mode[nsup]: 0/1 = every fully-summed row is a candidate, 2 = the 64 x 64
+ * diagonal tile (NULL: 1 everywhere). */
+typedef struct oracle_mf oracle_mf;
+oracle_mf* oracle_mf_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const int64_t* p0,
+                            const int64_t* q, int64_t nsup, const int64_t* first, const int64_t* parent,
+                            const int64_t* rowptr, const int64_t* rows, const int32_t* mode,
+                            double diag_tol, double piv_tol, int nthreads, int* status);
+int oracle_mf_factor(oracle_mf* h, const double* nzval);
+void oracle_mf_result(const oracle_mf* h, int32_t* rowperm, int32_t* flags, double* Rs);
+void oracle_mf_destroy(oracle_mf* h);
+int oracle_dominant(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* a);
+
 #ifdef __cplusplus
 }
 #endif

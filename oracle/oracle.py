@@ -51,8 +51,8 @@ _f64p = ctypes.POINTER(ctypes.c_double)
 def build():
     """Compile liboracle.so (gcc) if missing or stale."""
     so = os.path.join(_HERE, "liboracle.so")
-    src = os.path.join(_HERE, "oracle.c")
-    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+    srcs = [os.path.join(_HERE, f) for f in ("oracle.c", "mf.c", "oracle.h")]
+    if not os.path.exists(so) or any(os.path.getmtime(so) < os.path.getmtime(f) for f in srcs):
         subprocess.check_call(["make", "-s", "-C", _HERE])
     return so
 
@@ -71,6 +71,17 @@ def lib():
         L.oracle_lu_nnz.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.oracle_lu_export.argtypes = [ctypes.c_void_p, _i64p, _i64p, _f64p, _i64p, _i64p, _f64p]
         L.oracle_ldiv.argtypes = [ctypes.c_void_p, _f64p, _i64p, _i64p, _f64p, _f64p]
+        vp = ctypes.c_void_p
+        L.oracle_mf_create.restype = vp
+        L.oracle_mf_create.argtypes = [ctypes.c_int64, vp, vp, vp, vp, ctypes.c_int64, vp, vp, vp, vp, vp,
+                                       ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_int)]
+        L.oracle_mf_factor.restype = ctypes.c_int
+        L.oracle_mf_factor.argtypes = [vp, vp]
+        L.oracle_mf_result.argtypes = [vp, vp, vp, vp]
+        L.oracle_mf_destroy.argtypes = [vp]
+        L.oracle_dominant.restype = ctypes.c_int
+        L.oracle_dominant.argtypes = [ctypes.c_int64, vp, vp, vp]
         _LIB = L
     return _LIB
 
@@ -143,6 +154,124 @@ class OracleLU:
         wrk = _csc_rsolve(self.U, wrk)
         x[self.q] = wrk
         return x
+
+
+# --------------------------------------------------------------------------------------
+# Independent pivot choice: multifrontal restatement of the GPU's documented pivot rule (mf.c)
+# --------------------------------------------------------------------------------------
+def _vp(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def dominant(A):
+    """Diagonal dominance by columns or rows (the pivoting-mode test)."""
+    A, cp, ri, x = _csc(A)
+    return bool(lib().oracle_dominant(A.shape[0], _vp(cp), _vp(ri), _vp(x)))
+
+
+class MultifrontalOracle:
+    """Multifrontal LU of (Rs .* A)[p0, q] over a given assembly tree (mf.c), choosing its own
+    pivots with threshold partial pivoting (diagonal preference) inside each front's candidate
+    rows.  `fronts`: dict(first, parent, rowptr, rows, p0) as exported by smlu_get_fronts /
+    smlu_plan_fronts plus the column order `q`; `mode`: candidate set per front (None: every
+    fully-summed row).  factor(values) -> status (0 ok, 1 zero candidate column)."""
+
+    def __init__(self, A, q, fronts, mode=None, diag_tol=0.1, pivot_tol=0.1, threads=1):
+        A, cp, ri, _ = _csc(A)
+        self.n = A.shape[0]
+        self._keep = [np.ascontiguousarray(v, dtype=np.int64) for v in
+                      (cp, ri, fronts["p0"], q, fronts["first"], fronts["parent"], fronts["rowptr"],
+                       fronts["rows"])]
+        cp, ri, p0, q, first, parent, rowptr, rows = self._keep
+        self.p0, self.first = p0, first
+        self.nsup = first.size - 1
+        self.mode = None if mode is None else np.ascontiguousarray(mode, dtype=np.int32)
+        st = ctypes.c_int(0)
+        self._h = lib().oracle_mf_create(self.n, _vp(cp), _vp(ri), _vp(p0), _vp(q), self.nsup, _vp(first),
+                                         _vp(parent), _vp(rowptr), _vp(rows), _vp(self.mode),
+                                         float(diag_tol), float(pivot_tol), int(threads), ctypes.byref(st))
+        if not self._h:
+            raise RuntimeError(f"oracle_mf_create failed ({st.value})")
+
+    def factor(self, values):
+        v = np.ascontiguousarray(values, dtype=np.float64)
+        rc = lib().oracle_mf_factor(self._h, _vp(v))
+        if rc < 0:
+            raise MemoryError("oracle_mf_factor failed")
+        self.rowperm = np.empty(self.n, np.int32)
+        self.flags = np.empty(self.nsup, np.int32)
+        self.Rs = np.empty(self.n)
+        lib().oracle_mf_result(self._h, _vp(self.rowperm), _vp(self.flags), _vp(self.Rs))
+        return rc
+
+    @property
+    def p(self):
+        """Final row order: p[k] = p0[first_s + rowperm[k]] (new -> old)."""
+        f = np.repeat(self.first[:-1], np.diff(self.first))
+        return self.p0[f + self.rowperm]
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().oracle_mf_destroy(self._h)
+        self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+SMALL_M = 128        # fronts up to this order are factored whole (mode 0)
+FULL_PIV_NS = 512    # blocked fronts with at most this many pivots search every fully-summed row
+
+
+def front_modes(fronts, pivmode, dominant_values, full_piv_ns=None):
+    """The GPU schedule's candidate set per front (restated from DESIGN.md §4 / build_schedule):
+    M <= 128 -> 0 (small front, all fully-summed rows); else ns <= limit -> 1 (all fully-summed
+    rows), otherwise 2 (the 64 x 64 diagonal tile).  limit: unbounded after a re-pivoting refactor
+    (pivmode 1), 128 for dominant values, 512 otherwise."""
+    first, rowptr = fronts["first"], fronts["rowptr"]
+    ns = np.diff(first)
+    M = ns + np.diff(rowptr)
+    if full_piv_ns is None:
+        full_piv_ns = np.iinfo(np.int64).max if pivmode == 1 else (SMALL_M if dominant_values else FULL_PIV_NS)
+    return np.where(M <= SMALL_M, 0, np.where(ns <= full_piv_ns, 1, 2)).astype(np.int32)
+
+
+def gpu_pivot_choice(A, q, fronts, *, pivmode=0, dominant_values=None, given=False, pivot_tol=0.1,
+                     diag_tol=0.1, full_piv_ns=None, values=None):
+    """Independent restatement of the GPU path's whole pivot decision for one factorization:
+    the candidate modes, threshold partial pivoting inside every front (mf.c), and the
+    re-pivoting refactor (a zero or weak pivot while diagonal-tile fronts exist -> every blocked
+    front again with all fully-summed rows as candidates).  `pivmode`: the handle's mode before
+    this factorization (dominant values reset it to 0).  A given (p, q) keeps the diagonal unless
+    it is exactly zero (diag_tol 0) and is never re-pivoted.  Returns (p, pivmode, modes, flags)."""
+    A = sp.csc_matrix(A)
+    A.sort_indices()
+    vals = A.data if values is None else values
+    matched = not np.array_equal(fronts["p0"], q)
+    if dominant_values is None:
+        dominant_values = (not matched and not given) and dominant(sp.csc_matrix((vals, A.indices, A.indptr),
+                                                                                 shape=A.shape))
+    if dominant_values:
+        pivmode = 0
+    dt = 0.0 if given else diag_tol
+
+    def run(pm):
+        modes = front_modes(fronts, pm, dominant_values, full_piv_ns)
+        mf = MultifrontalOracle(A, q, fronts, modes, diag_tol=dt, pivot_tol=pivot_tol)
+        st = mf.factor(vals)
+        out = (mf.p, modes, mf.flags.copy(), st)
+        mf.close()
+        return out
+
+    p, modes, flags, st = run(pivmode)
+    if ((st == 1 or (flags & 2).any()) and pivmode == 0 and (modes == 2).any() and pivot_tol > 0
+            and not given):
+        pivmode = 1
+        p, modes, flags, st = run(1)
+    return p, pivmode, modes, flags
 
 
 def _csc_lsolve(L, b):

@@ -2798,6 +2798,18 @@ static int device_dominant(smlu_handle* h, bool* dom) {
   return SMLU_OK;
 }
 
+// lu! on the values already in h->A: the pivoting mode re-decided on the device, then the
+// factorization (with the re-pivoting fallback).
+static int refactor_resident(smlu_handle* h) {
+  if (!h->plan.given_order && !h->plan.matched) {
+    bool dom = false;
+    int rc = device_dominant(h, &dom);
+    if (rc == SMLU_OK) rc = apply_dominance(h, dom);
+    if (rc != SMLU_OK) return rc;
+  }
+  return run_factor(h);
+}
+
 int smlu_refactor(smlu_handle* h, const double* nzval) {
   if (!h || !nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
   HIPCHK(hipSetDevice(h->device));
@@ -2815,13 +2827,7 @@ int smlu_refactor_device(smlu_handle* h, const double* d_nzval) {
   HIPCHK(hipSetDevice(h->device));
   if (d_nzval != h->A.p)
     HIPCHK(hipMemcpyAsync(h->A.p, d_nzval, sizeof(double) * h->plan.nnzA, hipMemcpyDeviceToDevice, h->stream));
-  if (!h->plan.given_order && !h->plan.matched && !h->zc) {
-    bool dom = false;
-    int rc = device_dominant(h, &dom);
-    if (rc == SMLU_OK) rc = apply_dominance(h, dom);
-    if (rc != SMLU_OK) return rc;
-  }
-  return run_factor(h);
+  return refactor_resident(h);
 }
 
 static int refactor_csc_impl(smlu_handle* h, int64_t n, const int64_t* colptr, const int64_t* rowval,
@@ -3014,7 +3020,7 @@ int smlu_refactor_z_device(smlu_handle* h, const double* d_nzval) {
     HIPCHK(h->d_zoff.upload(h->zoff.data(), h->zoff.size(), h->stream));
   }
   HIPCHK(launch_expand_z(h->stream, h->znnz, d_nzval, h->d_zdst.p, h->d_zoff.p, h->A.p));
-  return run_factor(h);
+  return refactor_resident(h);
 }
 
 int smlu_refactor_csc_z(smlu_handle* h, int64_t n, const int64_t* colptr, const int64_t* rowval,
@@ -3768,6 +3774,35 @@ int smlu_plan_supernodes(const smlu_plan* pl, int64_t* first, int64_t* parent, i
     if (parent) parent[s] = P.s_parent[s];
     if (level) level[s] = P.s_level[s];
   }
+  return SMLU_OK;
+}
+
+static void fronts_of(const Plan& P, int64_t* first, int64_t* parent, int64_t* rowptr, int64_t* rows,
+                      int64_t* p0) {
+  for (int64_t s = 0; s <= P.nsup; ++s) {
+    if (first) first[s] = P.s_first[s];
+    if (rowptr) rowptr[s] = P.s_rowptr[s];
+  }
+  for (int64_t s = 0; s < P.nsup; ++s)
+    if (parent) parent[s] = P.s_parent[s];
+  if (rows)
+    for (int64_t e = 0; e < P.s_rowptr[P.nsup]; ++e) rows[e] = P.s_rows[e];
+  if (p0)
+    for (int64_t i = 0; i < P.n; ++i) p0[i] = P.p0[i];
+}
+
+int smlu_plan_fronts(const smlu_plan* pl, int64_t* rowptr, int64_t* rows, int64_t* p0) {
+  if (!pl) return SMLU_ERR_ARG;
+  fronts_of(pl->plan, nullptr, nullptr, rowptr, rows, p0);
+  return SMLU_OK;
+}
+
+int smlu_get_fronts(smlu_handle* h, int64_t* first, int64_t* parent, int64_t* rowptr, int64_t* rows,
+                    int64_t* p0, int32_t* mode) {
+  if (!h) return fail(h, SMLU_ERR_ARG, "NULL handle");
+  fronts_of(h->plan, first, parent, rowptr, rows, p0);
+  if (mode)
+    for (int64_t s = 0; s < h->plan.nsup; ++s) mode[s] = h->hsn[s].mode;
   return SMLU_OK;
 }
 

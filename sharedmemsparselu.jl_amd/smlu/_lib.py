@@ -87,6 +87,8 @@ SIGNATURES = {
     "smlu_plan_stat": (f64, [vp, ctypes.c_char_p]),
     "smlu_plan_pattern": (i32, [vp, vp, vp, vp]),
     "smlu_plan_supernodes": (i32, [vp, vp, vp, vp]),
+    "smlu_plan_fronts": (i32, [vp, vp, vp, vp]),
+    "smlu_get_fronts": (i32, [vp, vp, vp, vp, vp, vp, vp]),
     "smlu_plan_destroy": (None, [vp]),
     "smlu_version": (ctypes.c_char_p, []),
     "smlu_dist_create": (i32, [i64, vp, vp, vp, ctypes.POINTER(SmluOpts), i32, i32, vp, ctypes.POINTER(vp)]),

@@ -177,6 +177,23 @@ class ParallelSparseLU:
     def stat(self, key):
         return C.lib().smlu_stat(self._h, key.encode())
 
+    def fronts(self):
+        """The analysis' assembly tree and the current schedule's pivot-candidate mode per front
+        (smlu_get_fronts): dict(first, parent, rowptr, rows, p0, mode), 0-based."""
+        ns = int(self.stat("nsuper"))
+        n = int(self.stat("n"))
+        first = np.empty(ns + 1, np.int64)
+        parent = np.empty(ns, np.int64)
+        rowptr = np.empty(ns + 1, np.int64)
+        mode = np.empty(ns, np.int32)
+        L = C.lib()
+        _check(L.smlu_get_fronts(self._h, C.ptr(first), C.ptr(parent), C.ptr(rowptr), None, None,
+                                 C.ptr(mode)), self._h)
+        rows = np.empty(rowptr[-1], np.int64)
+        p0 = np.empty(n, np.int64)
+        _check(L.smlu_get_fronts(self._h, None, None, None, C.ptr(rows), C.ptr(p0), None), self._h)
+        return dict(first=first, parent=parent, rowptr=rowptr, rows=rows, p0=p0, mode=mode)
+
     # ---- device-resident entry points (values / vectors already in HBM) ----
     def refactor_device(self, d_values):
         """lu! with values already on the device (torch tensor or raw pointer int; complex

@@ -60,6 +60,17 @@ class Plan:
         C.lib().smlu_plan_supernodes(self._h, C.ptr(first), C.ptr(parent), C.ptr(level))
         return first, parent, level
 
+    def fronts(self):
+        """Assembly tree for the CPU multifrontal oracle: (first, parent, rowptr, rows, p0)."""
+        first, parent, _ = self.supernodes()
+        ns = first.size - 1
+        rowptr = np.empty(ns + 1, np.int64)
+        C.lib().smlu_plan_fronts(self._h, C.ptr(rowptr), None, None)
+        rows = np.empty(rowptr[-1], np.int64)
+        p0 = np.empty(int(self.stat("n")), np.int64)
+        C.lib().smlu_plan_fronts(self._h, C.ptr(rowptr), C.ptr(rows), C.ptr(p0))
+        return first, parent, rowptr, rows, p0
+
     def partition(self, nparts):
         """Owner rank per supernode of an `nparts`-rank partitioned handle (-1: a front shared
         by several ranks as a block-cyclic column partition) and the number of shared fronts."""
