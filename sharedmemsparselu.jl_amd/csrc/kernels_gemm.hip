@@ -600,6 +600,177 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma6(const GemmTask* __rest
 }
 
 // ------------------------------------------------------------------------------------
+// MFMA tile v2 (tile code 130; the default Schur-update kernel): the same 128 x 128 output tile
+// per 256-thread workgroup, each wave a 64 x 64 quadrant of 4 x 4 v_mfma_f64_16x16x4_f64 blocks,
+// the same per-element accumulation order (k ascending, one MFMA-FMA per k: bitwise identical to
+// gemm128_mfma_body and the VALU tiles), but half the memory instructions of v1:
+//  * 16-byte global loads: A as row pairs (m contiguous), B as k pairs (k contiguous);
+//  * A staged [k][128] in LDS with 16-byte stores; MFMA block rows are interleaved so that one
+//    conflict-free ds_read_b128 feeds two blocks: block i, lane row li holds tile row
+//    wr + 32 (i >> 1) + 2 li + (i & 1);
+//  * B staged [col][k] with k padded to 18 doubles: 16-byte stores, conflict-free b64 reads;
+//  * C read and written as row pairs (16-byte accesses, 256 contiguous bytes per 16 lanes);
+//  * the LDS fragments of the next k-quad are read while the current quad's 16 MFMAs run, and
+//    the next K slice's global loads are in flight across the whole slice.
+// Interior tiles only (m, n in range); edge tiles take gemm128_mfma_body<.., false>.
+// ------------------------------------------------------------------------------------
+#define B2LD 18
+#ifndef MFMA2_NOEDGE
+#define MFMA2_NOEDGE 0
+#endif
+typedef double v2du __attribute__((ext_vector_type(2), aligned(8)));   // 8-byte aligned pairs (global)
+typedef double v2d __attribute__((ext_vector_type(2)));                 // 16-byte aligned pairs (LDS)
+struct Mfma2Lds {
+  double A[2][HBK_][HBM_];    // [buf][k][row]
+  double B[2][HBM_][B2LD];    // [buf][col][k], negated
+};
+
+// Global accesses: wave-uniform 64-bit base (SGPRs, recomputed by scalar ALU where used) + a
+// per-lane 32-bit byte offset fixed for the whole tile, so no 64-bit per-lane address is live
+// across the K loop (the v1 interior spilled its precomputed C addresses).
+__device__ __forceinline__ v2d ldu2(const char* ubase, uint32_t off) {
+  return *(const __attribute__((address_space(1))) v2du*)(ubase + off);
+}
+__device__ __forceinline__ void stu2(char* ubase, uint32_t off, v2d v) {
+  *(__attribute__((address_space(1))) v2du*)(ubase + off) = v;
+}
+
+template <bool TRSM>
+__device__ __forceinline__ void gemm128_mfma2_interior(const GemmTask& t, int m0, int n0, Mfma2Lds& S,
+                                                       const GrowthArgs& ga) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = (wv & 1) * 64, wc = (wv >> 1) * 64;
+  const int li = lane & 15, lk = lane >> 4;
+  const int K = t.k;
+  const int64_t lda = t.lda, ldb = t.ldb, ldc = t.ldc;
+  // C <-> accumulators as row pairs: blocks 2ip and 2ip+1 hold rows 2li and 2li+1 of a 32-row strip
+  const uint32_t c_lo = (uint32_t)(((int64_t)lk * ldc + 2 * li) * 8);
+  auto cbase = [&](int ip, int j, int r) {
+    return reinterpret_cast<char*>(t.C) + ((int64_t)(n0 + wc + 16 * j + 4 * r) * ldc + m0 + wr + 32 * ip) * 8;
+  };
+  v4d acc[4][4];
+#pragma unroll
+  for (int ip = 0; ip < 2; ++ip)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const v2d c = ldu2(cbase(ip, j, r), c_lo);
+        acc[2 * ip][j][r] = c.x;
+        acc[2 * ip + 1][j][r] = c.y;
+      }
+  // staging of one K slice: A row pair 2*lane at k = wv + 4q (16-byte loads along m);
+  // B k pair 2*(lane & 7) of column 8 wv + (lane >> 3) + 32 q (16-byte loads along k)
+  const uint32_t a_lo = (uint32_t)(lane * 16);
+  const uint32_t b_lo = (uint32_t)((((int64_t)(lane >> 3)) * ldb + 2 * (lane & 7)) * 8);
+  const int b_k = 2 * (lane & 7);
+  auto abase = [&](int k0, int q) {
+    return reinterpret_cast<const char*>(t.A) + ((int64_t)(k0 + wv + 4 * q) * lda + m0) * 8;
+  };
+  auto bbase = [&](int k0, int q) {
+    return reinterpret_cast<const char*>(t.B) + ((int64_t)(n0 + 8 * wv + 32 * q) * ldb + k0) * 8;
+  };
+  v2d ra[4], rb[4];
+  auto gload_full = [&](int k0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ra[q] = ldu2(abase(k0, q), a_lo);
+      rb[q] = ldu2(bbase(k0, q), b_lo);
+    }
+  };
+  auto gload_tail = [&](int k0) {   // partial slice: k >= K reads as zero
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      ra[q] = k0 + wv + 4 * q < K ? ldu2(abase(k0, q), a_lo) : v2d{0.0, 0.0};
+      if (k0 + b_k + 1 < K) {
+        rb[q] = ldu2(bbase(k0, q), b_lo);
+      } else {
+        rb[q].x = k0 + b_k < K ? *(const gdbl*)(bbase(k0, q) + b_lo) : 0.0;
+        rb[q].y = 0.0;
+      }
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      *reinterpret_cast<v2d*>(&S.A[buf][wv + 4 * q][2 * lane]) = ra[q];
+      *reinterpret_cast<v2d*>(&S.B[buf][8 * wv + (lane >> 3) + 32 * q][b_k]) = -rb[q];
+    }
+  };
+  auto slice = [&](int cur) {
+#pragma unroll
+    for (int kq = 0; kq < HBK_ / 4; ++kq) {
+      const int k = 4 * kq + lk;
+      v2d fa[2];
+      double fb[4];
+#pragma unroll
+      for (int ip = 0; ip < 2; ++ip) fa[ip] = *reinterpret_cast<const v2d*>(&S.A[cur][k][wr + 32 * ip + 2 * li]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = S.B[cur][wc + 16 * j + li][k];
+#pragma unroll
+      for (int ip = 0; ip < 2; ++ip)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[2 * ip][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[j], fa[ip].x, acc[2 * ip][j], 0, 0, 0);
+          acc[2 * ip + 1][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[j], fa[ip].y, acc[2 * ip + 1][j], 0, 0, 0);
+        }
+    }
+  };
+  const int nk = (K + HBK_ - 1) / HBK_;
+  const int nfull = K / HBK_;
+  if (nfull > 0) gload_full(0);
+  else gload_tail(0);
+  sstore(0);
+  __syncthreads();
+  int kt = 0;
+  for (; kt + 1 < nfull; ++kt) {   // next slice complete: guard-free loads in flight
+    gload_full((kt + 1) * HBK_);
+    slice(kt & 1);
+    sstore((kt & 1) ^ 1);
+    __syncthreads();
+  }
+  if (kt + 1 < nk) {                // next slice partial
+    gload_tail((kt + 1) * HBK_);
+    slice(kt & 1);
+    sstore((kt & 1) ^ 1);
+    __syncthreads();
+    ++kt;
+  }
+  slice(kt & 1);                    // last slice
+  double gmax = 0.0;
+#pragma unroll
+  for (int ip = 0; ip < 2; ++ip)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const v2d c = v2d{acc[2 * ip][j][r], acc[2 * ip + 1][j][r]};
+        stu2(cbase(ip, j, r), c_lo, c);
+        if (TRSM) gmax = fmax(gmax, fmax(fabs(c.x), fabs(c.y)));
+      }
+  if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
+}
+
+template <bool TRSM>
+__global__ __launch_bounds__(256, 2) void k_gemm128_mfma2(const GemmTask* __restrict__ tasks, int ntask,
+                                                          GrowthArgs ga) {
+  __shared__ __attribute__((aligned(16))) double lds[sizeof(Mfma2Lds) / sizeof(double)];
+  const int64_t b = blockIdx.x;
+  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+  int tm, tn;
+  tile_rc<HBM_>(t, b - t.tile0, tm, tn);
+  const int m0 = tm * HBM_, n0 = tn * HBM_;
+  if (m0 + HBM_ <= t.m && n0 + HBM_ <= t.n) {
+    gemm128_mfma2_interior<TRSM>(t, m0, n0, *reinterpret_cast<Mfma2Lds*>(lds), ga);
+  } else if (!MFMA2_NOEDGE) {
+    auto& As = *reinterpret_cast<double(*)[2][HBK_][HBM_]>(lds);
+    auto& Bs = *reinterpret_cast<double(*)[2][HBK_][HLDB_]>(lds + 2 * HBK_ * HBM_);
+    gemm128_mfma_body<TRSM, false>(t, m0, n0, As, Bs, ga);
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Inverses of a factored 64 x 64 diagonal tile for the GEMM-form triangular solves:
 //   NL = I - L_kk^{-1} (L unit lower: the strictly lower part of the tile),
 //   NU = I - U_kk^{-1} (U upper with its diagonal),
@@ -687,7 +858,9 @@ hipError_t launch_gemm_g(hipStream_t st, int64_t ntiles, const GemmTask* tasks, 
   if (ntiles <= 0) return hipSuccess;
   const GrowthArgs ga{info, growth, piv_tol};
   const bool trsm = info != nullptr;
-  if (tile == 138 && trsm) k_gemm128_mfma6<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  if (tile == 130 && trsm) k_gemm128_mfma2<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  else if (tile == 130) k_gemm128_mfma2<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  else if (tile == 138 && trsm) k_gemm128_mfma6<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 138) k_gemm128_mfma6<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 129 && trsm) k_gemm128_mfma<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 129) k_gemm128_mfma<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
