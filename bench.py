@@ -38,80 +38,163 @@ def _fit_power(xs, ts):
     return float(np.exp(la)), float(alpha)
 
 
-def cpu_baseline(N_head, upd_head, nnz_head, ordering, grid_hint, samples=(24, 32, 40)):
-    """CPU baselines on the GPU box's host, reported beside the GPU number:
+def cpu_threads():
+    """Host threads for the CPU baseline: OMP_NUM_THREADS when set (the GPU box sets it to its CPU
+    share, 16), else every core this process may run on."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(env))) if env and env.isdigit() else aff
 
-    * value: the oracle (scalar C port of the reference's numeric LU, fixed pivots, 1 core as
-      the reference's UMFPACK path runs) timed on 3D Poisson 24^3, 32^3 and 40^3 with the same
-      ordering algorithm; log(time) fitted linearly in log(upd) (upd = sum_k |L_k||U_k|, exact
-      from each plan) and EXTRAPOLATED to the headline config's upd -> seconds and nnz(L+U)/s
-      of one headline refactor on one core.  A full C3 run would take hours.
-    * superlu: scipy's SuperLU (splu, MMD on A'+A, diag_pivot_thresh 0.1: UMFPACK-like symmetric
-      strategy) as the third-party anchor: timed at C2 (2D Poisson 512^2) and at the same 3D
-      samples, extrapolated to the headline n with its own fitted exponent.
-    * throughput_16_independent: 16 concurrent oracle factorizations of the 32^3 sample (one
-      per core of the box's CPU share; NOT a parallel factorization of one matrix)."""
+
+def cpu_baseline(N_head, flops_head, nnz_head, grid_hint, samples=(48, 64, 80)):
+    """CPU baseline on the GPU box's host, reported beside the GPU number:
+
+    * value: the multifrontal CPU port (oracle/mf.c: the same assembly tree as the GPU plan,
+      threshold partial pivoting inside every front, AVX2 register-blocked updates, OpenMP tasks
+      over the assembly tree and inside the large fronts) factoring ONE matrix on all host threads
+      (`cores`), timed on 3D Poisson 48^3 / 64^3 / 80^3 with the GPU's ordering; log(time) fitted
+      in log(dense flops of the plan) and extrapolated to the headline 128^3 (17x the 80^3 sample's
+      flops).  The reference's own path (UMFPACK through Julia) does not exist on the box.
+    * single_core: the same port on one thread at 40^3 (the reference's UMFPACK runs single-threaded).
+    * superlu: scipy's SuperLU (splu, MMD on A'+A, diag_pivot_thresh 0.1) at C2, a third-party anchor.
+    * c1_chunked_solve: the reference's own dense-chunk solve (oracle.ChunkedSolve, a line-by-line
+      restatement of get_chunking_parameters / fill_chunks! / lsolve! / rsolve!, :101-392) at C1."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     import scipy.sparse.linalg as spla
     import smlu
     from smlu import matrices as mats
-    rows, lu_t, lu_n = [], [], []
-    keep = None
-    for N in samples:
+    threads = cpu_threads()
+
+    def mf_time(N, th):
         A = mats.poisson3d(N)
+        A.sort_indices()
         P = smlu.Plan(A, grid=(N,) * 3 if grid_hint else None)
-        q = P.q()
-        Rs = O.rowscale(A)
+        first, parent, rowptr, rows, p0 = P.fronts()
+        fr = dict(first=first, parent=parent, rowptr=rowptr, rows=rows, p0=p0)
+        mf = O.MultifrontalOracle(A, P.q(), fr, None, threads=th)
+        st = mf.factor(A.data)   # first factorization untimed: page faults of the factor store and heap
         t0 = time.perf_counter()
-        F = O.OracleLU(A, q, q, Rs)
+        st = mf.factor(A.data)   # the timed refactor (same pattern, as lu!)
         dt = time.perf_counter() - t0
-        nnz = F.L.nnz + F.U.nnz - A.shape[0]
-        rows.append({"N": N, "seconds": dt, "upd": P.stat("upd"), "nnzLU": nnz,
-                     "nnzLU_per_s": nnz / dt, "gflops": 2 * P.stat("upd") / dt / 1e9})
-        t0 = time.perf_counter()
-        lu = spla.splu(A.tocsc(), permc_spec="MMD_AT_PLUS_A", diag_pivot_thresh=0.1)
-        lu_t.append(time.perf_counter() - t0)
-        lu_n.append({"N": N, "seconds": lu_t[-1], "nnzLU": int(lu.L.nnz + lu.U.nnz - A.shape[0])})
-        if N == 32:
-            keep = (A, q, Rs, nnz)
-        log(f"cpu baseline sample {N}^3: oracle {dt:.2f} s, superlu {lu_t[-1]:.2f} s")
-    a, alpha = _fit_power([r["upd"] for r in rows], [r["seconds"] for r in rows])
-    t_head = a * upd_head ** alpha
-    res = {"value": nnz_head / t_head, "unit": "nnz(L+U)/s", "cores": 1, "kind": "port",
-           "sample": (f"oracle (fixed-pivot Gilbert-Peierls LU, scalar C, 1 core) on 3D Poisson "
-                      f"{'/'.join(f'{N}^3' for N in samples)} ({ordering} order); time fitted as "
-                      f"{a:.3g} * upd^{alpha:.3f} and extrapolated to {N_head}^3 (upd={upd_head:.4g}): "
-                      f"{t_head:.0f} s per refactor"),
-           "extrapolated": True, "headline_seconds": t_head, "fit": {"a": a, "alpha": alpha},
-           "samples": rows}
-    # SuperLU anchor: C2 measured; headline n extrapolated from the 3D samples (t ~ n^beta)
+        mf.close()
+        assert st == 0
+        return {"N": N, "seconds": dt, "dense_flops": P.stat("dense_flops"), "upd": P.stat("upd"),
+                "nnzLU": P.stat("nnzLU"), "nnzLU_per_s": P.stat("nnzLU") / dt,
+                "gflops": P.stat("dense_flops") / dt / 1e9}
+
+    rows = []
+    for N in samples:
+        rows.append(mf_time(N, threads))
+        log(f"cpu baseline {N}^3 on {threads} threads: {rows[-1]['seconds']:.2f} s, "
+            f"{rows[-1]['gflops']:.1f} GFLOP/s")
+    a, alpha = _fit_power([r["dense_flops"] for r in rows], [r["seconds"] for r in rows])
+    t_head = a * flops_head ** alpha
+    res = {"value": nnz_head / t_head, "unit": "nnz(L+U)/s", "cores": threads, "kind": "port",
+           "nproc": os.cpu_count(),
+           "sample": (f"multifrontal CPU port (oracle/mf.c, same plan, partial pivoting, OpenMP on "
+                      f"{threads} threads, AVX2) on 3D Poisson {'/'.join(f'{N}^3' for N in samples)}; "
+                      f"time fitted as {a:.3g} * flops^{alpha:.3f} and extrapolated to {N_head}^3 "
+                      f"({flops_head / rows[-1]['dense_flops']:.1f}x the largest sample's flops): "
+                      f"{t_head:.1f} s per refactor"),
+           "extrapolated": True, "extrapolation_factor": flops_head / rows[-1]["dense_flops"],
+           "headline_seconds": t_head, "fit": {"a": a, "alpha": alpha}, "samples": rows}
+    one = mf_time(40, 1)
+    res["single_core"] = dict(one, cores=1)
+    log(f"cpu baseline 40^3 on 1 thread: {one['seconds']:.2f} s")
     A2 = mats.poisson2d(512)
     t0 = time.perf_counter()
     lu = spla.splu(A2.tocsc(), permc_spec="MMD_AT_PLUS_A", diag_pivot_thresh=0.1)
     t_c2 = time.perf_counter() - t0
-    b, beta = _fit_power([N ** 3 for N in samples], lu_t)
-    t_sl = b * float(N_head ** 3) ** beta
-    res["superlu"] = {"kind": "third-party", "cores": 1,
-                      "c2_poisson2d_512_seconds": t_c2, "c2_nnzLU": int(lu.L.nnz + lu.U.nnz - A2.shape[0]),
-                      "c2_nnzLU_per_s": (lu.L.nnz + lu.U.nnz - A2.shape[0]) / t_c2,
-                      "samples_3d": lu_n, "fit": {"b": b, "beta": beta},
-                      "headline_seconds_extrapolated": t_sl,
-                      "note": "scipy.sparse.linalg.splu (SuperLU), MMD on A'+A, diag_pivot_thresh 0.1; "
-                              "its own ordering and fill, so nnz(L+U) differs from the GPU plan's"}
-    # 16 independent copies of the 32^3 sample at once (the C oracle releases the GIL)
-    from concurrent.futures import ThreadPoolExecutor
-    A, q, Rs, nnz = keep
-    C = max(1, min(16, os.cpu_count() or 1))
+    res["superlu"] = {"kind": "third-party", "cores": 1, "c2_poisson2d_512_seconds": t_c2,
+                      "c2_nnzLU": int(lu.L.nnz + lu.U.nnz - A2.shape[0]),
+                      "note": "scipy.sparse.linalg.splu (SuperLU), MMD on A'+A, diag_pivot_thresh 0.1"}
+    # C1: the reference's chunked solve, restated verbatim, on its own CPU layout
+    A1 = mats.random_dominant(1000, 0.01, seed=47)
+    q1 = smlu.Plan(A1).q()   # the GPU plan's column order; diagonal pivots (row-dominant C1)
+    ref = O.OracleLU(A1, q1, q1)
+    cs = O.ChunkedSolve(ref.L, ref.U)
+    b1 = np.random.default_rng(3).random(A1.shape[0])
+    reps = 20
     t0 = time.perf_counter()
-    with ThreadPoolExecutor(C) as ex:
-        list(ex.map(lambda _: O.OracleLU(A, q, q, Rs), range(C)))
-    dtc = time.perf_counter() - t0
-    res["throughput_16_independent"] = {
-        "value": C * nnz / dtc, "unit": "nnz(L+U)/s", "cores": C, "kind": "port",
-        "sample": f"{C} independent oracle factorizations of the 32^3 sample running concurrently "
-                  f"({dtc:.2f} s): aggregate throughput over {C} problems, not one parallel factorization"}
+    for _ in range(reps):
+        w = ref.Rs * b1
+        cs.lsolve(w)
+        cs.rsolve(w)
+    res["c1_chunked_solve"] = {"ms_per_solve": (time.perf_counter() - t0) / reps * 1e3, "cores": 1,
+                               "chunks": cs.total_chunks,
+                               "note": "oracle.ChunkedSolve: trsv on 8x8 diagonal chunks + gemv on the "
+                                       "negated dense rectangles (src/SharedMemSparseLU.jl:349-392)"}
     return res
+
+
+def gpu_configs(dev):
+    """The BASELINE configs besides the headline, on this GPU (reported, not the metric):
+    C1 factorize + solve (1000x1000 random 1 %); C2 factorize + solve (2D 5-point Poisson 512^2);
+    C5 steady state: 1000 numeric refactorizations of C2 with new values (8 value sets cycled,
+    resident in HBM), the solution checked after the last one."""
+    import torch
+    import smlu
+    from smlu import matrices as mats
+    out = {}
+    A1 = mats.random_dominant(1000, 0.01, seed=47)
+    t0 = time.perf_counter()
+    F1 = smlu.ParallelSparseLU(A1, device=dev.index)
+    c1_create = time.perf_counter() - t0
+    b1 = np.random.default_rng(3).random(A1.shape[0])
+    x1 = np.empty_like(b1)
+    smlu.ldiv_(x1, F1, b1)
+    t0 = time.perf_counter()
+    for _ in range(20):
+        smlu.ldiv_(x1, F1, b1)
+    out["c1"] = {"create_s": c1_create, "solve_ms_host_vectors": (time.perf_counter() - t0) / 20 * 1e3,
+                 "residual": float(np.abs(A1 @ x1 - b1).max() / np.abs(b1).max()), "nnzLU": F1.stat("nnzLU")}
+    F1.close()
+    A2 = mats.poisson2d(512)
+    n2 = A2.shape[0]
+    t0 = time.perf_counter()
+    F2 = smlu.ParallelSparseLU(A2, device=dev.index)
+    c2_create = time.perf_counter() - t0
+    dpos = torch.from_numpy(mats.diag_positions(A2)).to(dev)
+    base = torch.from_numpy(np.ascontiguousarray(A2.data)).to(dev)
+    vals = []
+    for r in range(8):
+        v = base.clone()
+        v[dpos] += torch.from_numpy(np.random.default_rng(100 + r).random(n2)).to(dev)
+        vals.append(v)
+    b = torch.from_numpy(np.random.default_rng(5).random(n2)).to(dev)
+    x = torch.empty_like(b)
+    F2.refactor_device(vals[0])
+    F2.solve_device(x, b)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    F2.refactor_device(vals[1])
+    torch.cuda.synchronize()
+    t_ref = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    F2.solve_device(x, b)
+    torch.cuda.synchronize()
+    t_sol = time.perf_counter() - t0
+    R = 1000
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for r in range(R):
+        F2.refactor_device(vals[r % 8])
+    torch.cuda.synchronize()
+    t_ss = time.perf_counter() - t0
+    F2.solve_device(x, b)
+    Al = A2.copy()
+    Al.data = vals[(R - 1) % 8].cpu().numpy()
+    xh, bh = x.cpu().numpy(), b.cpu().numpy()
+    nnz2 = F2.stat("nnzLU")
+    out["c2"] = {"create_s": c2_create, "refactor_ms": t_ref * 1e3, "solve_ms": t_sol * 1e3,
+                 "factorize_plus_solve_ms": (t_ref + t_sol) * 1e3, "nnzLU": nnz2,
+                 "nnzLU_per_s": nnz2 / t_ref}
+    out["c5_steady_state_c2"] = {"refactors": R, "seconds": t_ss, "ms_per_refactor": t_ss / R * 1e3,
+                                 "nnzLU_per_s": nnz2 * R / t_ss,
+                                 "residual_after": float(np.abs(Al @ xh - bh).max() / np.abs(bh).max())}
+    F2.close()
+    return out
 
 
 def ordering_compare(N):
@@ -185,6 +268,7 @@ def main():
                     help="grid side of the 3D Poisson workload")
     ap.add_argument("--ordering", default="nd", choices=["nd", "geometric"])
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the C1/C2/C5 side measurements")
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--test-one-gpu", action="store_true",
                     help="rehearsal: all ranks on cuda:0, gloo transport (never for measurements)")
@@ -371,7 +455,10 @@ def main():
             log("ordering comparison (host symbolic analysis) ...")
             res["config"]["ordering_compare"] = ordering_compare(N)
             log("cpu baseline ...")
-            res["cpu_baseline"] = cpu_baseline(N, upd, nnzLU, args.ordering, args.ordering == "geometric")
+            res["cpu_baseline"] = cpu_baseline(N, dense_flops, nnzLU, args.ordering == "geometric")
+        if not args.no_configs and world == 1:
+            log("configs C1 / C2 / C5 steady state ...")
+            res["configs"] = gpu_configs(dev)
         print(json.dumps(res), flush=True)
     F.close()
     if world > 1:

@@ -32,6 +32,7 @@
  */
 #include "oracle.h"
 
+#include <malloc.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -57,6 +58,7 @@ struct oracle_mf {
   int64_t *colptr, *rowval;     /* pattern copy (row scaling) */
   double diag_tol, piv_tol;
   int nthreads;
+  double* work;                 /* flops of each front's subtree (task cut-off) */
 };
 
 static int64_t ns_of(const oracle_mf* h, int64_t s) { return h->first[s + 1] - h->first[s]; }
@@ -84,7 +86,7 @@ void oracle_mf_destroy(oracle_mf* h) {
   if (h->f22)
     for (int64_t s = 0; s < h->nsup; ++s) free(h->f22[s]);
   free(h->f22); free(h->Rs); free(h->rowperm); free(h->flags);
-  free(h->colptr); free(h->rowval);
+  free(h->colptr); free(h->rowval); free(h->work);
   free(h);
 }
 
@@ -95,6 +97,10 @@ oracle_mf* oracle_mf_create(int64_t n, const int64_t* colptr, const int64_t* row
                             const int64_t* rowptr, const int64_t* rows, const int32_t* mode,
                             double diag_tol, double piv_tol, int nthreads, int* status) {
   *status = 0;
+  /* front and contribution blocks are allocated and freed per factorization: keep them on the
+   * heap (no mmap/munmap and page faults per front once the heap has grown) */
+  mallopt(M_MMAP_THRESHOLD, 1 << 30);
+  mallopt(M_TRIM_THRESHOLD, 1 << 30);
   oracle_mf* h = calloc(1, sizeof(oracle_mf));
   int64_t *p0inv = NULL, *qinv = NULL, *col2s = NULL, *cnt = NULL, *efront = NULL;
   if (!h) { *status = -3; return NULL; }
@@ -194,6 +200,12 @@ oracle_mf* oracle_mf_create(int64_t n, const int64_t* colptr, const int64_t* row
     }
     ALLOC(h->store, off);
   }
+  ALLOC(h->work, nsup);
+  for (int64_t s = 0; s < nsup; ++s) {   /* children precede parents */
+    const double ns = (double)ns_of(h, s), M = ns + (double)nu_of(h, s);
+    h->work[s] += 2.0 * M * M * ns;
+    if (parent[s] >= 0) h->work[parent[s]] += h->work[s];
+  }
   ALLOC(h->f22, nsup); ALLOC(h->Rs, n); ALLOC(h->rowperm, n); ALLOC(h->flags, nsup);
   free(p0inv); free(qinv); free(col2s); free(cnt); free(efront);
   return h;
@@ -204,37 +216,71 @@ fail:
   return NULL;
 }
 
-/* C[m x n] -= A[m x k] * B[k x n], column-major; threaded over column blocks when par != 0 */
+typedef double v4d __attribute__((vector_size(32)));   /* AVX2 (x86-64-v3) */
+
+static inline v4d ldu4(const double* p) {
+  v4d v;
+  memcpy(&v, p, sizeof v);
+  return v;
+}
+static inline void stu4(double* p, v4d v) { memcpy(p, &v, sizeof v); }
+
+/* 8 x 4 register block of C -= A * B over k0..k1 (A column-major: 8 contiguous rows). */
+static inline void micro_8x4(int64_t kk, const double* A, int64_t lda, const double* B, int64_t ldb, double* C,
+                             int64_t ldc) {
+  v4d c00 = ldu4(C), c01 = ldu4(C + 4);
+  v4d c10 = ldu4(C + ldc), c11 = ldu4(C + ldc + 4);
+  v4d c20 = ldu4(C + 2 * ldc), c21 = ldu4(C + 2 * ldc + 4);
+  v4d c30 = ldu4(C + 3 * ldc), c31 = ldu4(C + 3 * ldc + 4);
+  for (int64_t k = 0; k < kk; ++k) {
+    const v4d a0 = ldu4(A + k * lda), a1 = ldu4(A + k * lda + 4);
+    const double* b = B + k;
+    const v4d b0 = {b[0], b[0], b[0], b[0]};
+    const v4d b1 = {b[ldb], b[ldb], b[ldb], b[ldb]};
+    const v4d b2 = {b[2 * ldb], b[2 * ldb], b[2 * ldb], b[2 * ldb]};
+    const v4d b3 = {b[3 * ldb], b[3 * ldb], b[3 * ldb], b[3 * ldb]};
+    c00 -= a0 * b0; c01 -= a1 * b0;
+    c10 -= a0 * b1; c11 -= a1 * b1;
+    c20 -= a0 * b2; c21 -= a1 * b2;
+    c30 -= a0 * b3; c31 -= a1 * b3;
+  }
+  stu4(C, c00); stu4(C + 4, c01);
+  stu4(C + ldc, c10); stu4(C + ldc + 4, c11);
+  stu4(C + 2 * ldc, c20); stu4(C + 2 * ldc + 4, c21);
+  stu4(C + 3 * ldc, c30); stu4(C + 3 * ldc + 4, c31);
+}
+
+/* C[m x n] -= A[m x k] * B[k x n], column-major: 8 x 4 register blocks (AVX2 FMA) over k blocks
+ * of 256 and row blocks of 96 (the A block stays in L2, its 8-row slice in L1 across the
+ * column steps); the column blocks are OpenMP tasks when par != 0. */
 static void gemm_sub(int64_t m, int64_t n, int64_t k, const double* A, int64_t lda, const double* B,
                      int64_t ldb, double* C, int64_t ldc, int par) {
   if (m <= 0 || n <= 0 || k <= 0) return;
-  const int64_t MB = 192, KB = 128, NB = 32;
+  const int64_t MB = 96, KB = 256, NB = 64;
   const int64_t nbn = (n + NB - 1) / NB;
-#pragma omp parallel for schedule(dynamic) if (par)
+#pragma omp taskloop grainsize(1) if (par && nbn > 1)
   for (int64_t jb = 0; jb < nbn; ++jb) {
     const int64_t j0 = jb * NB, j1 = j0 + NB < n ? j0 + NB : n;
     for (int64_t k0 = 0; k0 < k; k0 += KB) {
-      const int64_t k1 = k0 + KB < k ? k0 + KB : k;
+      const int64_t k1 = k0 + KB < k ? k0 + KB : k, kk = k1 - k0;
       for (int64_t i0 = 0; i0 < m; i0 += MB) {
         const int64_t i1 = i0 + MB < m ? i0 + MB : m;
-        for (int64_t j = j0; j < j1; ++j) {
-          double* c = C + j * ldc;
-          int64_t kk = k0;
-          for (; kk + 4 <= k1; kk += 4) {   /* four rank-1 updates per pass over the column */
-            const double b0 = B[j * ldb + kk], b1 = B[j * ldb + kk + 1];
-            const double b2 = B[j * ldb + kk + 2], b3 = B[j * ldb + kk + 3];
-            const double* a0 = A + kk * lda;
-            const double* a1 = a0 + lda;
-            const double* a2 = a1 + lda;
-            const double* a3 = a2 + lda;
-            for (int64_t i = i0; i < i1; ++i) c[i] -= a0[i] * b0 + a1[i] * b1 + a2[i] * b2 + a3[i] * b3;
-          }
-          for (; kk < k1; ++kk) {
-            const double b = B[j * ldb + kk];
-            const double* a = A + kk * lda;
-            for (int64_t i = i0; i < i1; ++i) c[i] -= a[i] * b;
-          }
+        const int64_t i8 = i0 + ((i1 - i0) / 8) * 8;
+        int64_t j = j0;
+        for (; j + 4 <= j1; j += 4) {
+          for (int64_t i = i0; i < i8; i += 8)
+            micro_8x4(kk, A + i + k0 * lda, lda, B + k0 + j * ldb, ldb, C + i + j * ldc, ldc);
+          for (int64_t jj = j; jj < j + 4; ++jj)     /* leftover rows */
+            for (int64_t kq = k0; kq < k1; ++kq) {
+              const double b = B[jj * ldb + kq];
+              for (int64_t i = i8; i < i1; ++i) C[jj * ldc + i] -= A[kq * lda + i] * b;
+            }
         }
+        for (; j < j1; ++j)                           /* leftover columns */
+          for (int64_t kq = k0; kq < k1; ++kq) {
+            const double b = B[j * ldb + kq];
+            for (int64_t i = i0; i < i1; ++i) C[j * ldc + i] -= A[kq * lda + i] * b;
+          }
       }
     }
   }
@@ -302,7 +348,7 @@ static int factor_front(double* W, int64_t M, int64_t ns, int mode, double diag_
     if (ke >= M) continue;
     /* U12 rows of the panel: L11^{-1} W[kb:ke, ke:M] (unit lower), then the trailing update */
     const int64_t w = ke - kb, nr = M - ke;
-#pragma omp parallel for schedule(static) if (par && nr > 256)
+#pragma omp taskloop grainsize(64) if (par && nr > 256)
     for (int64_t j = ke; j < M; ++j) {
       double* cj = W + j * M;
       for (int64_t k = kb; k < ke; ++k) {
@@ -351,25 +397,38 @@ static int do_front(oracle_mf* h, const double* nzval, int64_t s, int par) {
   return 0;
 }
 
-/* One numeric factorization (row scaling + every front, level by level).  Returns 0, or 1 when
- * some front flagged a zero candidate column, negative on allocation failure. */
+/* Front s after its children: the assembly tree as OpenMP tasks (children in parallel, the
+ * front when all of them are done); fronts with enough work also split their updates into
+ * tasks (taskloop over column blocks). */
+static void front_task(oracle_mf* h, const double* nzval, int64_t s, int* err) {
+  for (int64_t c = h->chptr[s]; c < h->chptr[s + 1]; ++c) {
+    const int64_t ch = h->chlist[c];
+#pragma omp task firstprivate(ch) shared(err) if (h->nthreads > 1 && h->work[ch] > 2e6)
+    front_task(h, nzval, ch, err);
+  }
+#pragma omp taskwait
+  const int64_t ns = ns_of(h, s), M = ns + nu_of(h, s);
+  const int r = do_front(h, nzval, s, h->nthreads > 1 && (double)M * M * ns > 5e7);
+  if (r) {
+#pragma omp atomic write
+    *err = 1;
+  }
+}
+
+/* One numeric factorization (row scaling + every front).  Returns 0, or 1 when some front
+ * flagged a zero candidate column, negative on allocation failure. */
 int oracle_mf_factor(oracle_mf* h, const double* nzval) {
   oracle_rowscale(h->n, h->colptr, h->rowval, nzval, h->Rs);
   int err = 0;
-#ifdef _OPENMP
-  omp_set_max_active_levels(1);
-#endif
-  for (int64_t l = 0; l < h->nlev; ++l) {
-    const int64_t a = h->levptr[l], b = h->levptr[l + 1];
-    if (b - a >= 2 * h->nthreads) {   /* many fronts: one thread per front */
-#pragma omp parallel for schedule(dynamic) num_threads(h->nthreads) reduction(| : err)
-      for (int64_t t = a; t < b; ++t) err |= do_front(h, nzval, h->levlist[t], 0) != 0;
-    } else {                          /* few (large) fronts: threads inside each front */
-#ifdef _OPENMP
-      omp_set_num_threads(h->nthreads);
-#endif
-      for (int64_t t = a; t < b; ++t) err |= do_front(h, nzval, h->levlist[t], h->nthreads > 1) != 0;
-    }
+#pragma omp parallel num_threads(h->nthreads)
+#pragma omp single
+  {
+    for (int64_t s = 0; s < h->nsup; ++s)
+      if (h->parent[s] < 0) {
+#pragma omp task firstprivate(s) shared(err)
+        front_task(h, nzval, s, &err);
+      }
+#pragma omp taskwait
   }
   if (err) return -3;
   for (int64_t s = 0; s < h->nsup; ++s) {
