@@ -489,6 +489,156 @@ void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step, const SNod
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Sync-free triangular sweep of the large fronts of one level (one launch per level and direction,
+// replacing one launch per 64-column block).  Work item = a chunk of 256 rows (forward: rows
+// [256q, 256q+256) of the front; backward: the pivot blocks nblk-1-4q-t, t < 4); one workgroup,
+// one thread per row.  A chunk applies the column blocks solved by earlier chunks of its front as
+// their flags appear, then runs its own (up to four) diagonal blocks in sequence inside the
+// workgroup -- wave t solves block 4q+t (the 64-step readlane chain of tri64_row), the waves below
+// apply it -- and publishes each solved block: x values by write-through (sc1) stores, the
+// storing wave's vmcnt drained, a workgroup barrier, then one sc1 flag store; consumers poll the
+// flag with sc1 loads and read the x values with sc1 loads (MI355X_MICROARCH.md, hand-off form
+// "one lane of each storing workgroup").  Deadlock-free by tickets: work items are taken in ticket
+// order (atomic counter), and an item only waits on items of lower tickets, which are running.
+// Per right-hand side the arithmetic does not depend on the batch width (batched == single).
+// sync: this launch's ticket counter at sync[0], flags of front f at sync[1 + pad_f + block];
+// zeroed before every solve.  status: set to 1 if a wait ever times out (never expected).
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ void sweep_wait(int32_t* f, int32_t* status) {
+  if (threadIdx.x == 0) {
+    int n = 0;
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++n > (1 << 22)) {
+        __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave per SIMD: the preloaded diagonal row and the tile row are 128 VGPRs each.
+template <bool UPPER, int NR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, int32_t* __restrict__ sync, int32_t* __restrict__ status,
+                 const SNode* __restrict__ sn, const double* __restrict__ store, double* __restrict__ x,
+                 double* __restrict__ vbuf, Rhs rh) {
+  __shared__ double xs[64][NR];
+  __shared__ int64_t s_item;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) s_item = atomicAdd(&sync[0], 1);
+  __syncthreads();
+  const int64_t item = s_item;
+  const int fi = find_front_tile(ft, nft, item);
+  const SNode s = sn[ft[fi].s];
+  int32_t* flags = sync + 1 + ft[fi].pad;
+  const int64_t q = item - ft[fi].wg0;
+  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns, nblk = (ns + 63) / 64;
+  const double* Lp = store + s.Loff;
+  const int nr = NR == 1 ? 1 : rh.n;
+  double* v = vbuf + s.voff;
+  double* xf = x + s.first;
+  // my row; blocks of other chunks (external) and of this chunk (internal, block ids in order)
+  int64_t row, myblk;
+  if (!UPPER) {
+    row = 256 * q + tid;
+    myblk = row < ns ? row / 64 : nblk;
+  } else {
+    myblk = nblk - 1 - 4 * q - wv;
+    row = 64 * myblk + lane;
+  }
+  const bool has = UPPER ? (myblk >= 0 && row < ns) : row < M;
+  double o[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) o[r] = (has && r < nr) ? v[r * rh.ldv + row] : 0.0;
+  // the diagonal block's row of a pivot row, loaded up front (off the chain's critical path); in
+  // the forward sweep the update rows sharing a wave with the last (partial) pivot block take
+  // that block's columns in the chain too
+  double drow[64];
+  double dinv = 1.0;
+  {
+    const int64_t b = UPPER ? myblk : row / 64;
+    const bool inb = has && b < nblk;
+    const int bw = (int)min<int64_t>(64, ns - 64 * (inb ? b : 0));
+    const int li = (int)(row - 64 * b);
+#pragma unroll
+    for (int j = 0; j < 64; ++j)
+      drow[j] = (inb && j < bw && (UPPER ? j > li : j < li)) ? Lp[(64 * b + j) * M + row] : 0.0;
+    if (UPPER && inb) dinv = recip(Lp[(64 * b + li) * M + row]);
+  }
+  double d[64];   // my row of the column block being applied, loaded before its x is available
+  auto load_tile = [&](int64_t c, int bw) {
+#pragma unroll
+    for (int j = 0; j < 64; ++j) d[j] = j < bw ? Lp[(64 * c + j) * M + row] : 0.0;
+  };
+  auto fma_tile = [&](int bw) {   // o -= L[row, block] * x_block (x in xs)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      if (r < nr) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < 64; ++j)
+          if (j < bw) acc = fma(d[j], xs[j][r], acc);
+        o[r] -= acc;
+      }
+    }
+  };
+  // external blocks (solved by earlier chunks): forward 0 .. min(4q, nblk)-1, backward nblk-1
+  // down to nblk-4q; every row of this chunk lies beyond them
+  const int64_t next = min<int64_t>(4 * q, nblk);
+  for (int64_t e = 0; e < next; ++e) {
+    const int64_t c = UPPER ? nblk - 1 - e : e;
+    const int bw = (int)min<int64_t>(64, ns - 64 * c);
+    if (has) load_tile(c, bw);
+    sweep_wait(flags + c, status);
+    if (wv == 0 && lane < bw)
+      for (int r = 0; r < nr; ++r) xs[lane][r] = ld_sc1(xf + r * rh.ldx + 64 * c + lane);
+    __syncthreads();
+    if (has) fma_tile(bw);
+    __syncthreads();
+  }
+  // internal blocks: wave t solves block b and publishes it, the waves beyond apply it
+  for (int t = 0; t < 4; ++t) {
+    const int64_t b = UPPER ? nblk - 1 - 4 * q - t : 4 * q + t;
+    if (b < 0 || b >= nblk) break;
+    const int bw = (int)min<int64_t>(64, ns - 64 * b);
+    if (wv > t && has) load_tile(b, bw);
+    if (wv == t) {
+#pragma unroll
+      for (int r = 0; r < NR; ++r) {
+        if (r < nr) {
+          const double y = tri64_row<UPPER>(o[r], drow, dinv, bw, lane);
+          o[r] = y;
+          if (lane < bw && has) {
+            xs[lane][r] = y;
+            st_sc1(xf + r * rh.ldx + 64 * b + lane, y);
+            v[r * rh.ldv + 64 * b + lane] = y;
+          }
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(flags + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wv > t && has) fma_tile(bw);
+    __syncthreads();
+  }
+  // forward: the update rows leave their value for the parent
+  if (!UPPER && has && myblk >= nblk) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+      if (r < nr) v[r * rh.ldv + row] = o[r];
+  }
+}
+
 // x_s[i] (in v) = x[first+i] - sum_j U12[i,j] * x[R_j]: 64 rows per workgroup, 8 waves; wave w
 // sums the columns [w*nu/8, (w+1)*nu/8) 32 at a time, the 32 U12 loads of a chunk issued
 // together (8 waves x 32 x 512 B in flight per workgroup), x[R] staged per chunk in LDS; the
@@ -766,6 +916,19 @@ hipError_t launch_bwd_u12(hipStream_t st, int64_t nwg, const FrontTile* ft, int 
   else if (rh.n <= 4) k_bwd_u12<4><<<(unsigned)nwg, 512, 0, st>>>(ft, nft, sn, rows, store, x, vbuf, rh);
   else if (rh.n <= 8) k_bwd_u12<8><<<(unsigned)nwg, 512, 0, st>>>(ft, nft, sn, rows, store, x, vbuf, rh);
   else k_bwd_u12<16><<<(unsigned)nwg, 512, 0, st>>>(ft, nft, sn, rows, store, x, vbuf, rh);
+  return hipGetLastError();
+}
+hipError_t launch_tri_sweep(hipStream_t st, bool upper, int64_t nwg, const FrontTile* ft, int nft, int32_t* sync,
+                            int32_t* status, const SNode* sn, const double* store, double* x, double* vbuf, Rhs rh) {
+  if (nwg <= 0) return hipSuccess;
+#define SWEEP(NR)                                                                                             \
+  (upper ? (k_tri_sweep<true, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sync, status, sn, store, x, vbuf, rh)) \
+         : (k_tri_sweep<false, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sync, status, sn, store, x, vbuf, rh)))
+  if (rh.n <= 1) SWEEP(1);
+  else if (rh.n <= 4) SWEEP(4);
+  else if (rh.n <= 8) SWEEP(8);
+  else SWEEP(16);
+#undef SWEEP
   return hipGetLastError();
 }
 hipError_t launch_residual(hipStream_t st, int64_t n, const int64_t* rowptr, const int32_t* ent,

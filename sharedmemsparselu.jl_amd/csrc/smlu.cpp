@@ -59,6 +59,8 @@ hipError_t launch_tri_block(hipStream_t, bool, int64_t, const FrontTile*, int, i
                             const double*, double*, double*, Rhs);
 hipError_t launch_bwd_u12(hipStream_t, int64_t, const FrontTile*, int, const SNode*, const int32_t*,
                           const double*, const double*, double*, Rhs);
+hipError_t launch_tri_sweep(hipStream_t, bool, int64_t, const FrontTile*, int, int32_t*, int32_t*, const SNode*,
+                            const double*, double*, double*, Rhs);
 hipError_t launch_fwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                       const int32_t*, const double*, double*, double*, Rhs);
 hipError_t launch_bwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*,
@@ -96,12 +98,12 @@ thread_local std::string g_last_error;
 enum Kind : int {
   K_MEMSET_STORE, K_MEMSET_SCRATCH, K_SCATTER, K_EXTADD, K_FRONT_LDS, K_PANEL, K_TRSMU, K_TRSML,
   K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_GEMM22, K_LASWP, K_STEPTRSM, K_GEMMU,
-  K_GEMMO, K_FORK, K_JOIN, K_TRIINV, K_BWDU12C, K_VCOPY, K_FWDT, K_BWDT, K_NKIND
+  K_GEMMO, K_FORK, K_JOIN, K_TRIINV, K_BWDU12C, K_VCOPY, K_FWDT, K_BWDT, K_SWEEPF, K_SWEEPB, K_NKIND
 };
 const char* kKindName[K_NKIND] = {"memset", "memset", "assemble", "assemble", "small", "panel",
                                   "trsm", "trsm", "gemm", "solve", "solve", "solve", "solve",
                                   "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "sync", "sync", "trsm", "solve", "solve",
-                                  "solve", "solve"};
+                                  "solve", "solve", "solve", "solve"};
 constexpr int kSolveBigNs = 256;  // fronts with more pivots use the multi-workgroup solve
 // ... and so do fronts whose L panel (M x ns entries) exceeds this: one workgroup streams a
 // tall panel at single-CU bandwidth (a 10^4-row front with 200 pivots took ~350 us per sweep)
@@ -348,6 +350,8 @@ struct smlu_handle {
   DBuf<XContrib> xtasks;
   DBuf<int2> aents;
   DBuf<FrontTile> ftiles;
+  DBuf<int32_t> ssync, sstatus;   // sync-free solve sweeps: tickets + block flags (zeroed per solve); timeouts
+  int64_t ssync_n = 0;
   DBuf<GemmTask> gtasks;
   DBuf<SwapTask> stasks;
   DBuf<XCol> xcols;
@@ -439,6 +443,8 @@ struct smlu_handle {
     xtasks.free();
     aents.free();
     ftiles.free();
+    ssync.free();
+    sstatus.free();
     gtasks.free();
     stasks.free();
     xcols.free();
@@ -1654,6 +1660,10 @@ static int build_schedule(smlu_handle* h) {
   };
   auto holder = [&](int64_t c) { return P.dist(c) ? P.blk_owner(c, P.npblk(c) - 1) : P.owner[c]; };
   static const bool no_tiny = std::getenv("SMLU_NO_TINY_SOLVE") != nullptr;   // dev knob
+  // large fronts: one sync-free sweep launch per level and direction (default) or one launch per
+  // 64-column block (SMLU_SOLVE_STEPS=1, the previous schedule)
+  static const bool sweep_solve = !(std::getenv("SMLU_SOLVE_STEPS") && std::atoi(std::getenv("SMLU_SOLVE_STEPS")) == 1);
+  int64_t ssync_n = 1;   // [0] unused
   static const int64_t big_work = [] {
     const char* e = std::getenv("SMLU_SOLVE_BIGWORK");   // dev knob (sweeps)
     return e ? std::atoll(e) : kSolveBigWork;
@@ -1708,6 +1718,43 @@ static int build_schedule(smlu_handle* h) {
       }
       U.cnt = (int64_t)bigs.size();
       U.nwg = wg;
+      if (sweep_solve) {   // one sync-free sweep launch per direction (k_tri_sweep)
+        Launch F, B;
+        F.kind = K_SWEEPF;
+        B.kind = K_SWEEPB;
+        F.off = (int64_t)ft.size();
+        F.aux = ssync_n;
+        int64_t wf = 0;
+        int32_t fb = 0;
+        for (auto s : bigs) {
+          const SNode& r = h->hsn[s];
+          ft.push_back(FrontTile{(int32_t)s, fb, wf});
+          wf += ((int64_t)r.ns + r.nu + 255) / 256;
+          fb += (r.ns + 63) / 64;
+        }
+        F.cnt = (int64_t)bigs.size();
+        F.nwg = wf;
+        ssync_n += 1 + fb;
+        h->fwd.push_back(F);
+        B.off = (int64_t)ft.size();
+        B.aux = ssync_n;
+        int64_t wb = 0;
+        fb = 0;
+        for (auto s : bigs) {
+          const SNode& r = h->hsn[s];
+          const int64_t nbs = (r.ns + 63) / 64;
+          ft.push_back(FrontTile{(int32_t)s, fb, wb});
+          wb += (nbs + 3) / 4;
+          fb += (int32_t)nbs;
+        }
+        B.cnt = (int64_t)bigs.size();
+        B.nwg = wb;
+        ssync_n += 1 + fb;
+        bl.push_back(U);
+        bl.push_back(B);
+        bwd_levels.push_back(bl);
+        goto shared_fronts;
+      }
       std::vector<Launch> bsteps;
       for (int64_t t = 0; t < nb; ++t) {
         Launch F, B;
@@ -1748,6 +1795,7 @@ static int build_schedule(smlu_handle* h) {
       for (auto& b : bsteps) bl.push_back(b);
     }
     bwd_levels.push_back(bl);
+  shared_fronts:
     // forward solve of the shared front: the children's update vectors go to the first block's
     // owner, which gathers the front vector; the vector then follows the pivot blocks' owners
     // (shared fronts of this level, in front order on every rank)
@@ -1980,6 +2028,13 @@ static int build_schedule(smlu_handle* h) {
   HIPCHK(h->xtasks.upload(xt.data(), xt.size(), st));
   HIPCHK(h->aents.upload(ae.data(), ae.size(), st));
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
+  h->ssync_n = ssync_n;
+  HIPCHK(h->ssync.alloc((size_t)ssync_n));
+  HIPCHK(hipMemsetAsync(h->ssync.p, 0, sizeof(int32_t) * ssync_n, st));
+  if (!h->sstatus.p) {
+    HIPCHK(h->sstatus.alloc(1));
+    HIPCHK(hipMemsetAsync(h->sstatus.p, 0, sizeof(int32_t), st));
+  }
   if (h->nranks > 1) max_list = std::max<int64_t>(max_list, dist_slots);
   if (!tinv_patch.empty() || h->nranks > 1) {   // operands in the tile-inverse slots: patch in the buffer address
     HIPCHK(h->tinv.alloc((size_t)max_list * 8192));
@@ -2430,6 +2485,7 @@ static void release_schedule(smlu_handle* h) {
   h->xtasks.free();
   h->aents.free();
   h->ftiles.free();
+  h->ssync.free();
   h->gtasks.free();
   h->stasks.free();
   h->xcols.free();
@@ -2507,6 +2563,10 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, d
     case K_BWDU:
       return launch_bwd_u12(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->sn.p, h->rows.p, h->store.p, w, v,
                             rh);
+    case K_SWEEPF:
+    case K_SWEEPB:
+      return launch_tri_sweep(st, L.kind == K_SWEEPB, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->ssync.p + L.aux,
+                              h->sstatus.p, h->sn.p, h->store.p, w, v, rh);
     case K_BWDU12C:
       return launch_bwd_u12_cols(st, h->sn.p, L.node, h->hsn[L.node].ns, L.aux, L.aux2, (int)L.cnt, h->rows.p,
                                  h->store.p, w, h->vbuf.p);
@@ -2555,6 +2615,9 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
     return (int)SMLU_OK;
   };
   auto sweeps = [&]() {
+    // tickets and block flags of the sync-free sweeps start from zero in every solve
+    if (h->ssync_n > 1 && hipMemsetAsync(h->ssync.p, 0, sizeof(int32_t) * h->ssync_n, st) != hipSuccess)
+      return fail(h, SMLU_ERR_HIP, "memset of the solve sweep flags failed");
     if (mode != 2) {
       int rc = run_seq(h->fwd, h->fwd_seg, h->fwd_comm);
       if (rc != SMLU_OK) return rc;
@@ -3682,6 +3745,17 @@ double smlu_stat(const smlu_handle* h, const char* key) {
     return c;
   }
   if (k == "repivots") return (double)h->repivots;
+  if (k == "sweep_timeouts") {   // a sync-free solve sweep's wait ever timed out (never expected)
+    int32_t v = 0;
+    if (h->sstatus.p && hipMemcpy(&v, h->sstatus.p, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return v;
+  }
+  if (k == "solve_sweeps") {
+    int64_t c = 0;
+    for (const Launch& L : h->fwd) c += L.kind == K_SWEEPF;
+    for (const Launch& L : h->bwd) c += L.kind == K_SWEEPB;
+    return (double)c;
+  }
   if (k.rfind("launches_", 0) == 0) {   // launches per kernel variant in the factor schedule
     const std::string v = k.substr(9);
     double c = 0;

@@ -1,0 +1,90 @@
+"""The sync-free triangular sweep of the large fronts (k_tri_sweep: one launch per level and
+direction, chunks of 256 rows chained by flags in ticket order) against the oracle's ldiv!
+(src/SharedMemSparseLU.jl:286-342) and against the previous one-launch-per-64-column-block
+schedule (SMLU_SOLVE_STEPS=1), and the sequence that once faulted a flag-chained solve:
+single-vector solves, then batches of every width, then single solves again, every batch column
+bitwise equal to its single solve."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import oracle as O
+import smlu
+from smlu import matrices as mats
+
+from _parity import TOL, DENSE_TOL, isapprox
+
+pytestmark = pytest.mark.gpu
+
+
+def _cases():
+    rng = np.random.default_rng(77)
+    D = rng.random((1100, 1100)) + 1100 * np.eye(1100) * rng.random(1100)
+    return {"poisson3d_28": mats.poisson3d(28),            # root separator 784 pivots, 13 blocks
+            "poisson2d_160": mats.poisson2d(160),          # tall fronts: ns ~ 160-320, M in the thousands
+            "dense_1100": sp.csc_matrix(D)}                # one front, 18 blocks, 5 chunks
+
+
+@pytest.mark.parametrize("name", ["poisson3d_28", "poisson2d_160", "dense_1100"])
+def test_sweep_matches_oracle_and_step_schedule(gpu, monkeypatch, name):
+    import torch
+    A = _cases()[name]
+    n = A.shape[0]
+    F = smlu.ParallelSparseLU(A)
+    assert F.stat("solve_sweeps") > 0
+    b = np.random.default_rng(1).random(n)
+    x = np.empty(n)
+    smlu.ldiv_(x, F, b)
+    ref = O.OracleLU(A, F.p, F.q)
+    xo = np.empty(n)
+    ref.ldiv(xo, b)
+    tol = DENSE_TOL if name.startswith("dense") else TOL
+    assert isapprox(x, xo, tol, tol)
+    # lsolve!/rsolve! through the sweeps (single direction each) against the oracle's
+    w = np.random.default_rng(2).random(n)
+    wl = w.copy()
+    smlu.lsolve_(F, wl)
+    assert np.allclose(wl, ref.lsolve(w.copy()), rtol=1e-12, atol=1e-12 * abs(w).max())
+    wu = w.copy()
+    smlu.rsolve_(F, wu)
+    xr = ref.rsolve(w.copy())
+    assert np.linalg.norm(wu - xr) <= 1e-10 * np.linalg.norm(xr)
+    # the previous per-block schedule gives the same solution to rounding
+    monkeypatch.setenv("SMLU_SOLVE_STEPS", "1")
+    F2 = smlu.ParallelSparseLU(A)
+    monkeypatch.delenv("SMLU_SOLVE_STEPS")
+    assert F2.stat("solve_sweeps") == 0
+    x2 = np.empty(n)
+    smlu.ldiv_(x2, F2, b)
+    assert np.linalg.norm(x - x2) <= 1e-12 * np.linalg.norm(x2)
+    assert F.stat("sweep_timeouts") == 0
+    F.close()
+    F2.close()
+
+
+def test_single_batch_single_sequence_bitwise(gpu):
+    # the order that faulted the round-2 flag-chained solve at 128^3: single, batched, single
+    import torch
+    A = mats.poisson3d(40)
+    n = A.shape[0]
+    F = smlu.ParallelSparseLU(A)
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(9)
+    b = torch.from_numpy(rng.random(n)).to(dev)
+    x = torch.empty_like(b)
+    F.solve_device(x, b)
+    x_first = x.clone()
+    for k in (2, 4, 8, 16):
+        B = torch.from_numpy(rng.random((k, n))).to(dev)
+        X = torch.empty_like(B)
+        F.solve_multi_device(X, B)
+        for j in range(k):
+            F.solve_device(x, B[j].contiguous())
+            assert torch.equal(x, X[j]), (k, j)
+    F.solve_device(x, b)
+    assert torch.equal(x, x_first)
+    xh = x.cpu().numpy()
+    bh = b.cpu().numpy()
+    assert np.abs(A @ xh - bh).max() <= 1e-12 * np.abs(bh).max()
+    assert F.stat("sweep_timeouts") == 0
+    F.close()
