@@ -195,6 +195,17 @@ int smlu_get_factors(smlu_handle* h, int64_t* Lcolptr, int64_t* Lrowval, double*
 int smlu_get_fronts(smlu_handle* h, int64_t* first, int64_t* parent, int64_t* rowptr, int64_t* rows,
                     int64_t* p0, int32_t* mode);
 
+/* F.L, F.U, F.p, F.q, F.Rs of a ComplexF64 handle (src/SharedMemSparseLU.jl:47-52: L and U are
+ * SparseMatrixCSC{ComplexF64}): the complex n x n factors, values as interleaved (re, im) doubles
+ * (2*nnz), same conventions as smlu_get_factors (L unit diagonal first, U diagonal last, rows
+ * sorted; F.L*F.U == (F.Rs .* A)[F.p, F.q]).  Folded exactly from the real-equivalent factors;
+ * available when the pivot sequence kept every complex row pair together (always under diagonal
+ * pivoting), else SMLU_ERR_STATE (smlu_get_factors still gives the 2n x 2n real-equivalent ones). */
+int smlu_get_sizes_z(smlu_handle* h, int64_t* n, int64_t* nnz_L, int64_t* nnz_U);
+int smlu_get_factors_z(smlu_handle* h, int64_t* Lcolptr, int64_t* Lrowval, double* Lnzval,
+                       int64_t* Ucolptr, int64_t* Urowval, double* Unzval,
+                       int64_t* p, int64_t* q, double* Rs);
+
 /* cleanup_ParallelSparseLU!(F) — exported but undefined in the reference
  * (src/SharedMemSparseLU.jl:31): frees device memory, stream and host plan. */
 void smlu_destroy(smlu_handle* h);

@@ -3561,6 +3561,116 @@ int smlu_get_factors(smlu_handle* h, int64_t* Lcolptr, int64_t* Lrowval, double*
   return SMLU_OK;
 }
 
+// ---- ComplexF64 factors (F.L::SparseMatrixCSC{ComplexF64}, src/SharedMemSparseLU.jl:47-48) ----
+// The handle holds the LU of K = phi(A) (phi: x + iy -> [[x, -y], [y, x]]).  When the row pivots
+// kept every complex row pair together and in order (pK[2k] = 2i, pK[2k+1] = 2i + 1: always under
+// diagonal pivoting, and whenever a complex pivot's real part carries its column), K's factors fold
+// exactly into the complex LU B = L U of B = (Rs .* A)[p, q]:  phi(L) = L_K D^{-1} and
+// phi(U) = D U_K with D = blockdiag([[1, 0], [Im u_kk / Re u_kk, 1]]), which gives
+//   l_ik = L_K[2i+1, 2k+1] - i L_K[2i, 2k+1]   and   u_kj = U_K[2k, 2j] - i U_K[2k, 2j+1]
+// (odd columns of L_K, even rows of U_K).  A pivot sequence that split a pair has no complex LU
+// form: SMLU_ERR_STATE, and the real-equivalent factors stay available (smlu_get_factors).
+struct ExportedZ {
+  std::vector<int64_t> Lp, Li, Up, Ui, p, q;
+  std::vector<double> Lx, Ux;   // interleaved (re, im)
+};
+
+static int export_complex(smlu_handle* h, ExportedZ& Z, bool values) {
+  if (!h->zc) return fail(h, SMLU_ERR_ARG, "not a complex handle (smlu_create_z)");
+  Exported X;
+  int rc = export_factors(h, X, values);
+  if (rc != SMLU_OK) return rc;
+  const int64_t n = h->zn;
+  Z.p.resize(n);
+  Z.q.resize(n);
+  for (int64_t k = 0; k < n; ++k) {
+    if (X.p[2 * k] % 2 != 0 || X.p[2 * k + 1] != X.p[2 * k] + 1)
+      return fail(h, SMLU_ERR_STATE, "complex factors: the row pivots split complex row pair " + std::to_string(k) +
+                                         " (only the real-equivalent factors exist; smlu_get_factors)");
+    if (X.q[2 * k] % 2 != 0 || X.q[2 * k + 1] != X.q[2 * k] + 1)
+      return fail(h, SMLU_ERR_STATE, "internal: complex column pair split");
+    Z.p[k] = X.p[2 * k] / 2;
+    Z.q[k] = X.q[2 * k] / 2;
+  }
+  // L: complex column k from K's column 2k+1 (rows >= 2k+1); pairs (2i, 2i+1) are adjacent
+  Z.Lp.assign(n + 1, 0);
+  Z.Li.clear();
+  Z.Lx.clear();
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t c = 2 * k + 1;
+    for (int64_t e = X.Lp[c]; e < X.Lp[c + 1]; ++e) {
+      const int64_t r = X.Li[e], i = r / 2;
+      if (Z.Li.size() == (size_t)Z.Lp[k] || Z.Li.back() != i) {
+        Z.Li.push_back(i);
+        Z.Lx.push_back(0.0);
+        Z.Lx.push_back(0.0);
+      }
+      const double v = values ? X.Lx[e] : 0.0;
+      if (r & 1) Z.Lx[Z.Lx.size() - 2] = v;    // real part: row 2i+1 of the odd column
+      else Z.Lx[Z.Lx.size() - 1] = -v;         // imaginary part: minus row 2i
+    }
+    Z.Lp[k + 1] = (int64_t)Z.Li.size();
+  }
+  // U: complex column j from the even rows of K's columns 2j (real part) and 2j+1 (minus imaginary)
+  Z.Up.assign(n + 1, 0);
+  Z.Ui.clear();
+  Z.Ux.clear();
+  for (int64_t j = 0; j < n; ++j) {
+    int64_t a = X.Up[2 * j], ae = X.Up[2 * j + 1], b = X.Up[2 * j + 1], be = X.Up[2 * j + 2];
+    while (true) {
+      while (a < ae && (X.Ui[a] & 1)) ++a;
+      while (b < be && (X.Ui[b] & 1)) ++b;
+      if (a >= ae && b >= be) break;
+      const int64_t ra = a < ae ? X.Ui[a] : INT64_MAX, rb = b < be ? X.Ui[b] : INT64_MAX;
+      const int64_t r = std::min(ra, rb);
+      Z.Ui.push_back(r / 2);
+      Z.Ux.push_back(ra == r && values ? X.Ux[a] : 0.0);
+      Z.Ux.push_back(rb == r && values ? -X.Ux[b] : 0.0);
+      if (ra == r) ++a;
+      if (rb == r) ++b;
+    }
+    Z.Up[j + 1] = (int64_t)Z.Ui.size();
+  }
+  return SMLU_OK;
+}
+
+int smlu_get_sizes_z(smlu_handle* h, int64_t* n, int64_t* nnzL, int64_t* nnzU) {
+  if (!h) return fail(h, SMLU_ERR_ARG, "NULL handle");
+  ExportedZ Z;
+  int rc = export_complex(h, Z, false);
+  if (rc != SMLU_OK) return rc;
+  if (n) *n = h->zn;
+  if (nnzL) *nnzL = Z.Lp[h->zn];
+  if (nnzU) *nnzU = Z.Up[h->zn];
+  return SMLU_OK;
+}
+
+int smlu_get_factors_z(smlu_handle* h, int64_t* Lcolptr, int64_t* Lrowval, double* Lnzval, int64_t* Ucolptr,
+                       int64_t* Urowval, double* Unzval, int64_t* p, int64_t* q, double* Rs) {
+  if (!h) return fail(h, SMLU_ERR_ARG, "NULL handle");
+  if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
+  HIPCHK(hipSetDevice(h->device));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  ExportedZ Z;
+  int rc = export_complex(h, Z, true);
+  if (rc != SMLU_OK) return rc;
+  const int64_t n = h->zn, b = h->opts.index_base;
+  if (Lcolptr) for (int64_t j = 0; j <= n; ++j) Lcolptr[j] = Z.Lp[j] + b;
+  if (Lrowval) for (size_t e = 0; e < Z.Li.size(); ++e) Lrowval[e] = Z.Li[e] + b;
+  if (Lnzval) std::memcpy(Lnzval, Z.Lx.data(), sizeof(double) * Z.Lx.size());
+  if (Ucolptr) for (int64_t j = 0; j <= n; ++j) Ucolptr[j] = Z.Up[j] + b;
+  if (Urowval) for (size_t e = 0; e < Z.Ui.size(); ++e) Urowval[e] = Z.Ui[e] + b;
+  if (Unzval) std::memcpy(Unzval, Z.Ux.data(), sizeof(double) * Z.Ux.size());
+  if (p) for (int64_t i = 0; i < n; ++i) p[i] = Z.p[i] + b;
+  if (q) for (int64_t i = 0; i < n; ++i) q[i] = Z.q[i] + b;
+  if (Rs) {   // the real-equivalent rows 2i and 2i+1 share the scale of complex row i
+    std::vector<double> rk(2 * n);
+    HIPCHK(hipMemcpy(rk.data(), h->Rs.p, sizeof(double) * 2 * n, hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < n; ++i) Rs[i] = rk[2 * i];
+  }
+  return SMLU_OK;
+}
+
 // ---- the reference's dense-chunk solve layout on the GPU -------------------
 // Chunk geometry, negated rectangles and back-to-front U chunks exactly as
 // get_chunking_parameters / allocate_chunks / fill_chunks! (src/SharedMemSparseLU.jl:101-243)

@@ -177,19 +177,19 @@ function Base.getproperty(F::ParallelSparseLU{Tf,Ti}, s::Symbol) where {Tf,Ti}  
     s in (:L, :U, :p, :q, :Rs) || return getfield(F, s)
     h = getfield(F, :handle)
     n = Int64(getfield(F, :n)); nl = Ref{Int64}(0); nu = Ref{Int64}(0)
-    # a ComplexF64 handle exports the factors of its real-equivalent 2n x 2n matrix (smlu.h)
-    ccall((:smlu_stat, libsmlu), Float64, (Ptr{Cvoid}, Cstring), h, "complex") == 1 && (n *= 2)
-    check(ccall((:smlu_get_sizes, libsmlu), Int32, (Ptr{Cvoid}, Ptr{Int64}, Ref{Int64}, Ref{Int64}),
-                h, C_NULL, nl, nu), h)
-    Lp = Vector{Int64}(undef, n + 1); Li = Vector{Int64}(undef, nl[]); Lx = Vector{Float64}(undef, nl[])
-    Up = Vector{Int64}(undef, n + 1); Ui = Vector{Int64}(undef, nu[]); Ux = Vector{Float64}(undef, nu[])
+    # ComplexF64: the complex factors, folded from the real-equivalent ones (smlu_get_factors_z)
+    z = Tf === ComplexF64
+    check(ccall(fnptr(z ? :smlu_get_sizes_z : :smlu_get_sizes), Int32,
+                (Ptr{Cvoid}, Ptr{Int64}, Ref{Int64}, Ref{Int64}), h, C_NULL, nl, nu), h)
+    Lp = Vector{Int64}(undef, n + 1); Li = Vector{Int64}(undef, nl[]); Lx = Vector{Tf}(undef, nl[])
+    Up = Vector{Int64}(undef, n + 1); Ui = Vector{Int64}(undef, nu[]); Ux = Vector{Tf}(undef, nu[])
     p = Vector{Int64}(undef, n); q = Vector{Int64}(undef, n); Rs = Vector{Float64}(undef, n)
-    check(ccall((:smlu_get_factors, libsmlu), Int32,
-                (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Ptr{Int64}, Ptr{Int64},
-                 Ptr{Float64}, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}),
+    check(ccall(fnptr(z ? :smlu_get_factors_z : :smlu_get_factors), Int32,
+                (Ptr{Cvoid}, Ptr{Int64}, Ptr{Int64}, Ptr{Tf}, Ptr{Int64}, Ptr{Int64},
+                 Ptr{Tf}, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}),
                 h, Lp, Li, Lx, Up, Ui, Ux, p, q, Rs), h)
-    s === :L && return SparseMatrixCSC(n, n, Lp, Li, Lx)
-    s === :U && return SparseMatrixCSC(n, n, Up, Ui, Ux)
+    s === :L && return SparseMatrixCSC{Tf,Ti}(n, n, Vector{Ti}(Lp), Vector{Ti}(Li), Lx)   # L::SparseMatrixCSC{Tf,Ti}
+    s === :U && return SparseMatrixCSC{Tf,Ti}(n, n, Vector{Ti}(Up), Vector{Ti}(Ui), Ux)
     s === :p && return Vector{Ti}(p)           # p::Vector{Ti}, q::Vector{Ti} as the reference (:49-50)
     s === :q && return Vector{Ti}(q)
     return Rs

@@ -79,6 +79,8 @@ SIGNATURES = {
     "smlu_chunked_ldiv_device": (i32, [vp, vp, vp]),
     "smlu_get_sizes": (i32, [vp, i64p, i64p, i64p]),
     "smlu_get_factors": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+    "smlu_get_sizes_z": (i32, [vp, i64p, i64p, i64p]),
+    "smlu_get_factors_z": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
     "smlu_destroy": (None, [vp]),
     "smlu_last_error_string": (ctypes.c_char_p, [vp]),
     "smlu_last_error_col": (i64, [vp]),

@@ -140,6 +140,26 @@ class ParallelSparseLU:
 
     # ---- factor access (F.L, F.U, F.p, F.q, F.Rs) ----
     def _download(self):
+        """F.L, F.U, F.p, F.q, F.Rs as the reference has them: complex n x n factors on a complex
+        handle (smlu_get_factors_z), real ones otherwise."""
+        if not self.is_complex:
+            return self.real_equivalent_factors()
+        if getattr(self, "_zfactors", None) is None:
+            L = C.lib()
+            n = self.n
+            nl, nu = ctypes.c_int64(), ctypes.c_int64()
+            _check(L.smlu_get_sizes_z(self._h, None, ctypes.byref(nl), ctypes.byref(nu)), self._h)
+            Lp = np.empty(n + 1, np.int64); Li = np.empty(nl.value, np.int64); Lx = np.empty(nl.value, np.complex128)
+            Up = np.empty(n + 1, np.int64); Ui = np.empty(nu.value, np.int64); Ux = np.empty(nu.value, np.complex128)
+            p = np.empty(n, np.int64); q = np.empty(n, np.int64); Rs = np.empty(n)
+            _check(L.smlu_get_factors_z(self._h, C.ptr(Lp), C.ptr(Li), C.ptr(Lx), C.ptr(Up), C.ptr(Ui),
+                                        C.ptr(Ux), C.ptr(p), C.ptr(q), C.ptr(Rs)), self._h)
+            self._zfactors = dict(L=sp.csc_matrix((Lx, Li, Lp), shape=(n, n)),
+                                  U=sp.csc_matrix((Ux, Ui, Up), shape=(n, n)), p=p, q=q, Rs=Rs)
+        return self._zfactors
+
+    def real_equivalent_factors(self):
+        """The factors the GPU holds: on a complex handle those of the 2n x 2n real-equivalent K."""
         if self._factors is None:
             L = C.lib()
             n = 2 * self.n if self.is_complex else self.n   # complex: the real-equivalent matrix
@@ -202,6 +222,7 @@ class ParallelSparseLU:
         fn = C.lib().smlu_refactor_z_device if self.is_complex else C.lib().smlu_refactor_device
         rc = _check(fn(self._h, ctypes.c_void_p(ptr)), self._h)
         self._factors = None
+        self._zfactors = None
         if rc == C.SMLU_SINGULAR:
             raise SingularException(C.lib().smlu_last_error_col(self._h))
         return rc
@@ -259,6 +280,7 @@ def lu_(F: ParallelSparseLU, A):
         fn = L.smlu_refactor_csc_z if F.is_complex else L.smlu_refactor_csc
         rc = fn(F._h, F.n, C.ptr(F._colptr), C.ptr(F._rowval), C.ptr(vals))
     F._factors = None
+    F._zfactors = None
     _check(rc, F._h)
     if rc == C.SMLU_SINGULAR:
         raise SingularException(L.smlu_last_error_col(F._h))

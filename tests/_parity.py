@@ -21,6 +21,12 @@ def assert_same_pattern(G, R):
     assert np.array_equal(G.indices, R.indices), "rowval differs from the oracle's"
 
 
+def _real(F):
+    """The factors the GPU holds (a complex handle: those of its real-equivalent K)."""
+    return F.real_equivalent_factors() if getattr(F, "is_complex", False) else \
+        dict(L=F.L, U=F.U, p=F.p, q=F.q, Rs=F.Rs)
+
+
 def pivot_parity(A, F, prev_pivmode=0, full_piv_ns=None, given=False):
     """The GPU's pivot DECISIONS against an independent restatement of its rule: the multifrontal
     oracle (oracle/mf.c) chooses its own row order on the handle's assembly tree (threshold
@@ -28,11 +34,12 @@ def pivot_parity(A, F, prev_pivmode=0, full_piv_ns=None, given=False):
     modes and the re-pivoting refactor restated in oracle.gpu_pivot_choice).  p must be
     bit-identical; so must the per-front candidate modes and the final pivoting mode."""
     fr = F.fronts()
-    p_or, pm, modes, _ = O.gpu_pivot_choice(A, F.q, fr, pivmode=prev_pivmode, full_piv_ns=full_piv_ns,
+    fx = _real(F)
+    p_or, pm, modes, _ = O.gpu_pivot_choice(A, fx["q"], fr, pivmode=prev_pivmode, full_piv_ns=full_piv_ns,
                                             given=given)
     assert np.array_equal(modes, fr["mode"]), "per-front pivot candidate modes differ from the restated rule"
     assert int(F.stat("pivmode")) == pm, (F.stat("pivmode"), pm)
-    bad = np.flatnonzero(np.asarray(F.p) != p_or)
+    bad = np.flatnonzero(np.asarray(fx["p"]) != p_or)
     assert bad.size == 0, f"pivot order differs from the oracle's at {bad.size} positions, first {bad[:8]}"
     return p_or
 
@@ -41,12 +48,13 @@ def factor_parity(A, F, rtol=1e-12, prev_pivmode=0, full_piv_ns=None):
     """Pivot order chosen independently by the multifrontal oracle (pivot_parity), then the
     exported factors vs the oracle's fixed-pivot LU of (Rs.*A)[p, q]."""
     pivot_parity(A, F, prev_pivmode=prev_pivmode, full_piv_ns=full_piv_ns)
-    p, q, Rs = F.p, F.q, F.Rs
+    fx = _real(F)
+    p, q, Rs = fx["p"], fx["q"], fx["Rs"]
     Ro = O.rowscale(A)
     assert np.array_equal(Rs, Ro), "row scaling must be bitwise identical"
     ref = O.OracleLU(A, p, q, Ro)
     assert ref.status == 0
-    L, U = F.L, F.U
+    L, U = fx["L"], fx["U"]
     for G, R in ((L, ref.L), (U, ref.U)):
         # pattern: bit-identical colptr/rowval to the oracle's structural fill of (Rs.*A)[p,q]
         assert_same_pattern(G, R)

@@ -69,7 +69,7 @@ def test_complex_helmholtz3d(gpu, N, grid):
     K = O.real_equivalent(A)
     factor_parity(K, F, rtol=1e-10)
     # the column order keeps each complex column's two real columns together
-    q = F.q
+    q = F.real_equivalent_factors()["q"]
     assert np.array_equal(q[0::2] // 2, q[1::2] // 2)
     check_solve(F, A, np.random.default_rng(N), tol=1e-11)
 
@@ -85,7 +85,11 @@ def test_complex_imaginary_diagonal(gpu):
     A = sp.csc_matrix(A)
     F = smlu.ParallelSparseLU(A)
     factor_parity(O.real_equivalent(A), F, rtol=1e-10)
-    assert not np.array_equal(F.p, F.q)   # interchanges happened
+    fk = F.real_equivalent_factors()
+    assert not np.array_equal(fk["p"], fk["q"])   # interchanges happened
+    # the interchanges split complex row pairs: there is no complex LU form of these factors
+    with pytest.raises(smlu.SmluError):
+        F.L
     check_solve(F, A, rng)
 
 
@@ -174,11 +178,12 @@ def test_complex_lsolve_rsolve(gpu):
     b = crand(rng, n)
     x = b.copy()
     smlu.lsolve_(F, x)
-    ref = spla.spsolve_triangular(F.L.tocsr(), b.view(np.float64), lower=True)
+    fk = F.real_equivalent_factors()
+    ref = spla.spsolve_triangular(fk["L"].tocsr(), b.view(np.float64), lower=True)
     assert isapprox(x.view(np.float64), ref, TOL, TOL)
     x = b.copy()
     smlu.rsolve_(F, x)
-    ref = spla.spsolve_triangular(F.U.tocsr(), b.view(np.float64), lower=False)
+    ref = spla.spsolve_triangular(fk["U"].tocsr(), b.view(np.float64), lower=False)
     assert isapprox(x.view(np.float64), ref, 1e-10, 1e-10)
 
 
@@ -199,3 +204,48 @@ def test_complex_type_checks(gpu):
         smlu.ldiv_(np.empty(25, np.complex128), F, np.ones(25, np.complex128))
     with pytest.raises(TypeError):
         smlu.lu_(F, A.astype(np.complex128) * 1j)
+
+
+def _check_complex_factors(A, F):
+    """F.L, F.U, F.p, F.q, F.Rs of a complex handle are complex n x n (the reference's
+    SparseMatrixCSC{ComplexF64}, src/SharedMemSparseLU.jl:47-52): UMFPACK's conventions (L unit
+    diagonal stored first, U diagonal last, rows sorted) and L*U == (Rs.*A)[p, q]; they fold the
+    real-equivalent factors exactly (Rs of complex row i = Rs of K's rows 2i and 2i+1)."""
+    L, U, p, q, Rs = F.L, F.U, F.p, F.q, F.Rs
+    n = A.shape[0]
+    assert L.dtype == np.complex128 and U.dtype == np.complex128 and L.shape == (n, n)
+    fk = F.real_equivalent_factors()
+    assert np.array_equal(p, fk["p"][0::2] // 2) and np.array_equal(q, fk["q"][0::2] // 2)
+    assert np.array_equal(Rs, fk["Rs"][0::2]) and np.array_equal(fk["Rs"][0::2], fk["Rs"][1::2])
+    for j in range(n):
+        li = L.indices[L.indptr[j]:L.indptr[j + 1]]
+        ui = U.indices[U.indptr[j]:U.indptr[j + 1]]
+        assert li[0] == j and L.data[L.indptr[j]] == 1.0 and np.all(np.diff(li) > 0)
+        assert ui[-1] == j and np.all(np.diff(ui) > 0)
+    B = (sp.diags(Rs) @ A).tocsr()[p][:, q]
+    E = L @ U - B
+    assert abs(E).max() <= 1e-12 * max(abs(B).max(), 1.0)
+
+
+@pytest.mark.parametrize("case", ["helmholtz", "dominant", "fe"])
+def test_complex_factor_export(gpu, case):
+    rng = np.random.default_rng(71)
+    if case == "helmholtz":
+        A = helmholtz3d(12, shift=0.5)
+    elif case == "dominant":
+        R = mats.random_dominant(300, 0.02, seed=9).astype(np.complex128)
+        R.data = R.data * np.exp(1j * rng.random(R.nnz) * 2 * np.pi)
+        A = sp.csc_matrix(R)
+    else:
+        A = complex_fe(rng, 20)
+    F = smlu.ParallelSparseLU(A)
+    fk = F.real_equivalent_factors()
+    pk = fk["p"]
+    paired = np.all(pk[0::2] % 2 == 0) and np.array_equal(pk[1::2], pk[0::2] + 1)
+    if case != "fe":
+        assert paired   # diagonal-dominant / shifted-Laplacian values keep every pair
+    if paired:
+        _check_complex_factors(A, F)
+    else:
+        with pytest.raises(smlu.SmluError):
+            F.L
