@@ -608,13 +608,13 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma6(const GemmTask* __rest
 //  * A staged [k][128] in LDS with 16-byte stores; MFMA block rows are interleaved so that one
 //    conflict-free ds_read_b128 feeds two blocks: block i, lane row li holds tile row
 //    wr + 32 (i >> 1) + 2 li + (i & 1);
-//  * B staged [col][k] with k padded to 18 doubles: 16-byte stores, conflict-free b64 reads;
+//  * B staged [col][k] with k padded to 17 doubles: conflict-free b64 (and merged read2_b64) reads;
 //  * C read and written as row pairs (16-byte accesses, 256 contiguous bytes per 16 lanes);
 //  * the LDS fragments of the next k-quad are read while the current quad's 16 MFMAs run, and
 //    the next K slice's global loads are in flight across the whole slice.
 // Interior tiles only (m, n in range); edge tiles take gemm128_mfma_body<.., false>.
 // ------------------------------------------------------------------------------------
-#define B2LD 18
+#define B2LD 17   // odd: conflict-free ds_read_b64 and the compiler's merged ds_read2_b64 (k, k+4) pairs
 #ifndef MFMA2_NOEDGE
 #define MFMA2_NOEDGE 0
 #endif
@@ -695,7 +695,9 @@ __device__ __forceinline__ void gemm128_mfma2_interior(const GemmTask& t, int m0
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       *reinterpret_cast<v2d*>(&S.A[buf][wv + 4 * q][2 * lane]) = ra[q];
-      *reinterpret_cast<v2d*>(&S.B[buf][8 * wv + (lane >> 3) + 32 * q][b_k]) = -rb[q];
+      double* bd = &S.B[buf][8 * wv + (lane >> 3) + 32 * q][b_k];   // 8-byte aligned (odd row stride)
+      bd[0] = -rb[q].x;
+      bd[1] = -rb[q].y;
     }
   };
   auto slice = [&](int cur) {
@@ -756,7 +758,9 @@ template <bool TRSM>
 __global__ __launch_bounds__(256, 2) void k_gemm128_mfma2(const GemmTask* __restrict__ tasks, int ntask,
                                                           GrowthArgs ga) {
   __shared__ __attribute__((aligned(16))) double lds[sizeof(Mfma2Lds) / sizeof(double)];
-  const int64_t b = blockIdx.x;
+  // XCD-aware: the workgroups of one XCD take one contiguous range of tiles, so the 8 x 8 tile
+  // groups of tile_rc run side by side in one L2 and share their A and B panels there
+  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
   const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
   int tm, tn;
   tile_rc<HBM_>(t, b - t.tile0, tm, tn);

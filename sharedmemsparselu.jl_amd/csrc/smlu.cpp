@@ -689,6 +689,8 @@ static int build_schedule(smlu_handle* h) {
   if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
   if (const char* e = std::getenv("SMLU_T128MIN")) h->t128_min = std::atoll(e);
   h->small_k = !(std::getenv("SMLU_SMALLK") && std::atoi(std::getenv("SMLU_SMALLK")) == 0);
+  // MFMA 128 tile: 130 = v2 (16-byte operand traffic, kernels_gemm.hip), 129 = v1 (SMLU_MFMA_TILE)
+  const int mfma_tile = std::getenv("SMLU_MFMA_TILE") ? std::atoi(std::getenv("SMLU_MFMA_TILE")) : 130;
   // GEMM-form TRSM (k_tri_inv + GEMM tasks) needs the growth epilogue of the MFMA/64 tiles
   {
     const char* e = std::getenv("SMLU_TRSM_GEMM");
@@ -753,7 +755,7 @@ static int build_schedule(smlu_handle* h) {
     int64_t t128 = 0;
     for (auto& g : cand) t128 += (int64_t)((g.m + 127) / 128) * ((g.n + 127) / 128);
     int tile = t128 >= h->t128_min ? 128 : 64;
-    if (tile == 128 && h->opts.use_mfma) tile = 129;   // fp64 MFMA variant of the 128 tile
+    if (tile == 128 && h->opts.use_mfma) tile = mfma_tile;   // fp64 MFMA variant of the 128 tile
     if (tile == 64 && h->small_k) {                    // every k <= 64: one-shot K staging
       int kmax = 0;
       for (auto& g : cand) kmax = std::max(kmax, g.k);
@@ -1662,7 +1664,7 @@ static int build_schedule(smlu_handle* h) {
   static const bool no_tiny = std::getenv("SMLU_NO_TINY_SOLVE") != nullptr;   // dev knob
   // large fronts: one sync-free sweep launch per level and direction (default) or one launch per
   // 64-column block (SMLU_SOLVE_STEPS=1, the previous schedule)
-  static const bool sweep_solve = !(std::getenv("SMLU_SOLVE_STEPS") && std::atoi(std::getenv("SMLU_SOLVE_STEPS")) == 1);
+  const bool sweep_solve = !(std::getenv("SMLU_SOLVE_STEPS") && std::atoi(std::getenv("SMLU_SOLVE_STEPS")) == 1);
   int64_t ssync_n = 1;   // [0] unused
   static const int64_t big_work = [] {
     const char* e = std::getenv("SMLU_SOLVE_BIGWORK");   // dev knob (sweeps)
@@ -3872,8 +3874,8 @@ double smlu_stat(const smlu_handle* h, const char* key) {
     for (const Launch& L : h->fac) {
       const bool gemm = L.kind == K_GEMM || L.kind == K_GEMMU || L.kind == K_GEMMO || L.kind == K_GEMM22;
       const bool trsm = L.kind == K_TRSML;
-      if (v == "mfma128" && gemm && L.aux == 129) ++c;
-      else if (v == "mfma128_trsm" && trsm && L.aux == 129) ++c;
+      if (v == "mfma128" && gemm && (L.aux == 129 || L.aux == 130)) ++c;
+      else if (v == "mfma128_trsm" && trsm && (L.aux == 129 || L.aux == 130)) ++c;
       else if (v == "valu128" && gemm && L.aux == 128) ++c;
       else if (v == "k64" && gemm && L.aux == 65) ++c;
       else if (v == "k64_trsm" && trsm && L.aux == 65) ++c;

@@ -21,11 +21,11 @@ def _cases():
     rng = np.random.default_rng(77)
     D = rng.random((1100, 1100)) + 1100 * np.eye(1100) * rng.random(1100)
     return {"poisson3d_28": mats.poisson3d(28),            # root separator 784 pivots, 13 blocks
-            "poisson2d_160": mats.poisson2d(160),          # tall fronts: ns ~ 160-320, M in the thousands
+            "poisson2d_300": mats.poisson2d(300),          # root separator 300 pivots, tall fronts below
             "dense_1100": sp.csc_matrix(D)}                # one front, 18 blocks, 5 chunks
 
 
-@pytest.mark.parametrize("name", ["poisson3d_28", "poisson2d_160", "dense_1100"])
+@pytest.mark.parametrize("name", ["poisson3d_28", "poisson2d_300", "dense_1100"])
 def test_sweep_matches_oracle_and_step_schedule(gpu, monkeypatch, name):
     import torch
     A = _cases()[name]
