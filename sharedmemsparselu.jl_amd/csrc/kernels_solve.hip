@@ -499,11 +499,15 @@ void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step, const SNod
 // apply it -- and publishes each solved block: x values by write-through (sc1) stores, the
 // storing wave's vmcnt drained, a workgroup barrier, then one sc1 flag store; consumers poll the
 // flag with sc1 loads and read the x values with sc1 loads (MI355X_MICROARCH.md, hand-off form
-// "one lane of each storing workgroup").  Deadlock-free by tickets: work items are taken in ticket
+// "one lane of each storing workgroup").  The handed-off values go through a buffer of their own,
+// xh: 64 doubles per (block, rhs), 512-byte aligned, written whole by ONE store instruction of
+// one wave -- a consumer never holds in its L2 a line that a later block shares (reading x itself,
+// whose 128-byte lines straddle block boundaries, returned stale halves).  Deadlock-free by tickets: work items are taken in ticket
 // order (atomic counter), and an item only waits on items of lower tickets, which are running.
 // Per right-hand side the arithmetic does not depend on the batch width (batched == single).
 // sync: this launch's ticket counter at sync[0], flags of front f at sync[1 + pad_f + block];
-// zeroed before every solve.  status: set to 1 if a wait ever times out (never expected).
+// zeroed before every solve; xh: the hand-off slot of flag g (index into sync) at
+// xh + g * 64 * kMultiRhs.  status: set to 1 if a wait ever times out (never expected).
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ void sweep_wait(int32_t* f, int32_t* status) {
   if (threadIdx.x == 0) {
@@ -528,9 +532,9 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
 // One wave per SIMD: the preloaded diagonal row and the tile row are 128 VGPRs each.
 template <bool UPPER, int NR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, int32_t* __restrict__ sync, int32_t* __restrict__ status,
-                 const SNode* __restrict__ sn, const double* __restrict__ store, double* __restrict__ x,
-                 double* __restrict__ vbuf, Rhs rh) {
+void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, int32_t* __restrict__ sync, double* __restrict__ xh,
+                 int32_t* __restrict__ status, const SNode* __restrict__ sn, const double* __restrict__ store,
+                 double* __restrict__ x, double* __restrict__ vbuf, Rhs rh) {
   __shared__ double xs[64][NR];
   __shared__ int64_t s_item;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -540,6 +544,7 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, int32_t* __restrict_
   const int fi = find_front_tile(ft, nft, item);
   const SNode s = sn[ft[fi].s];
   int32_t* flags = sync + 1 + ft[fi].pad;
+  double* xhf = xh + (int64_t)(1 + ft[fi].pad) * 64 * kMultiRhs;   // hand-off slots of this front's blocks
   const int64_t q = item - ft[fi].wg0;
   const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns, nblk = (ns + 63) / 64;
   const double* Lp = store + s.Loff;
@@ -599,8 +604,8 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, int32_t* __restrict_
     const int bw = (int)min<int64_t>(64, ns - 64 * c);
     if (has) load_tile(c, bw);
     sweep_wait(flags + c, status);
-    if (wv == 0 && lane < bw)
-      for (int r = 0; r < nr; ++r) xs[lane][r] = ld_sc1(xf + r * rh.ldx + 64 * c + lane);
+    if (wv == 0)
+      for (int r = 0; r < nr; ++r) xs[lane][r] = ld_sc1(xhf + (c * kMultiRhs + r) * 64 + lane);
     __syncthreads();
     if (has) fma_tile(bw);
     __syncthreads();
@@ -617,9 +622,11 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, int32_t* __restrict_
         if (r < nr) {
           const double y = tri64_row<UPPER>(o[r], drow, dinv, bw, lane);
           o[r] = y;
-          if (lane < bw && has) {
+          const bool mine = lane < bw && has;
+          st_sc1(xhf + (b * kMultiRhs + r) * 64 + lane, mine ? y : 0.0);   // 4 whole lines, one store
+          if (mine) {
             xs[lane][r] = y;
-            st_sc1(xf + r * rh.ldx + 64 * b + lane, y);
+            xf[r * rh.ldx + 64 * b + lane] = y;
             v[r * rh.ldv + 64 * b + lane] = y;
           }
         }
@@ -919,11 +926,12 @@ hipError_t launch_bwd_u12(hipStream_t st, int64_t nwg, const FrontTile* ft, int 
   return hipGetLastError();
 }
 hipError_t launch_tri_sweep(hipStream_t st, bool upper, int64_t nwg, const FrontTile* ft, int nft, int32_t* sync,
-                            int32_t* status, const SNode* sn, const double* store, double* x, double* vbuf, Rhs rh) {
+                            double* xh, int32_t* status, const SNode* sn, const double* store, double* x, double* vbuf,
+                            Rhs rh) {
   if (nwg <= 0) return hipSuccess;
-#define SWEEP(NR)                                                                                             \
-  (upper ? (k_tri_sweep<true, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sync, status, sn, store, x, vbuf, rh)) \
-         : (k_tri_sweep<false, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sync, status, sn, store, x, vbuf, rh)))
+#define SWEEP(NR)                                                                                                 \
+  (upper ? (k_tri_sweep<true, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sync, xh, status, sn, store, x, vbuf, rh)) \
+         : (k_tri_sweep<false, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sync, xh, status, sn, store, x, vbuf, rh)))
   if (rh.n <= 1) SWEEP(1);
   else if (rh.n <= 4) SWEEP(4);
   else if (rh.n <= 8) SWEEP(8);

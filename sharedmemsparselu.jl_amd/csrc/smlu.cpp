@@ -59,8 +59,8 @@ hipError_t launch_tri_block(hipStream_t, bool, int64_t, const FrontTile*, int, i
                             const double*, double*, double*, Rhs);
 hipError_t launch_bwd_u12(hipStream_t, int64_t, const FrontTile*, int, const SNode*, const int32_t*,
                           const double*, const double*, double*, Rhs);
-hipError_t launch_tri_sweep(hipStream_t, bool, int64_t, const FrontTile*, int, int32_t*, int32_t*, const SNode*,
-                            const double*, double*, double*, Rhs);
+hipError_t launch_tri_sweep(hipStream_t, bool, int64_t, const FrontTile*, int, int32_t*, double*, int32_t*,
+                            const SNode*, const double*, double*, double*, Rhs);
 hipError_t launch_fwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                       const int32_t*, const double*, double*, double*, Rhs);
 hipError_t launch_bwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*,
@@ -351,6 +351,7 @@ struct smlu_handle {
   DBuf<int2> aents;
   DBuf<FrontTile> ftiles;
   DBuf<int32_t> ssync, sstatus;   // sync-free solve sweeps: tickets + block flags (zeroed per solve); timeouts
+  DBuf<double> sxh;               // sweep hand-off slots: 64 x kMultiRhs doubles per flag
   int64_t ssync_n = 0;
   DBuf<GemmTask> gtasks;
   DBuf<SwapTask> stasks;
@@ -445,6 +446,7 @@ struct smlu_handle {
     ftiles.free();
     ssync.free();
     sstatus.free();
+    sxh.free();
     gtasks.free();
     stasks.free();
     xcols.free();
@@ -2032,6 +2034,7 @@ static int build_schedule(smlu_handle* h) {
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
   h->ssync_n = ssync_n;
   HIPCHK(h->ssync.alloc((size_t)ssync_n));
+  if (ssync_n > 1) HIPCHK(h->sxh.alloc((size_t)ssync_n * 64 * kMultiRhs));
   HIPCHK(hipMemsetAsync(h->ssync.p, 0, sizeof(int32_t) * ssync_n, st));
   if (!h->sstatus.p) {
     HIPCHK(h->sstatus.alloc(1));
@@ -2488,6 +2491,7 @@ static void release_schedule(smlu_handle* h) {
   h->aents.free();
   h->ftiles.free();
   h->ssync.free();
+  h->sxh.free();
   h->gtasks.free();
   h->stasks.free();
   h->xcols.free();
@@ -2568,7 +2572,7 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, d
     case K_SWEEPF:
     case K_SWEEPB:
       return launch_tri_sweep(st, L.kind == K_SWEEPB, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->ssync.p + L.aux,
-                              h->sstatus.p, h->sn.p, h->store.p, w, v, rh);
+                              h->sxh.p + L.aux * 64 * kMultiRhs, h->sstatus.p, h->sn.p, h->store.p, w, v, rh);
     case K_BWDU12C:
       return launch_bwd_u12_cols(st, h->sn.p, L.node, h->hsn[L.node].ns, L.aux, L.aux2, (int)L.cnt, h->rows.p,
                                  h->store.p, w, h->vbuf.p);
