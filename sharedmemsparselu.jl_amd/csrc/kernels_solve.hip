@@ -494,57 +494,75 @@ void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step, const SNod
 // replacing one launch per 64-column block).  Work item = a chunk of 256 rows (forward: rows
 // [256q, 256q+256) of the front; backward: the pivot blocks nblk-1-4q-t, t < 4); one workgroup,
 // one thread per row.  A chunk applies the column blocks solved by earlier chunks of its front as
-// their flags appear, then runs its own (up to four) diagonal blocks in sequence inside the
+// they are published, then runs its own (up to four) diagonal blocks in sequence inside the
 // workgroup -- wave t solves block 4q+t (the 64-step readlane chain of tri64_row), the waves below
-// apply it -- and publishes each solved block: x values by write-through (sc1) stores, the
-// storing wave's vmcnt drained, a workgroup barrier, then one sc1 flag store; consumers poll the
-// flag with sc1 loads and read the x values with sc1 loads (MI355X_MICROARCH.md, hand-off form
-// "one lane of each storing workgroup").  The handed-off values go through a buffer of their own,
-// xh: 64 doubles per (block, rhs), 512-byte aligned, written whole by ONE store instruction of
-// one wave -- a consumer never holds in its L2 a line that a later block shares (reading x itself,
-// whose 128-byte lines straddle block boundaries, returned stale halves).  Deadlock-free by tickets: work items are taken in ticket
-// order (atomic counter), and an item only waits on items of lower tickets, which are running.
-// Per right-hand side the arithmetic does not depend on the batch width (batched == single).
-// sync: this launch's ticket counter at sync[0], flags of front f at sync[1 + pad_f + block];
-// zeroed before every solve; xh: the hand-off slot of flag g (index into sync) at
+// apply it -- and publishes each solved block.
+// Protocol: every word shared between workgroups is accessed by device-scope ATOMICS, performed at
+// the memory side, so no cache level can hand out a stale copy and nothing has to be reset between
+// solves (a hipGraph replay of reset + sweep does not guarantee that other XCDs' L2s see the reset:
+// a single-vector solve after a batched one read stale flags and hung).
+//  * tickets: one 64-bit counter per launch, never reset; a workgroup's ticket t gives its work item
+//    t mod nwg and the launch's epoch t / nwg + 1 (launches of a sweep are stream-ordered, so each
+//    takes one contiguous range of tickets);
+//  * block b is published by writing its 64 x NR solved values into its hand-off slot (atomic swaps)
+//    and then setting flag[b] to the epoch (atomic max) behind the wave's vmcnt drain and a barrier;
+//  * a consumer polls flag[b] (atomic compare-and-swap that never matches) until it reaches the epoch
+//    and reads the slot the same way on the raw bits.
+// Deadlock-free: items are taken in ticket order and an item only waits on items of lower tickets
+// (earlier chunks of the same front), which are running.  Per right-hand side the arithmetic does
+// not depend on the batch width (a batched column is bitwise the single solve).
+// tick: this launch's counter; flags of front f at flags + pad_f; hand-off slot of flag g at
 // xh + g * 64 * kMultiRhs.  status: set to 1 if a wait ever times out (never expected).
 // ------------------------------------------------------------------------------------
-__device__ __forceinline__ void sweep_wait(int32_t* f, int32_t* status) {
+// Reads as compare-and-swap with a value never stored (an idempotent add of 0 would be lowered to
+// a plain cached load): the returned old value comes from the memory-side atomic unit.
+__device__ __forceinline__ int32_t atomic_read_i32(int32_t* p) {
+  int32_t e = INT32_MIN;   // flags hold epochs >= 0
+  __hip_atomic_compare_exchange_strong(p, &e, INT32_MIN, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return e;
+}
+__device__ __forceinline__ double atomic_read_f64(double* p) {
+  unsigned long long e = 0x7ff4dead5eed0001ull;   // a signalling-NaN pattern no solve writes
+  __hip_atomic_compare_exchange_strong(reinterpret_cast<unsigned long long*>(p), &e, 0x7ff4dead5eed0001ull,
+                                       __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __longlong_as_double((long long)e);
+}
+__device__ __forceinline__ void atomic_write_f64(double* p, double v) {
+  (void)__hip_atomic_exchange(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
+                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sweep_wait(int32_t* f, int32_t epoch, int32_t* status) {
   if (threadIdx.x == 0) {
     int n = 0;
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+    while (atomic_read_i32(f) < epoch) {
       __builtin_amdgcn_s_sleep(1);
       if (++n > (1 << 22)) {
-        __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        (void)__hip_atomic_fetch_max(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
   }
   __syncthreads();
 }
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
-// One wave per SIMD: the preloaded diagonal row and the tile row are 128 VGPRs each.
 template <bool UPPER, int NR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
-void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, int32_t* __restrict__ sync, double* __restrict__ xh,
-                 int32_t* __restrict__ status, const SNode* __restrict__ sn, const double* __restrict__ store,
-                 double* __restrict__ x, double* __restrict__ vbuf, Rhs rh) {
+void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* __restrict__ tick,
+                 int32_t* __restrict__ flags0, double* __restrict__ xh, int32_t* __restrict__ status,
+                 const SNode* __restrict__ sn, const double* __restrict__ store, double* __restrict__ x,
+                 double* __restrict__ vbuf, Rhs rh) {
   __shared__ double xs[64][NR];
-  __shared__ int64_t s_item;
+  __shared__ unsigned long long s_ticket;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (tid == 0) s_item = atomicAdd(&sync[0], 1);
+  if (tid == 0) s_ticket = __hip_atomic_fetch_add(tick, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  const int64_t item = s_item;
+  const int64_t item = (int64_t)(s_ticket % gridDim.x);
+  const int32_t epoch = (int32_t)(s_ticket / gridDim.x) + 1;
   const int fi = find_front_tile(ft, nft, item);
   const SNode s = sn[ft[fi].s];
-  int32_t* flags = sync + 1 + ft[fi].pad;
-  double* xhf = xh + (int64_t)(1 + ft[fi].pad) * 64 * kMultiRhs;   // hand-off slots of this front's blocks
+  int32_t* flags = flags0 + ft[fi].pad;
+  double* xhf = xh + (int64_t)ft[fi].pad * 64 * kMultiRhs;   // hand-off slots of this front's blocks
   const int64_t q = item - ft[fi].wg0;
   const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns, nblk = (ns + 63) / 64;
   const double* Lp = store + s.Loff;
@@ -603,9 +621,9 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, int32_t* __restrict_
     const int64_t c = UPPER ? nblk - 1 - e : e;
     const int bw = (int)min<int64_t>(64, ns - 64 * c);
     if (has) load_tile(c, bw);
-    sweep_wait(flags + c, status);
+    sweep_wait(flags + c, epoch, status);
     if (wv == 0)
-      for (int r = 0; r < nr; ++r) xs[lane][r] = ld_sc1(xhf + (c * kMultiRhs + r) * 64 + lane);
+      for (int r = 0; r < nr; ++r) xs[lane][r] = atomic_read_f64(xhf + (c * kMultiRhs + r) * 64 + lane);
     __syncthreads();
     if (has) fma_tile(bw);
     __syncthreads();
@@ -623,7 +641,7 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, int32_t* __restrict_
           const double y = tri64_row<UPPER>(o[r], drow, dinv, bw, lane);
           o[r] = y;
           const bool mine = lane < bw && has;
-          st_sc1(xhf + (b * kMultiRhs + r) * 64 + lane, mine ? y : 0.0);   // 4 whole lines, one store
+          atomic_write_f64(xhf + (b * kMultiRhs + r) * 64 + lane, mine ? y : 0.0);
           if (mine) {
             xs[lane][r] = y;
             xf[r * rh.ldx + 64 * b + lane] = y;
@@ -634,7 +652,7 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, int32_t* __restrict_
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    if (tid == 0) __hip_atomic_store(flags + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) (void)__hip_atomic_fetch_max(flags + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wv > t && has) fma_tile(bw);
     __syncthreads();
   }
@@ -925,13 +943,13 @@ hipError_t launch_bwd_u12(hipStream_t st, int64_t nwg, const FrontTile* ft, int 
   else k_bwd_u12<16><<<(unsigned)nwg, 512, 0, st>>>(ft, nft, sn, rows, store, x, vbuf, rh);
   return hipGetLastError();
 }
-hipError_t launch_tri_sweep(hipStream_t st, bool upper, int64_t nwg, const FrontTile* ft, int nft, int32_t* sync,
-                            double* xh, int32_t* status, const SNode* sn, const double* store, double* x, double* vbuf,
-                            Rhs rh) {
+hipError_t launch_tri_sweep(hipStream_t st, bool upper, int64_t nwg, const FrontTile* ft, int nft,
+                            unsigned long long* tick, int32_t* flags, double* xh, int32_t* status, const SNode* sn,
+                            const double* store, double* x, double* vbuf, Rhs rh) {
   if (nwg <= 0) return hipSuccess;
-#define SWEEP(NR)                                                                                                 \
-  (upper ? (k_tri_sweep<true, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sync, xh, status, sn, store, x, vbuf, rh)) \
-         : (k_tri_sweep<false, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sync, xh, status, sn, store, x, vbuf, rh)))
+#define SWEEP(NR)                                                                                                   \
+  (upper ? (k_tri_sweep<true, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh)) \
+         : (k_tri_sweep<false, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh)))
   if (rh.n <= 1) SWEEP(1);
   else if (rh.n <= 4) SWEEP(4);
   else if (rh.n <= 8) SWEEP(8);

@@ -59,8 +59,8 @@ hipError_t launch_tri_block(hipStream_t, bool, int64_t, const FrontTile*, int, i
                             const double*, double*, double*, Rhs);
 hipError_t launch_bwd_u12(hipStream_t, int64_t, const FrontTile*, int, const SNode*, const int32_t*,
                           const double*, const double*, double*, Rhs);
-hipError_t launch_tri_sweep(hipStream_t, bool, int64_t, const FrontTile*, int, int32_t*, double*, int32_t*,
-                            const SNode*, const double*, double*, double*, Rhs);
+hipError_t launch_tri_sweep(hipStream_t, bool, int64_t, const FrontTile*, int, unsigned long long*, int32_t*, double*,
+                            int32_t*, const SNode*, const double*, double*, double*, Rhs);
 hipError_t launch_fwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                       const int32_t*, const double*, double*, double*, Rhs);
 hipError_t launch_bwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*,
@@ -350,8 +350,9 @@ struct smlu_handle {
   DBuf<XContrib> xtasks;
   DBuf<int2> aents;
   DBuf<FrontTile> ftiles;
-  DBuf<int32_t> ssync, sstatus;   // sync-free solve sweeps: tickets + block flags (zeroed per solve); timeouts
-  DBuf<double> sxh;               // sweep hand-off slots: 64 x kMultiRhs doubles per flag
+  DBuf<int32_t> ssync, sstatus;   // sync-free solve sweeps: block flags (epochs, never reset); timeouts
+  DBuf<unsigned long long> stick; // ... one monotone ticket counter per sweep launch
+  DBuf<double> sxh;               // ... hand-off slots: 64 x kMultiRhs doubles per flag
   int64_t ssync_n = 0;
   DBuf<GemmTask> gtasks;
   DBuf<SwapTask> stasks;
@@ -446,6 +447,7 @@ struct smlu_handle {
     ftiles.free();
     ssync.free();
     sstatus.free();
+    stick.free();
     sxh.free();
     gtasks.free();
     stasks.free();
@@ -1667,7 +1669,7 @@ static int build_schedule(smlu_handle* h) {
   // large fronts: one sync-free sweep launch per level and direction (default) or one launch per
   // 64-column block (SMLU_SOLVE_STEPS=1, the previous schedule)
   const bool sweep_solve = !(std::getenv("SMLU_SOLVE_STEPS") && std::atoi(std::getenv("SMLU_SOLVE_STEPS")) == 1);
-  int64_t ssync_n = 1;   // [0] unused
+  int64_t ssync_n = 0, ntick = 0;   // flags and ticket counters of the sweep launches
   static const int64_t big_work = [] {
     const char* e = std::getenv("SMLU_SOLVE_BIGWORK");   // dev knob (sweeps)
     return e ? std::atoll(e) : kSolveBigWork;
@@ -1728,6 +1730,7 @@ static int build_schedule(smlu_handle* h) {
         B.kind = K_SWEEPB;
         F.off = (int64_t)ft.size();
         F.aux = ssync_n;
+        F.aux2 = ntick++;
         int64_t wf = 0;
         int32_t fb = 0;
         for (auto s : bigs) {
@@ -1738,10 +1741,11 @@ static int build_schedule(smlu_handle* h) {
         }
         F.cnt = (int64_t)bigs.size();
         F.nwg = wf;
-        ssync_n += 1 + fb;
+        ssync_n += fb;
         h->fwd.push_back(F);
         B.off = (int64_t)ft.size();
         B.aux = ssync_n;
+        B.aux2 = ntick++;
         int64_t wb = 0;
         fb = 0;
         for (auto s : bigs) {
@@ -1753,7 +1757,7 @@ static int build_schedule(smlu_handle* h) {
         }
         B.cnt = (int64_t)bigs.size();
         B.nwg = wb;
-        ssync_n += 1 + fb;
+        ssync_n += fb;
         bl.push_back(U);
         bl.push_back(B);
         bwd_levels.push_back(bl);
@@ -2033,9 +2037,14 @@ static int build_schedule(smlu_handle* h) {
   HIPCHK(h->aents.upload(ae.data(), ae.size(), st));
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
   h->ssync_n = ssync_n;
-  HIPCHK(h->ssync.alloc((size_t)ssync_n));
-  if (ssync_n > 1) HIPCHK(h->sxh.alloc((size_t)ssync_n * 64 * kMultiRhs));
-  HIPCHK(hipMemsetAsync(h->ssync.p, 0, sizeof(int32_t) * ssync_n, st));
+  if (ssync_n > 0) {   // zeroed once per schedule: the sweeps never reset them (epochs, kernels_solve.hip)
+    HIPCHK(h->ssync.alloc((size_t)ssync_n));
+    HIPCHK(h->stick.alloc((size_t)ntick));
+    HIPCHK(h->sxh.alloc((size_t)ssync_n * 64 * kMultiRhs));
+    HIPCHK(hipMemsetAsync(h->ssync.p, 0, sizeof(int32_t) * ssync_n, st));
+    HIPCHK(hipMemsetAsync(h->stick.p, 0, sizeof(unsigned long long) * ntick, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
   if (!h->sstatus.p) {
     HIPCHK(h->sstatus.alloc(1));
     HIPCHK(hipMemsetAsync(h->sstatus.p, 0, sizeof(int32_t), st));
@@ -2491,6 +2500,7 @@ static void release_schedule(smlu_handle* h) {
   h->aents.free();
   h->ftiles.free();
   h->ssync.free();
+  h->stick.free();
   h->sxh.free();
   h->gtasks.free();
   h->stasks.free();
@@ -2571,8 +2581,9 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, d
                             rh);
     case K_SWEEPF:
     case K_SWEEPB:
-      return launch_tri_sweep(st, L.kind == K_SWEEPB, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->ssync.p + L.aux,
-                              h->sxh.p + L.aux * 64 * kMultiRhs, h->sstatus.p, h->sn.p, h->store.p, w, v, rh);
+      return launch_tri_sweep(st, L.kind == K_SWEEPB, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->stick.p + L.aux2,
+                              h->ssync.p + L.aux, h->sxh.p + L.aux * 64 * kMultiRhs, h->sstatus.p, h->sn.p, h->store.p,
+                              w, v, rh);
     case K_BWDU12C:
       return launch_bwd_u12_cols(st, h->sn.p, L.node, h->hsn[L.node].ns, L.aux, L.aux2, (int)L.cnt, h->rows.p,
                                  h->store.p, w, h->vbuf.p);
@@ -2621,9 +2632,6 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
     return (int)SMLU_OK;
   };
   auto sweeps = [&]() {
-    // tickets and block flags of the sync-free sweeps start from zero in every solve
-    if (h->ssync_n > 1 && hipMemsetAsync(h->ssync.p, 0, sizeof(int32_t) * h->ssync_n, st) != hipSuccess)
-      return fail(h, SMLU_ERR_HIP, "memset of the solve sweep flags failed");
     if (mode != 2) {
       int rc = run_seq(h->fwd, h->fwd_seg, h->fwd_comm);
       if (rc != SMLU_OK) return rc;
