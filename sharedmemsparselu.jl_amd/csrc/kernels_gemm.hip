@@ -27,6 +27,19 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t b, int64_t nwg) {
   const int64_t q = nwg >> 3, r = nwg & 7, x = b & 7;
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
 }
+// Windowed XCD-aware placement for launches whose tasks differ in cost (the batched F22 updates:
+// thousands of small-k tasks next to a few large-k ones).  Blocks are dealt round-robin to the 8
+// XCDs and roughly 512 run at a time (256 CUs x 2), so within each window of 512 blocks the 64 of
+// one XCD take 64 consecutive tiles (one 8 x 8 group of tile_rc: shared A and B panels in that L2),
+// while consecutive groups go to different XCDs: every XCD gets a share of every task.  (xcd_remap's
+// one contiguous range per XCD left XCDs idle behind the large-k tasks.)  Bijective; a partial last
+// window keeps dispatch order.
+__device__ __forceinline__ int64_t xcd_window_remap(int64_t b, int64_t nwg) {
+  constexpr int64_t W = 512;
+  if (b >= (nwg / W) * W) return b;
+  const int64_t w0 = b - b % W, i = b % W;
+  return w0 + (i & 7) * (W / 8) + (i >> 3);
+}
 template <int TS>
 __device__ __forceinline__ void tile_rc(const GemmTask& t, int64_t tl, int& tm, int& tn) {
   constexpr int GM = 8;
@@ -758,9 +771,7 @@ template <bool TRSM>
 __global__ __launch_bounds__(256, 2) void k_gemm128_mfma2(const GemmTask* __restrict__ tasks, int ntask,
                                                           GrowthArgs ga) {
   __shared__ __attribute__((aligned(16))) double lds[sizeof(Mfma2Lds) / sizeof(double)];
-  // XCD-aware: the workgroups of one XCD take one contiguous range of tiles, so the 8 x 8 tile
-  // groups of tile_rc run side by side in one L2 and share their A and B panels there
-  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t b = xcd_window_remap(blockIdx.x, gridDim.x);
   const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
   int tm, tn;
   tile_rc<HBM_>(t, b - t.tile0, tm, tn);

@@ -582,20 +582,18 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
   double o[NR];
 #pragma unroll
   for (int r = 0; r < NR; ++r) o[r] = (has && r < nr) ? v[r * rh.ldv + row] : 0.0;
-  // the diagonal block's row of a pivot row, loaded up front (off the chain's critical path); in
-  // the forward sweep the update rows sharing a wave with the last (partial) pivot block take
-  // that block's columns in the chain too
+  // the diagonal block's row of a pivot row, loaded up front (off the chain's critical path)
   double drow[64];
   double dinv = 1.0;
   {
-    const int64_t b = UPPER ? myblk : row / 64;
-    const bool inb = has && b < nblk;
-    const int bw = (int)min<int64_t>(64, ns - 64 * (inb ? b : 0));
+    const bool piv = has && myblk < nblk;
+    const int64_t b = piv ? myblk : 0;
+    const int bw = (int)min<int64_t>(64, ns - 64 * b);
     const int li = (int)(row - 64 * b);
 #pragma unroll
     for (int j = 0; j < 64; ++j)
-      drow[j] = (inb && j < bw && (UPPER ? j > li : j < li)) ? Lp[(64 * b + j) * M + row] : 0.0;
-    if (UPPER && inb) dinv = recip(Lp[(64 * b + li) * M + row]);
+      drow[j] = (piv && j < bw && (UPPER ? j > li : j < li)) ? Lp[(64 * b + j) * M + row] : 0.0;
+    if (UPPER && piv) dinv = recip(Lp[(64 * b + li) * M + row]);
   }
   double d[64];   // my row of the column block being applied, loaded before its x is available
   auto load_tile = [&](int64_t c, int bw) {
@@ -633,7 +631,10 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
     const int64_t b = UPPER ? nblk - 1 - 4 * q - t : 4 * q + t;
     if (b < 0 || b >= nblk) break;
     const int bw = (int)min<int64_t>(64, ns - 64 * b);
-    if (wv > t && has) load_tile(b, bw);
+    // rows that apply block b: the waves beyond t, and the update rows of wave t when block b is
+    // the last, partial one (forward): same per-block arithmetic as every other row
+    const bool applies = has && (wv > t || (wv == t && myblk >= nblk));
+    if (applies) load_tile(b, bw);
     if (wv == t) {
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
@@ -653,7 +654,7 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
     }
     __syncthreads();
     if (tid == 0) (void)__hip_atomic_fetch_max(flags + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (wv > t && has) fma_tile(bw);
+    if (applies) fma_tile(bw);
     __syncthreads();
   }
   // forward: the update rows leave their value for the parent

@@ -359,6 +359,7 @@ struct smlu_handle {
   DBuf<XCol> xcols;
   // schedule
   std::vector<Launch> fac, fwd, bwd;
+  std::vector<Launch> fwdm, bwdm;   // one GPU, batched right-hand sides: per-block launches instead of sweeps
   std::vector<SNode> hsn;
   double gemm_flops = 0, gemm22_flops = 0, dense_flops = 0;
   int64_t gemm_launches = 0, gemm128_launches = 0;
@@ -2035,6 +2036,46 @@ static int build_schedule(smlu_handle* h) {
   HIPCHK(h->ilist.upload(ilist.data(), ilist.size(), st));
   HIPCHK(h->xtasks.upload(xt.data(), xt.size(), st));
   HIPCHK(h->aents.upload(ae.data(), ae.size(), st));
+  // batched right-hand sides (one GPU): the sweep's single chain wave per block would run the NR
+  // chains one after another, so batches keep the per-64-column-block launches (k_tri_block: the
+  // diagonal block solved by four chain waves for four right-hand sides at a time)
+  h->fwdm.clear();
+  h->bwdm.clear();
+  if (h->nranks == 1) {
+    auto expand = [&](const Launch& S, bool upper, std::vector<Launch>& out) {
+      std::vector<int32_t> fr;
+      for (int64_t i = S.off; i < S.off + S.cnt; ++i) fr.push_back(ft[i].s);
+      int64_t nb = 0;
+      for (auto s : fr) nb = std::max<int64_t>(nb, (h->hsn[s].ns + 63) / 64);
+      for (int64_t t = 0; t < nb; ++t) {
+        Launch F;
+        F.kind = upper ? K_TRIB : K_TRIF;
+        F.step = (int)t;
+        F.off = (int64_t)ft.size();
+        int64_t w = 0, cnt = 0;
+        for (auto s : fr) {
+          const SNode& r = h->hsn[s];
+          const int64_t nbs = (r.ns + 63) / 64, M = (int64_t)r.ns + r.nu;
+          if (t >= nbs) continue;
+          const int64_t jb = upper ? (nbs - 1 - t) * 64 : t * 64, bw = std::min<int64_t>(64, r.ns - jb);
+          ft.push_back(FrontTile{s, 0, w});
+          w += upper ? std::max<int64_t>(1, (jb + 255) / 256) : std::max<int64_t>(1, (M - jb - bw + 255) / 256);
+          ++cnt;
+        }
+        F.cnt = cnt;
+        F.nwg = w;
+        out.push_back(F);
+      }
+    };
+    for (const Launch& L : h->fwd) {
+      if (L.kind == K_SWEEPF) expand(L, false, h->fwdm);
+      else h->fwdm.push_back(L);
+    }
+    for (const Launch& L : h->bwd) {
+      if (L.kind == K_SWEEPB) expand(L, true, h->bwdm);
+      else h->bwdm.push_back(L);
+    }
+  }
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
   h->ssync_n = ssync_n;
   if (ssync_n > 0) {   // zeroed once per schedule: the sweeps never reset them (epochs, kernels_solve.hip)
@@ -2632,12 +2673,14 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
     return (int)SMLU_OK;
   };
   auto sweeps = [&]() {
+    const bool batch = rh.n > 1 && h->nranks == 1;
+    static const std::vector<size_t> seg0(1, 0);
     if (mode != 2) {
-      int rc = run_seq(h->fwd, h->fwd_seg, h->fwd_comm);
+      int rc = batch ? run_seq(h->fwdm, seg0, h->fwd_comm) : run_seq(h->fwd, h->fwd_seg, h->fwd_comm);
       if (rc != SMLU_OK) return rc;
     }
     if (mode != 1) {
-      int rc = run_seq(h->bwd, h->bwd_seg, h->bwd_comm);
+      int rc = batch ? run_seq(h->bwdm, seg0, h->bwd_comm) : run_seq(h->bwd, h->bwd_seg, h->bwd_comm);
       if (rc != SMLU_OK) return rc;
     }
     return (int)SMLU_OK;

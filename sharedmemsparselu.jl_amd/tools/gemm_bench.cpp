@@ -13,12 +13,15 @@ using namespace smlu;
 static void fill(std::vector<double>& v, unsigned seed) { srand(seed); for (auto& x : v) x = rand() / (double)RAND_MAX - 0.5; }
 
 int main(int argc, char** argv) {
-  struct Shape { int m, n, k; } shapes[] = {{4096, 4096, 4096}, {8192, 8192, 1024}, {16384, 16384, 64}, {12000, 12000, 6000}, {1000, 1000, 300}, {300, 5000, 32}, {777, 1333, 129},
+  struct Shape { int m, n, k, lda = 0, ldb = 0, ldc = 0; } shapes[] = {{4096, 4096, 4096}, {8192, 8192, 1024}, {16384, 16384, 64}, {12000, 12000, 6000}, {1000, 1000, 300}, {300, 5000, 32}, {777, 1333, 129},
                                             {18000, 192, 64}, {192, 18000, 64}, {6000, 6000, 256}, {3000, 3000, 256}, {1500, 1500, 1000}, {18000, 256, 256}};
   std::vector<Shape> sv(std::begin(shapes), std::end(shapes));
   if (argc > 1) {   // shapes from the command line: m,n,k ...
     sv.clear();
-    for (int a = 1; a < argc; ++a) { Shape x; if (sscanf(argv[a], "%d,%d,%d", &x.m, &x.n, &x.k) == 3) sv.push_back(x); }
+    for (int a = 1; a < argc; ++a) {   // m,n,k or m,n,k,lda,ldb,ldc
+      Shape x;
+      if (sscanf(argv[a], "%d,%d,%d,%d,%d,%d", &x.m, &x.n, &x.k, &x.lda, &x.ldb, &x.ldc) >= 3) sv.push_back(x);
+    }
   }
   // variants: tile codes of launch_gemm (GB_TILES="129,130"); the first one is the reference
   std::vector<int> tiles_list = {64, 128, 129};
@@ -30,7 +33,8 @@ int main(int argc, char** argv) {
   hipStream_t st; CK(hipStreamCreate(&st));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (auto sh : sv) {
-    int m = sh.m, n = sh.n, k = sh.k, lda = m + 3, ldb = k + 1, ldc = m + 5;
+    int m = sh.m, n = sh.n, k = sh.k, lda = sh.lda ? sh.lda : m + 3, ldb = sh.ldb ? sh.ldb : k + 1,
+        ldc = sh.ldc ? sh.ldc : m + 5;
     std::vector<double> hA((size_t)lda * k), hB((size_t)ldb * n), hC((size_t)ldc * n);
     fill(hA, 1); fill(hB, 2); fill(hC, 3);
     double *A, *B, *C1, *C2; GemmTask* dt;
@@ -65,7 +69,7 @@ int main(int argc, char** argv) {
       float ms; CK(hipEventElapsedTime(&ms, e0, e1));
       res[variant] = 2.0 * m * n * (double)k * reps / (ms * 1e-3) / 1e12;
     }
-    printf("m=%6d n=%6d k=%6d ", m, n, k);
+    printf("m=%6d n=%6d k=%6d ld=%d,%d,%d ", m, n, k, lda, ldb, ldc);
     for (int v = 0; v < NV; ++v) printf(" t%d %6.2f TF (maxdiff vs t%d %.1e)", tiles_list[v], res[v], tiles_list[0], vdiff[v]);
     printf("\n");
     CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C1)); CK(hipFree(C2)); CK(hipFree(dt));

@@ -15,7 +15,7 @@ tr.sort(key=lambda x: int(x["Start_Timestamp"]))
 # first factorization only: up to the first k_perm_in (a solve) or the end
 g_tr = [x for x in tr if "k_gemm" in x["Kernel_Name"] or x["Kernel_Name"].startswith("Cijk")]
 sched = [r for r in csv.DictReader(open(sys.argv[2])) if r["name"] in ("gemm", "gemm22", "gemmu", "gemmo", "trsm")
-         and int(r["tile"]) in (64, 65, 128, 129, 200)]
+         and int(r["tile"]) in (64, 65, 128, 129, 130, 200)]
 n = min(len(g_tr), len(sched))
 print(f"trace gemm dispatches {len(g_tr)}, schedule gemm launches {len(sched)}; joining {n}")
 rows = []

@@ -1,0 +1,9 @@
+# per-dispatch GEMM report of one eager 128^3 factorization with the hand-written tiles only
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+export SMLU_NO_ROCBLAS=1
+bash tools/run_gemm_trace.sh r3f || { tail -20 gpurun_out/r3f.log; exit 1; }
+f=$(ls gpurun_out/r3f/*kernel_trace.csv 2>/dev/null | head -1)
+[ -z "$f" ] && f=$(find gpurun_out/r3f -name '*kernel_trace.csv' | head -1)
+python3 tools/gemm_dispatch_report.py $f gpurun_out/r3f_sched.csv > gpurun_out/r3f_report.txt 2>&1
+head -40 gpurun_out/r3f_report.txt
