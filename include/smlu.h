@@ -66,10 +66,11 @@ typedef struct smlu_opts {
                              when the last factorization flagged weak pivots (the pivot-failure
                              fallback of the diagonal-tile pivoting); 0 = never;
                              k > 0 = up to k steps (stops when the residual stops halving) */
-    int32_t vendor_gemm;  /* 1 (default) = the large plain Schur-update GEMMs (F22 -= L21*U12 and
-                             the trailing updates of the big fronts, one front per call) go to
-                             rocBLAS dgemm in deterministic mode (atomics off) when librocblas is
-                             present; 0 (or env SMLU_NO_ROCBLAS) = hand-written MFMA tile only */
+    int32_t vendor_gemm;  /* 0 (default) = every GEMM runs on the hand-written MFMA tiles;
+                             1 (or env SMLU_ROCBLAS) = the large plain Schur-update GEMMs
+                             (F22 -= L21*U12 and the trailing updates of the big fronts, one
+                             front per call) go to rocBLAS dgemm in deterministic mode (atomics
+                             off) when librocblas is present (a comparison path, not faster) */
 } smlu_opts;
 
 typedef struct smlu_handle smlu_handle;

@@ -2856,7 +2856,8 @@ void smlu_default_opts(smlu_opts* o) {
   o->leaf_size = 64;
   o->use_mfma = std::getenv("SMLU_VALU_GEMM") ? 0 : 1;   // fp64 MFMA by default
   o->refine = -1;
-  o->vendor_gemm = std::getenv("SMLU_NO_ROCBLAS") ? 0 : 1;
+  // hand-written MFMA tiles by default; rocBLAS only on request (comparison path)
+  o->vendor_gemm = (std::getenv("SMLU_ROCBLAS") && !std::getenv("SMLU_NO_ROCBLAS")) ? 1 : 0;
 }
 
 int smlu_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
