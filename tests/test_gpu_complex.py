@@ -210,13 +210,16 @@ def _check_complex_factors(A, F):
     """F.L, F.U, F.p, F.q, F.Rs of a complex handle are complex n x n (the reference's
     SparseMatrixCSC{ComplexF64}, src/SharedMemSparseLU.jl:47-52): UMFPACK's conventions (L unit
     diagonal stored first, U diagonal last, rows sorted) and L*U == (Rs.*A)[p, q]; they fold the
-    real-equivalent factors exactly (Rs of complex row i = Rs of K's rows 2i and 2i+1)."""
+    real-equivalent factors exactly (Rs of complex row i = Rs of K's row 2i; row 2i+1 agrees to rounding)."""
     L, U, p, q, Rs = F.L, F.U, F.p, F.q, F.Rs
     n = A.shape[0]
     assert L.dtype == np.complex128 and U.dtype == np.complex128 and L.shape == (n, n)
     fk = F.real_equivalent_factors()
     assert np.array_equal(p, fk["p"][0::2] // 2) and np.array_equal(q, fk["q"][0::2] // 2)
-    assert np.array_equal(Rs, fk["Rs"][0::2]) and np.array_equal(fk["Rs"][0::2], fk["Rs"][1::2])
+    assert np.array_equal(Rs, fk["Rs"][0::2])
+    # K's rows 2i and 2i+1 sum the same magnitudes |Re a_ij|, |Im a_ij| in swapped order per j:
+    # equal to the last bits only
+    assert np.allclose(fk["Rs"][0::2], fk["Rs"][1::2], rtol=1e-14, atol=0)
     for j in range(n):
         li = L.indices[L.indptr[j]:L.indptr[j + 1]]
         ui = U.indices[U.indptr[j]:U.indptr[j + 1]]
@@ -234,7 +237,12 @@ def test_complex_factor_export(gpu, case):
         A = helmholtz3d(12, shift=0.5)
     elif case == "dominant":
         R = mats.random_dominant(300, 0.02, seed=9).astype(np.complex128)
-        R.data = R.data * np.exp(1j * rng.random(R.nnz) * 2 * np.pi)
+        # random phases off the diagonal only: a diagonal entry near the imaginary axis makes the
+        # real-equivalent 2x2 block [[a, -b], [b, a]] swap its rows (|b| > 10|a|), which splits
+        # the pair (covered by the "fe" case and test_imaginary_diagonal*)
+        R = sp.coo_matrix(R)
+        off = R.row != R.col
+        R.data[off] = R.data[off] * np.exp(1j * rng.random(off.sum()) * 2 * np.pi)
         A = sp.csc_matrix(R)
     else:
         A = complex_fe(rng, 20)
