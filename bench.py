@@ -336,7 +336,7 @@ def main():
         vals.append(v)
     torch.cuda.synchronize()
 
-    kinds = ["gemm", "gemmu", "gemmo", "gemm22", "panel", "trsm", "small", "assemble", "memset"]
+    kinds = ["gemm", "gemmu", "gemmo", "gemm22", "panel", "trsm", "urows", "small", "assemble", "memset"]
     kind_ms = {k: 0.0 for k in kinds}
 
     def step(r):
@@ -435,6 +435,7 @@ def main():
                                  "stream); traffic = HBM bytes per launch from rocprofv3 PMC "
                                  "(FETCH_SIZE x2 + WRITE_SIZE, " + traffic_src + ")"},
             "kernel_ms_per_step": {k: v / K for k, v in kind_ms.items()},
+            "launches_per_refactor": F.stat("launches"),
             # per-kind HIP-event times exist for the single-GPU path only (partitioned: None)
             "gemm_split": ({"panel_tflops": (gemm_flops - F.stat("gemm22_flops")) / ((kind_ms["gemm"] + kind_ms["gemmu"] + kind_ms["gemmo"]) / K) / 1e9,
                             "f22_tflops": F.stat("gemm22_flops") / (kind_ms["gemm22"] / K) / 1e9,

@@ -617,6 +617,94 @@ __global__ __launch_bounds__(64) void k_panel_wave(const int32_t* __restrict__ l
   }
 }
 
+// Tail of the fused panel (k_panel_blk<NWV, true>): the finished tile (x, row positions pos)
+// goes to LDS as k_tri_inv reads it from HBM ([col][row], ld 65, identity outside w x w), wave v
+// forms columns 4v..4v+3 of NL = I - L^-1 and of NU = I - U^-1 with k_tri_inv's arithmetic, and
+// the outer block's other columns [ostart, oend) \ [kb, kb+w) get the tile's row interchanges
+// (every moved row read into registers, one barrier, then written to its new position).
+template <int NWV, int CW>
+__device__ __forceinline__ void panel_fused_tail(const double (&x)[CW], int pos, bool has, int w, int kb,
+                                                 int64_t M, const FrontPtrs& f, const SNode& s, int64_t slot,
+                                                 double* __restrict__ tinv, int ob, int lane, int wv) {
+  static_assert(NWV == 16 && CW == 4, "fused panel: 16 waves, 4 columns each");
+  __shared__ double sD[64 * 65];
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < 4096; idx += 64 * NWV) {
+    const int i = idx & 63, j = idx >> 6;
+    if (i >= w || j >= w) sD[j * 65 + i] = i == j ? 1.0 : 0.0;
+  }
+  if (has) {
+#pragma unroll
+    for (int j = 0; j < CW; ++j) {
+      const int c = wv * CW + j;
+      if (c < w) sD[c * 65 + pos] = x[j];
+    }
+  }
+  // row interchanges of the outer block's other columns: read every moved row first
+  const int ostart = (kb / ob) * ob, oend = min((int)f.ns, ostart + ob);
+  const int nother = oend - ostart - w;
+  const bool moved = has && pos != lane;
+  constexpr int kMaxCols = 20;   // (OB - 64) / NWV columns per wave for OB <= 384
+  double mv[kMaxCols];
+#pragma unroll
+  for (int q = 0; q < kMaxCols; ++q) {
+    const int cj = wv + NWV * q;
+    if (moved && cj < nother) {
+      const int col = ostart + cj + (ostart + cj >= kb ? w : 0);
+      mv[q] = f.L[(int64_t)col * M + kb + lane];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kMaxCols; ++q) {
+    const int cj = wv + NWV * q;
+    if (moved && cj < nother) {
+      const int col = ostart + cj + (ostart + cj >= kb ? w : 0);
+      f.L[(int64_t)col * M + kb + pos] = mv[q];
+    }
+  }
+  // tile inverses (k_tri_inv, parts 0-3 -> NL, 4-7 -> NU; here wave v = part*4 + wave)
+  const int c0 = wv * 4;
+  double* out = tinv + slot * 8192;
+  {
+    double z[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) z[r] = lane == c0 + r ? 1.0 : 0.0;
+#pragma unroll 4
+    for (int j = 0; j < 63; ++j) {
+      const double lij = sD[j * 65 + lane];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double zj = readlane_f64(z[r], j);
+        if (lane > j) z[r] = fma(-lij, zj, z[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out[(int64_t)(c0 + r) * 64 + lane] = lane > c0 + r ? -z[r] : 0.0;
+  }
+  {
+    double z[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) z[r] = lane == c0 + r ? 1.0 : 0.0;
+    const double rd = recip(sD[lane * 65 + lane]);
+#pragma unroll 4
+    for (int j = 63; j >= 0; --j) {
+      const double uij = sD[j * 65 + lane];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (lane == j) z[r] *= rd;
+        const double yj = readlane_f64(z[r], j);
+        if (lane < j) z[r] = fma(-uij, yj, z[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = c0 + r;
+      out[4096 + (int64_t)c * 64 + lane] = lane == c ? 1.0 - z[r] : (lane < c ? -z[r] : 0.0);
+    }
+  }
+}
+
 // Column-block variant of k_panel_cols (the default for 64-wide panels): wave w owns the
 // CW = 64/NWV consecutive columns [w*CW, (w+1)*CW) in registers (lane = candidate row).  The
 // owner of a block factors its CW columns wave-locally -- pivot search, scaling, rank-1 updates
@@ -625,7 +713,12 @@ __global__ __launch_bounds__(64) void k_panel_wave(const int32_t* __restrict__ l
 // rank-1 updates to its columns in column order, and every wave replays the transpositions.
 // One barrier per CW columns instead of one per column.  Same pivot choices and the same
 // element-wise FMAs in the same order as k_panel_cols (bitwise-identical panel).
-template <int NWV>
+//
+// FUSED = true (GEMM-form fronts, nb = 64): the same panel, then in the same workgroup the two
+// tile inverses k_tri_inv computes (same per-column arithmetic: bitwise-identical NL/NU in the
+// same tinv slot) and the row interchanges of the outer block's other columns that k_laswp
+// applies inside the block -- two launches fewer per inner step of the blocked fronts.
+template <int NWV, bool FUSED>
 __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restrict__ list, int step,
                                                         const SNode* __restrict__ sn,
                                                         double* __restrict__ store,
@@ -634,7 +727,8 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
                                                         int32_t* __restrict__ swaps,
                                                         int64_t swap_stride,
                                                         int32_t* __restrict__ info,
-                                                        double* __restrict__ growth, double diag_tol) {
+                                                        double* __restrict__ growth, double diag_tol,
+                                                        double* __restrict__ tinv, int ob) {
   constexpr int CW = 64 / NWV;
   __shared__ double s_l[2][CW][64];
   __shared__ int s_p[2][CW];
@@ -751,6 +845,7 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
     s_flag[wv] = flag;
     s_err[wv] = err;
   }
+  if constexpr (FUSED) panel_fused_tail<NWV, CW>(x, pos, has, w, kb, M, f, s, list[2 * blockIdx.x + 1], tinv, ob, lane, wv);
   __syncthreads();
   if (wv != 0) return;
   int32_t* rp = rowperm + s.first + kb;
@@ -1338,7 +1433,7 @@ hipError_t launch_panel1(hipStream_t st, int cnt, int lds_doubles, int rmax, int
                          const int32_t* list,
                          const SNode* sn, double* store, double* scratch, int32_t* rowperm,
                          int32_t* swaps, int64_t swap_stride, int32_t* info, double* growth,
-                         double diag_tol) {
+                         double diag_tol, double* fused_tinv, int ob) {
   if (cnt <= 0) return hipSuccess;
   size_t lds = (size_t)lds_doubles * sizeof(double);
 #define PANEL1_ARGS list, step, sn, store, scratch, rowperm, swaps, swap_stride, info, growth, diag_tol
@@ -1355,8 +1450,12 @@ hipError_t launch_panel1(hipStream_t st, int cnt, int lds_doubles, int rmax, int
     const char* e = std::getenv("SMLU_PANEL_BLK");
     return e ? std::atoi(e) : 16;
   }();
-  if (wmax > 32 && !lds_panel && blk_waves == 16) k_panel_blk<16><<<cnt, 1024, 0, st>>>(PANEL1_ARGS);
-  else if (wmax > 32 && !lds_panel && blk_waves == 8) k_panel_blk<8><<<cnt, 512, 0, st>>>(PANEL1_ARGS);
+  if (fused_tinv) {   // GEMM-form fronts: panel + tile inverses + in-block row interchanges
+    if (wmax <= 32 || ob > 64 + 16 * 20) return hipErrorInvalidValue;
+    k_panel_blk<16, true><<<cnt, 1024, 0, st>>>(PANEL1_ARGS, fused_tinv, ob);
+  }
+  else if (wmax > 32 && !lds_panel && blk_waves == 16) k_panel_blk<16, false><<<cnt, 1024, 0, st>>>(PANEL1_ARGS, nullptr, 0);
+  else if (wmax > 32 && !lds_panel && blk_waves == 8) k_panel_blk<8, false><<<cnt, 512, 0, st>>>(PANEL1_ARGS, nullptr, 0);
   else if (wmax > 32 && !lds_panel && cols_waves == 16) k_panel_cols<16><<<cnt, 1024, 0, st>>>(PANEL1_ARGS);
   else if (wmax > 32 && !lds_panel && cols_waves == 8) k_panel_cols<8><<<cnt, 512, 0, st>>>(PANEL1_ARGS);
   else if (wmax > 32 && !lds_panel && cols_waves == 4) k_panel_cols<4><<<cnt, 256, 0, st>>>(PANEL1_ARGS);

@@ -163,21 +163,14 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
 // GEMM-form triangular solves): the whole K extent of the A and B tiles is staged in one shot
 // (32 loads per thread in flight together with the 16 C loads), so a launch pays one memory
 // round trip instead of one per 16-deep slice.  Same per-element arithmetic as k_gemm.
-template <bool TRSM>
-__global__ __launch_bounds__(256) void k_gemm_k64(const GemmTask* __restrict__ tasks, int ntask, GrowthArgs ga) {
-  __shared__ double As[64][GBM + 2];   // [k][row]
-  __shared__ double Bs[64][GBN + 2];   // [k][col], negated
-  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
-  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
-  const gdbl* gA = gbl(t.A);
-  const gdbl* gB = gbl(t.B);
-  gdbl* gC = gbl(t.C);
-  int tm, tn;
-  tile_rc<GBM>(t, b - t.tile0, tm, tn);
-  const int m0 = tm * GBM, n0 = tn * GBN;
+// One 64 x 64 output tile [m0, m0+64) x [n0, n0+64) of an m x n task (k <= 64), by the whole
+// 256-thread workgroup; returns the thread's max |result| (growth epilogue of the TRSM form).
+// All loads (C, A, B) complete before the first store, so B == C (in place) is allowed.
+__device__ __forceinline__ double k64_tile(const gdbl* gA, int lda, const gdbl* gB, int ldb, gdbl* gC, int ldc,
+                                           int m, int n, int K, int m0, int n0,
+                                           double (&As)[64][GBM + 2], double (&Bs)[64][GBN + 2]) {
   const int tid = threadIdx.x;
   const int tx = tid & 15, ty = tid >> 4;
-  const int K = t.k;
   double acc[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -185,7 +178,7 @@ __global__ __launch_bounds__(256) void k_gemm_k64(const GemmTask* __restrict__ t
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = m0 + tx + 16 * i;
-      acc[i][j] = (col < t.n && row < t.m) ? gC[(int64_t)col * t.ldc + row] : 0.0;
+      acc[i][j] = (col < n && row < m) ? gC[(int64_t)col * ldc + row] : 0.0;
     }
   }
   // A: row = tid & 63, k = (tid >> 6) + 4r;  B: k = tid & 63, col = (tid >> 6) + 4r
@@ -194,9 +187,9 @@ __global__ __launch_bounds__(256) void k_gemm_k64(const GemmTask* __restrict__ t
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int kk = ak + 4 * r, row = m0 + ar;
-    ra[r] = (row < t.m && kk < K) ? gA[(int64_t)kk * t.lda + row] : 0.0;
+    ra[r] = (row < m && kk < K) ? gA[(int64_t)kk * lda + row] : 0.0;
     const int col = n0 + ak + 4 * r;
-    rb[r] = (col < t.n && ar < K) ? gB[(int64_t)col * t.ldb + ar] : 0.0;
+    rb[r] = (col < n && ar < K) ? gB[(int64_t)col * ldb + ar] : 0.0;
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -223,12 +216,25 @@ __global__ __launch_bounds__(256) void k_gemm_k64(const GemmTask* __restrict__ t
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = m0 + tx + 16 * i;
-      if (col < t.n && row < t.m) {
-        gC[(int64_t)col * t.ldc + row] = acc[i][j];
+      if (col < n && row < m) {
+        gC[(int64_t)col * ldc + row] = acc[i][j];
         gmax = fmax(gmax, fabs(acc[i][j]));
       }
     }
   }
+  return gmax;
+}
+
+template <bool TRSM>
+__global__ __launch_bounds__(256) void k_gemm_k64(const GemmTask* __restrict__ tasks, int ntask, GrowthArgs ga) {
+  __shared__ double As[64][GBM + 2];   // [k][row]
+  __shared__ double Bs[64][GBN + 2];   // [k][col], negated
+  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+  int tm, tn;
+  tile_rc<GBM>(t, b - t.tile0, tm, tn);
+  const double gmax = k64_tile(gbl(t.A), t.lda, gbl(t.B), t.ldb, gbl(t.C), t.ldc, t.m, t.n, t.k, tm * GBM,
+                               tn * GBN, As, Bs);
   if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
 }
 
@@ -786,6 +792,181 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma2(const GemmTask* __rest
 }
 
 // ------------------------------------------------------------------------------------
+// U rows of an outer block, fused (the end-of-block step of the GEMM-form fronts).  One
+// 256-thread workgroup per 64-column block of the columns right of the block (L-panel columns or
+// U12 columns) runs the whole sub-panel sequence on its columns; for each 64-row sub-panel u:
+//   T: C_u = L_uu^-1 C_u in GEMM form, C_u - NL_u C_u (NL_u = I - L_uu^-1, tinv slot0 + u);
+//   R: the rows below u inside the block, C_r -= L_ru C_u (k = 64), with -C_u kept in LDS.
+// These are exactly the K_TRSML + K_GEMMU tiles it replaces, with the same per-element
+// arithmetic (acc = C, then one fused multiply-add per k in ascending k: the fp64 MFMA does
+// them in order), so the factors are bitwise those of the per-sub-panel launches.  fp64 MFMA
+// 16x16x4 with the operands swapped (B fragment first) so that lane l holds rows (l & 15) of a
+// 16 x 16 block and C is read and written in 128-byte column runs; phase R's A fragments come
+// straight from HBM/L2 (one 8-byte load feeds 4 MFMAs), B from LDS.  One workgroup per CU
+// (4 waves, 20 accumulator blocks each in phase R).
+// ------------------------------------------------------------------------------------
+#ifndef KQR
+#define KQR 4     // k-quads of L fragments per round trip in phase R
+#endif
+#define ULDB 80   // LDS row stride of -C_u [k][col]: k, k+1 rows in opposite bank halves
+// Global accesses walk one per-lane pointer (a VGPR pair) per operand in steps of 4 columns,
+// the remaining offsets being instruction immediates; no branch around a load (values outside
+// the block are read and discarded by a select, row/column overruns stay inside the padded
+// allocation: kUrowsPad).  Loads beyond the last k-quad or row block are skipped wave-uniformly.
+// c ? x : +0.0 as a bit mask (keeps the compiler from sinking the load into a branch)
+__device__ __forceinline__ double sel0(bool c, double x) {
+  return __longlong_as_double(__double_as_longlong(x) & (c ? -1LL : 0LL));
+}
+__global__ __launch_bounds__(256, 1) void k_urows(const URowTask* __restrict__ tasks, const SNode* __restrict__ sn,
+                                                  double* __restrict__ store, const double* __restrict__ tinv) {
+  __shared__ double Bs[64 * ULDB];
+  const URowTask t = tasks[blockIdx.x];
+  const SNode s = sn[t.s];
+  const int64_t M = (int64_t)s.ns + s.nu;
+  const int64_t ld = t.ld;
+  const int nc = t.ncols;
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  gdbl* const C = gbl(store + t.coff);   // (row, col) at col * ld + row
+  const gdbl* const Lp = gbl(store + s.Loff);
+  for (int u = 0;; ++u) {
+    const int kbu = t.ob0 + 64 * u;
+    if (kbu >= t.ob1) break;
+    const int wu = min(64, t.ob1 - kbu);
+    const int nkq = (wu + 3) >> 2;
+    // stage -C_u (the B operand of phase T), zero outside wu x nc: wave wv stages columns wv + 4i
+    {
+      double v[16];
+      const gdbl* p = C + (int64_t)wv * ld + kbu + lane;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        v[i] = *p;
+        p += 4 * ld;
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) Bs[lane * ULDB + wv + 4 * i] = sel0(lane < wu && wv + 4 * i < nc, -v[i]);
+    }
+    // phase T: wave wv owns rows 32 (wv & 1) + [0, 32), columns 32 (wv >> 1) + [0, 32)
+    {
+      const int rb0 = 32 * (wv & 1), cb0 = 32 * (wv >> 1);
+      v4d acc[2][2];
+      {
+        gdbl* p = C + (int64_t)(cb0 + lk) * ld + kbu + rb0 + li;
+#pragma unroll
+        for (int c4 = 0; c4 < 8; ++c4) {   // columns cb0 + 4 c4 + lk = cb0 + 16 bj + lk + 4 r
+          const int bj = c4 >> 2, r = c4 & 3, col = cb0 + 4 * c4 + lk;
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi) {
+            const double x = p[16 * bi];
+            acc[bi][bj][r] = sel0(rb0 + 16 * bi + li < wu && col < nc, x);
+          }
+          p += 4 * ld;
+        }
+      }
+      double na[2][16];   // the wave's NL fragments for every k, one round trip
+      {
+        const gdbl* p = gbl(tinv + (int64_t)(t.slot0 + u) * 8192) + lk * 64 + rb0 + li;
+#pragma unroll
+        for (int kq = 0; kq < 16; ++kq) {
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi) {
+            const double x = p[16 * bi];
+            na[bi][kq] = sel0(rb0 + 16 * bi + li < wu && 4 * kq + lk < wu, x);
+          }
+          p += 256;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int kq = 0; kq < 16; ++kq) {
+        if (kq >= nkq) continue;
+        const int k = 4 * kq + lk;
+        double fb[2];
+#pragma unroll
+        for (int bj = 0; bj < 2; ++bj) fb[bj] = Bs[k * ULDB + cb0 + 16 * bj + li];
+#pragma unroll
+        for (int bi = 0; bi < 2; ++bi)
+#pragma unroll
+          for (int bj = 0; bj < 2; ++bj)
+            acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[bj], na[bi][kq], acc[bi][bj], 0, 0, 0);
+      }
+      __syncthreads();   // every wave is done reading the old -C_u
+      {
+        gdbl* p = C + (int64_t)(cb0 + lk) * ld + kbu + rb0 + li;
+#pragma unroll
+        for (int c4 = 0; c4 < 8; ++c4) {
+          const int bj = c4 >> 2, r = c4 & 3, col = cb0 + 4 * c4 + lk;
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi) {
+            const int row = rb0 + 16 * bi + li;
+            const double v = acc[bi][bj][r];
+            const bool in = row < wu && col < nc;
+            if (in) p[16 * bi] = v;
+            Bs[row * ULDB + col] = sel0(in, -v);
+          }
+          p += 4 * ld;
+        }
+      }
+      __syncthreads();
+    }
+    // phase R: rows [kbu + wu, ob1) in 16-row blocks; wave wv takes blocks wv, wv + 4, ... one at
+    // a time (4 accumulator blocks: the 64 columns), the next block's C and L fragments in flight
+    // while the current one's 64 MFMAs run
+    const int r0 = kbu + wu, mr = t.ob1 - r0;
+    const int nrb = (mr + 15) >> 4;
+    if (wv < nrb) {
+      v4d cc[4], cn[4];
+      double fa[16], fan[16];
+      auto load_blk = [&](int rb, v4d (&c)[4], double (&f)[16]) {
+        const gdbl* p = C + (int64_t)lk * ld + r0 + 16 * rb + li;
+#pragma unroll
+        for (int c4 = 0; c4 < 16; ++c4) {
+          c[c4 >> 2][c4 & 3] = *p;
+          p += 4 * ld;
+        }
+        const gdbl* pa = Lp + (int64_t)(kbu + lk) * M + r0 + 16 * rb + li;
+#pragma unroll
+        for (int kq = 0; kq < 16; ++kq) {
+          f[kq] = kq < nkq ? *pa : 0.0;
+          pa += 4 * M;
+        }
+      };
+      load_blk(wv, cc, fa);
+#pragma unroll 1
+      for (int rb = wv; rb < nrb; rb += 4) {
+        if (rb + 4 < nrb) load_blk(rb + 4, cn, fan);
+        const bool rin = 16 * rb + li < mr;
+        v4d acc[4];
+#pragma unroll
+        for (int bj = 0; bj < 4; ++bj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[bj][r] = sel0(rin && 16 * bj + lk + 4 * r < nc, cc[bj][r]);
+#pragma unroll
+        for (int kq = 0; kq < 16; ++kq) {
+          if (kq >= nkq) continue;
+          const int k = 4 * kq + lk;
+          const double a = sel0(rin && k < wu, fa[kq]);
+#pragma unroll
+          for (int bj = 0; bj < 4; ++bj)
+            acc[bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(Bs[k * ULDB + 16 * bj + li], a, acc[bj], 0, 0, 0);
+        }
+        gdbl* p = C + (int64_t)lk * ld + r0 + 16 * rb + li;
+#pragma unroll
+        for (int c4 = 0; c4 < 16; ++c4) {
+          if (rin && 4 * c4 + lk < nc) *p = acc[c4 >> 2][c4 & 3];
+          p += 4 * ld;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) cc[j] = cn[j];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) fa[j] = fan[j];
+      }
+    }
+    __syncthreads();   // C_u / C_r stores before the next sub-panel's loads; Bs free
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Inverses of a factored 64 x 64 diagonal tile for the GEMM-form triangular solves:
 //   NL = I - L_kk^{-1} (L unit lower: the strictly lower part of the tile),
 //   NU = I - U_kk^{-1} (U upper with its diagonal),
@@ -891,6 +1072,12 @@ hipError_t launch_gemm_g(hipStream_t st, int64_t ntiles, const GemmTask* tasks, 
 hipError_t launch_gemm(hipStream_t st, int64_t ntiles, const GemmTask* tasks, int ntask, int tile,
                        int64_t maxwg) {
   return launch_gemm_g(st, ntiles, tasks, ntask, tile, maxwg, nullptr, nullptr, 1.0);
+}
+hipError_t launch_urows(hipStream_t st, int cnt, const URowTask* tasks, const SNode* sn, double* store,
+                        const double* tinv) {
+  if (cnt <= 0) return hipSuccess;
+  k_urows<<<(unsigned)cnt, 256, 0, st>>>(tasks, sn, store, tinv);   // OB <= 384 (QMAX): checked by the caller
+  return hipGetLastError();
 }
 hipError_t launch_tri_inv(hipStream_t st, int cnt, int step, const int32_t* list, const SNode* sn,
                           double* store, double* scratch, double* tinv) {

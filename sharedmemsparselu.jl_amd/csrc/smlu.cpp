@@ -39,7 +39,7 @@ hipError_t launch_front_small(hipStream_t, int, int, const int32_t*, const SNode
                             int32_t*, int32_t*, double*, double, double);
 hipError_t init_kernel_attributes();
 hipError_t launch_panel1(hipStream_t, int, int, int, int, int, const int32_t*, const SNode*, double*, double*,
-                         int32_t*, int32_t*, int64_t, int32_t*, double*, double);
+                         int32_t*, int32_t*, int64_t, int32_t*, double*, double, double*, int);
 hipError_t launch_step_trsm(hipStream_t, int, const FrontTile*, int, int64_t, const FrontTile*, int, int64_t,
                             int, int, const SNode*, double*, double*, int32_t*, double*, double);
 hipError_t launch_laswp(hipStream_t, int64_t, const SwapTask*, int, const SNode*, double*, double*, const int32_t*,
@@ -49,6 +49,7 @@ hipError_t launch_trsm_u(hipStream_t, int64_t, const FrontTile*, int, int, int, 
 hipError_t launch_gemm(hipStream_t, int64_t, const GemmTask*, int, int, int64_t);
 hipError_t launch_gemm_g(hipStream_t, int64_t, const GemmTask*, int, int, int64_t, int32_t*, double*, double);
 hipError_t launch_tri_inv(hipStream_t, int, int, const int32_t*, const SNode*, double*, double*, double*);
+hipError_t launch_urows(hipStream_t, int, const URowTask*, const SNode*, double*, const double*);
 hipError_t launch_fwd_tiny(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                            const int32_t*, const double*, double*, double*, Rhs);
 hipError_t launch_bwd_tiny(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*, double*,
@@ -98,12 +99,12 @@ thread_local std::string g_last_error;
 enum Kind : int {
   K_MEMSET_STORE, K_MEMSET_SCRATCH, K_SCATTER, K_EXTADD, K_FRONT_LDS, K_PANEL, K_TRSMU, K_TRSML,
   K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_GEMM22, K_LASWP, K_STEPTRSM, K_GEMMU,
-  K_GEMMO, K_FORK, K_JOIN, K_TRIINV, K_BWDU12C, K_VCOPY, K_FWDT, K_BWDT, K_SWEEPF, K_SWEEPB, K_NKIND
+  K_GEMMO, K_FORK, K_JOIN, K_TRIINV, K_BWDU12C, K_VCOPY, K_FWDT, K_BWDT, K_SWEEPF, K_SWEEPB, K_UROWS, K_NKIND
 };
 const char* kKindName[K_NKIND] = {"memset", "memset", "assemble", "assemble", "small", "panel",
                                   "trsm", "trsm", "gemm", "solve", "solve", "solve", "solve",
                                   "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "sync", "sync", "trsm", "solve", "solve",
-                                  "solve", "solve", "solve", "solve"};
+                                  "solve", "solve", "solve", "solve", "urows"};
 constexpr int kSolveBigNs = 256;  // fronts with more pivots use the multi-workgroup solve
 // ... and so do fronts whose L panel (M x ns entries) exceeds this: one workgroup streams a
 // tall panel at single-CU bandwidth (a 10^4-row front with 200 pivots took ~350 us per sweep)
@@ -356,6 +357,7 @@ struct smlu_handle {
   int64_t ssync_n = 0;
   DBuf<GemmTask> gtasks;
   DBuf<SwapTask> stasks;
+  DBuf<URowTask> urtasks;     // fused U-row tasks (k_urows)
   DBuf<XCol> xcols;
   // schedule
   std::vector<Launch> fac, fwd, bwd;
@@ -452,6 +454,7 @@ struct smlu_handle {
     sxh.free();
     gtasks.free();
     stasks.free();
+    urtasks.free();
     xcols.free();
     stage_s.free();
     stage_r.free();
@@ -624,6 +627,7 @@ static int build_schedule(smlu_handle* h) {
   std::vector<FrontTile> ft;
   std::vector<GemmTask> gt;
   std::vector<SwapTask> st_tasks;
+  std::vector<URowTask> ur_tasks;
   std::vector<XCol> xc;
   std::vector<int2> ae;
   // A entries grouped by front, sorted by (local column, local row)
@@ -802,6 +806,13 @@ static int build_schedule(smlu_handle* h) {
   h->sb = std::max<int64_t>(h->ob, (h->sb / h->ob) * h->ob);
   auto sbw = [&](int64_t s) -> int64_t { return (gform(s) && !h->lookahead && h->nranks == 1) ? h->sb : h->ob; };
   const int64_t spf = std::max<int64_t>(h->sb, h->ob) / 32;   // swap / tile-inverse slots per front
+  // fused panels (k_panel_blk<16, true>: panel + tile inverses + in-block row interchanges) for
+  // the GEMM-form fronts (every 64-wide panel then belongs to one); SMLU_FUSED_PANEL=0: three launches
+  const bool fuse_panel = h->trsm_gemm && h->trsm_gemm64_only && h->ob <= 64 + 16 * 20 &&
+                          std::getenv("SMLU_FUSED_PANEL") && std::atoi(std::getenv("SMLU_FUSED_PANEL")) == 1;
+  // fused U rows at the end of an outer block (k_urows) for the GEMM-form fronts; SMLU_FUSED_UROWS=0:
+  // one TRSM + one update launch per sub-panel
+  const bool fuse_urows = h->ob <= 384 && !(std::getenv("SMLU_FUSED_UROWS") && std::atoi(std::getenv("SMLU_FUSED_UROWS")) == 0);
   // tinv operand encoding in tpatch: offset * 2 + (1 if the operand is B, 0 if A)
   auto tinv_slot_off = [](int64_t slot, bool upper) { return slot * 8192 + (upper ? 4096 : 0); };
   for (int l = 0; l < P.nlevels; ++l) {
@@ -1016,6 +1027,7 @@ static int build_schedule(smlu_handle* h) {
           L.aux = 0;
           L.nwg = rmax;
           L.aux2 = wmax;
+          L.cnt2 = c == 0 && fuse_panel;   // 64-wide panels of GEMM-form fronts: fused tail
           if (L.cnt > 0) h->fac.push_back(L);
         }
         if (pos != act.size()) return fail(h, SMLU_ERR_ARG, "internal: panel classes");
@@ -1027,7 +1039,7 @@ static int build_schedule(smlu_handle* h) {
         L.step = (int)t;
         L.off = (int64_t)ilist.size();
         for (auto s : act) {
-          if (!gform(s)) continue;
+          if (!gform(s) || fuse_panel) continue;   // fused into the panel launch
           ilist.push_back((int32_t)s);
           ilist.push_back((int32_t)slot_of(s, t % (sbw(s) / h->hsn[s].nb)));
         }
@@ -1046,7 +1058,7 @@ static int build_schedule(smlu_handle* h) {
           int64_t kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
           int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
           int64_t ncol = oend - ostart - w;
-          if (ncol <= 0) continue;
+          if (ncol <= 0 || (fuse_panel && gform(s))) continue;   // fused panels swap these rows themselves
           st_tasks.push_back(SwapTask{(int32_t)s, (int32_t)kb, 1, (int32_t)slot_of(s, t % (sbw(s) / r.nb)),
                                       (int32_t)ostart, (int32_t)oend, (int32_t)kb, (int32_t)(kb + w), wg});
           wg += (ncol + 63) / 64;
@@ -1188,7 +1200,34 @@ static int build_schedule(smlu_handle* h) {
       };
       // TRSM of the U rows of a set of OBs (one per front), sub-panel by sub-panel: L_uu^-1 C in
       // place on the given columns, then the rows below the sub-panel inside the OB
-      auto urows = [&](const std::vector<URows>& items) {
+      auto urows = [&](const std::vector<URows>& all_items) {
+        // GEMM-form fronts: one fused k_urows launch (every column block runs the whole
+        // sub-panel sequence); the others keep one launch pair per sub-panel
+        std::vector<URows> items;
+        {
+          L = Launch();
+          L.kind = K_UROWS;
+          L.step = (int)t;
+          L.off = (int64_t)ur_tasks.size();
+          for (auto& it : all_items) {
+            const SNode& r = h->hsn[it.s];
+            if (!(fuse_urows && gform(it.s))) {
+              items.push_back(it);
+              continue;
+            }
+            const int64_t M = (int64_t)r.ns + r.nu;
+            const int32_t slot0 = (int32_t)slot_of(it.s, (it.ob0 % sbw(it.s)) / r.nb);
+            for (int64_t c = it.c0; c < it.c1; c += 64)
+              ur_tasks.push_back(URowTask{(int32_t)it.s, (int32_t)it.ob0, (int32_t)it.ob1, slot0, (int32_t)M,
+                                          (int32_t)std::min<int64_t>(64, it.c1 - c), r.Loff + c * M});
+            if (it.u12)
+              for (int64_t c = 0; c < r.nu; c += 64)
+                ur_tasks.push_back(URowTask{(int32_t)it.s, (int32_t)it.ob0, (int32_t)it.ob1, slot0, r.ns,
+                                            (int32_t)std::min<int64_t>(64, r.nu - c), r.Uoff + c * r.ns});
+          }
+          L.cnt = (int64_t)ur_tasks.size() - L.off;
+          if (L.cnt > 0) h->fac.push_back(L);
+        }
         int64_t nsub = 0;
         for (auto& it : items) nsub = std::max<int64_t>(nsub, (it.ob1 - it.ob0 + h->hsn[it.s].nb - 1) / h->hsn[it.s].nb);
         for (int64_t u = 0; u < nsub; ++u) {
@@ -2102,6 +2141,7 @@ static int build_schedule(smlu_handle* h) {
   HIPCHK(h->gtasks.upload(gt.data(), gt.size(), st));
   h->hgt = gt;
   HIPCHK(h->stasks.upload(st_tasks.data(), st_tasks.size(), st));
+  HIPCHK(h->urtasks.upload(ur_tasks.data(), ur_tasks.size(), st));
   HIPCHK(h->xcols.upload(xc.data(), xc.size(), st));
   HIPCHK(h->swaps.alloc((size_t)max_list * kSwapStride));
   HIPCHK(h->vbuf.alloc((size_t)std::max<int64_t>(voff, 1)));
@@ -2205,7 +2245,10 @@ static int setup_device(smlu_handle* h) {
   }
   HIPCHK(h->A.alloc((size_t)std::max<int64_t>(P.nnzA, 1)));
   HIPCHK(h->Rs.alloc((size_t)P.n));
-  HIPCHK(h->store.alloc((size_t)std::max<int64_t>(h->lay.store_size, 1)));
+  // k_urows reads up to 64 columns and 16 rows past a block (values discarded): pad the store
+  int64_t maxM = 1;
+  for (int64_t s = 0; s < P.nsup; ++s) maxM = std::max<int64_t>(maxM, P.M(s));
+  HIPCHK(h->store.alloc((size_t)(std::max<int64_t>(h->lay.store_size, 1) + 64 * maxM + 4096)));
   HIPCHK(h->scratch.alloc((size_t)std::max<int64_t>(h->lay.scratch_size, 1)));
   if (h->nranks > 1) {   // received pivot block + tile inverses + swap lists + rowperm
     int64_t bc = 1;
@@ -2323,7 +2366,7 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
       return launch_panel1(st, (int)L.cnt, (int)L.aux, (int)L.nwg, (int)L.aux2, L.step,
                            h->ilist.p + L.off, h->sn.p,
                           h->store.p, h->scratch.p, h->rowperm.p, h->swaps.p, kSwapStride, h->info.p,
-                          h->growth.p, diag_tol);
+                          h->growth.p, diag_tol, L.cnt2 ? h->tinv.p : nullptr, (int)h->ob);
     case K_TRSMU:
       return launch_trsm_u(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->ob, (int)L.aux, h->sn.p,
                            h->store.p, h->scratch.p, h->swaps.p, kSwapStride);
@@ -2335,6 +2378,8 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
     case K_TRSML:
       return launch_gemm_g(st, L.nwg, h->gtasks.p + L.off, (int)L.cnt, (int)L.aux, 0, h->info.p,
                            h->growth.p, piv_tol);
+    case K_UROWS:
+      return launch_urows(st, (int)L.cnt, h->urtasks.p + L.off, h->sn.p, h->store.p, h->tinv.p);
     case K_TRIINV:
       return launch_tri_inv(st, (int)L.cnt, L.step, h->ilist.p + L.off, h->sn.p, h->store.p, h->scratch.p,
                             h->tinv.p);
@@ -2545,6 +2590,7 @@ static void release_schedule(smlu_handle* h) {
   h->sxh.free();
   h->gtasks.free();
   h->stasks.free();
+  h->urtasks.free();
   h->xcols.free();
   h->swaps.free();
   h->vbuf.free();
