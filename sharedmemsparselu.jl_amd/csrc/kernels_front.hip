@@ -622,22 +622,24 @@ __global__ __launch_bounds__(64) void k_panel_wave(const int32_t* __restrict__ l
 // forms columns 4v..4v+3 of NL = I - L^-1 and of NU = I - U^-1 with k_tri_inv's arithmetic, and
 // the outer block's other columns [ostart, oend) \ [kb, kb+w) get the tile's row interchanges
 // (every moved row read into registers, one barrier, then written to its new position).
-template <int NWV, int CW>
+template <int NWV, int CW, bool INV>
 __device__ __forceinline__ void panel_fused_tail(const double (&x)[CW], int pos, bool has, int w, int kb,
                                                  int64_t M, const FrontPtrs& f, const SNode& s, int64_t slot,
                                                  double* __restrict__ tinv, int ob, int lane, int wv) {
   static_assert(NWV == 16 && CW == 4, "fused panel: 16 waves, 4 columns each");
-  __shared__ double sD[64 * 65];
+  __shared__ double sD[INV ? 64 * 65 : 1];
   const int tid = threadIdx.x;
-  for (int idx = tid; idx < 4096; idx += 64 * NWV) {
-    const int i = idx & 63, j = idx >> 6;
-    if (i >= w || j >= w) sD[j * 65 + i] = i == j ? 1.0 : 0.0;
-  }
-  if (has) {
+  if (INV) {
+    for (int idx = tid; idx < 4096; idx += 64 * NWV) {
+      const int i = idx & 63, j = idx >> 6;
+      if (i >= w || j >= w) sD[j * 65 + i] = i == j ? 1.0 : 0.0;
+    }
+    if (has) {
 #pragma unroll
-    for (int j = 0; j < CW; ++j) {
-      const int c = wv * CW + j;
-      if (c < w) sD[c * 65 + pos] = x[j];
+      for (int j = 0; j < CW; ++j) {
+        const int c = wv * CW + j;
+        if (c < w) sD[c * 65 + pos] = x[j];
+      }
     }
   }
   // row interchanges of the outer block's other columns: read every moved row first
@@ -663,6 +665,7 @@ __device__ __forceinline__ void panel_fused_tail(const double (&x)[CW], int pos,
       f.L[(int64_t)col * M + kb + pos] = mv[q];
     }
   }
+  if (!INV) return;
   // tile inverses (k_tri_inv, parts 0-3 -> NL, 4-7 -> NU; here wave v = part*4 + wave)
   const int c0 = wv * 4;
   double* out = tinv + slot * 8192;
@@ -718,7 +721,7 @@ __device__ __forceinline__ void panel_fused_tail(const double (&x)[CW], int pos,
 // tile inverses k_tri_inv computes (same per-column arithmetic: bitwise-identical NL/NU in the
 // same tinv slot) and the row interchanges of the outer block's other columns that k_laswp
 // applies inside the block -- two launches fewer per inner step of the blocked fronts.
-template <int NWV, bool FUSED>
+template <int NWV, int FUSED>
 __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restrict__ list, int step,
                                                         const SNode* __restrict__ sn,
                                                         double* __restrict__ store,
@@ -845,7 +848,8 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
     s_flag[wv] = flag;
     s_err[wv] = err;
   }
-  if constexpr (FUSED) panel_fused_tail<NWV, CW>(x, pos, has, w, kb, M, f, s, list[2 * blockIdx.x + 1], tinv, ob, lane, wv);
+  if constexpr (FUSED > 0)
+    panel_fused_tail<NWV, CW, FUSED == 2>(x, pos, has, w, kb, M, f, s, list[2 * blockIdx.x + 1], tinv, ob, lane, wv);
   __syncthreads();
   if (wv != 0) return;
   int32_t* rp = rowperm + s.first + kb;
@@ -1433,7 +1437,7 @@ hipError_t launch_panel1(hipStream_t st, int cnt, int lds_doubles, int rmax, int
                          const int32_t* list,
                          const SNode* sn, double* store, double* scratch, int32_t* rowperm,
                          int32_t* swaps, int64_t swap_stride, int32_t* info, double* growth,
-                         double diag_tol, double* fused_tinv, int ob) {
+                         double diag_tol, int fused, double* tinv, int ob) {
   if (cnt <= 0) return hipSuccess;
   size_t lds = (size_t)lds_doubles * sizeof(double);
 #define PANEL1_ARGS list, step, sn, store, scratch, rowperm, swaps, swap_stride, info, growth, diag_tol
@@ -1450,12 +1454,13 @@ hipError_t launch_panel1(hipStream_t st, int cnt, int lds_doubles, int rmax, int
     const char* e = std::getenv("SMLU_PANEL_BLK");
     return e ? std::atoi(e) : 16;
   }();
-  if (fused_tinv) {   // GEMM-form fronts: panel + tile inverses + in-block row interchanges
-    if (wmax <= 32 || ob > 64 + 16 * 20) return hipErrorInvalidValue;
-    k_panel_blk<16, true><<<cnt, 1024, 0, st>>>(PANEL1_ARGS, fused_tinv, ob);
+  if (fused) {   // GEMM-form fronts: panel + in-block row interchanges (+ tile inverses if fused == 2)
+    if (wmax <= 32 || ob > 64 + 16 * 20 || (fused == 2 && !tinv)) return hipErrorInvalidValue;
+    if (fused == 2) k_panel_blk<16, 2><<<cnt, 1024, 0, st>>>(PANEL1_ARGS, tinv, ob);
+    else k_panel_blk<16, 1><<<cnt, 1024, 0, st>>>(PANEL1_ARGS, tinv, ob);
   }
-  else if (wmax > 32 && !lds_panel && blk_waves == 16) k_panel_blk<16, false><<<cnt, 1024, 0, st>>>(PANEL1_ARGS, nullptr, 0);
-  else if (wmax > 32 && !lds_panel && blk_waves == 8) k_panel_blk<8, false><<<cnt, 512, 0, st>>>(PANEL1_ARGS, nullptr, 0);
+  else if (wmax > 32 && !lds_panel && blk_waves == 16) k_panel_blk<16, 0><<<cnt, 1024, 0, st>>>(PANEL1_ARGS, nullptr, 0);
+  else if (wmax > 32 && !lds_panel && blk_waves == 8) k_panel_blk<8, 0><<<cnt, 512, 0, st>>>(PANEL1_ARGS, nullptr, 0);
   else if (wmax > 32 && !lds_panel && cols_waves == 16) k_panel_cols<16><<<cnt, 1024, 0, st>>>(PANEL1_ARGS);
   else if (wmax > 32 && !lds_panel && cols_waves == 8) k_panel_cols<8><<<cnt, 512, 0, st>>>(PANEL1_ARGS);
   else if (wmax > 32 && !lds_panel && cols_waves == 4) k_panel_cols<4><<<cnt, 256, 0, st>>>(PANEL1_ARGS);

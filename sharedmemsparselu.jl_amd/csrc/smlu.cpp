@@ -39,7 +39,7 @@ hipError_t launch_front_small(hipStream_t, int, int, const int32_t*, const SNode
                             int32_t*, int32_t*, double*, double, double);
 hipError_t init_kernel_attributes();
 hipError_t launch_panel1(hipStream_t, int, int, int, int, int, const int32_t*, const SNode*, double*, double*,
-                         int32_t*, int32_t*, int64_t, int32_t*, double*, double, double*, int);
+                         int32_t*, int32_t*, int64_t, int32_t*, double*, double, int, double*, int);
 hipError_t launch_step_trsm(hipStream_t, int, const FrontTile*, int, int64_t, const FrontTile*, int, int64_t,
                             int, int, const SNode*, double*, double*, int32_t*, double*, double);
 hipError_t launch_laswp(hipStream_t, int64_t, const SwapTask*, int, const SNode*, double*, double*, const int32_t*,
@@ -808,8 +808,11 @@ static int build_schedule(smlu_handle* h) {
   const int64_t spf = std::max<int64_t>(h->sb, h->ob) / 32;   // swap / tile-inverse slots per front
   // fused panels (k_panel_blk<16, true>: panel + tile inverses + in-block row interchanges) for
   // the GEMM-form fronts (every 64-wide panel then belongs to one); SMLU_FUSED_PANEL=0: three launches
-  const bool fuse_panel = h->trsm_gemm && h->trsm_gemm64_only && h->ob <= 64 + 16 * 20 &&
-                          std::getenv("SMLU_FUSED_PANEL") && std::atoi(std::getenv("SMLU_FUSED_PANEL")) == 1;
+  // 1 (default): panel + the in-block row interchanges (no k_laswp inside the block);
+  // 2: + the tile inverses (no k_tri_inv; one CU computes them: slower); 0: separate launches
+  const int fuse_mode = !(h->trsm_gemm && h->trsm_gemm64_only && h->ob <= 64 + 16 * 20) ? 0
+                        : std::getenv("SMLU_FUSED_PANEL") ? std::atoi(std::getenv("SMLU_FUSED_PANEL")) : 1;
+  const bool fuse_panel = fuse_mode > 0, fuse_inv = fuse_mode == 2;
   // fused U rows at the end of an outer block (k_urows) for the GEMM-form fronts; SMLU_FUSED_UROWS=0:
   // one TRSM + one update launch per sub-panel
   const bool fuse_urows = h->ob <= 384 && !(std::getenv("SMLU_FUSED_UROWS") && std::atoi(std::getenv("SMLU_FUSED_UROWS")) == 0);
@@ -1027,7 +1030,7 @@ static int build_schedule(smlu_handle* h) {
           L.aux = 0;
           L.nwg = rmax;
           L.aux2 = wmax;
-          L.cnt2 = c == 0 && fuse_panel;   // 64-wide panels of GEMM-form fronts: fused tail
+          L.cnt2 = c == 0 ? fuse_mode : 0;   // 64-wide panels of GEMM-form fronts: fused tail
           if (L.cnt > 0) h->fac.push_back(L);
         }
         if (pos != act.size()) return fail(h, SMLU_ERR_ARG, "internal: panel classes");
@@ -1039,7 +1042,7 @@ static int build_schedule(smlu_handle* h) {
         L.step = (int)t;
         L.off = (int64_t)ilist.size();
         for (auto s : act) {
-          if (!gform(s) || fuse_panel) continue;   // fused into the panel launch
+          if (!gform(s) || fuse_inv) continue;   // fused into the panel launch
           ilist.push_back((int32_t)s);
           ilist.push_back((int32_t)slot_of(s, t % (sbw(s) / h->hsn[s].nb)));
         }
@@ -2366,7 +2369,7 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
       return launch_panel1(st, (int)L.cnt, (int)L.aux, (int)L.nwg, (int)L.aux2, L.step,
                            h->ilist.p + L.off, h->sn.p,
                           h->store.p, h->scratch.p, h->rowperm.p, h->swaps.p, kSwapStride, h->info.p,
-                          h->growth.p, diag_tol, L.cnt2 ? h->tinv.p : nullptr, (int)h->ob);
+                          h->growth.p, diag_tol, (int)L.cnt2, h->tinv.p, (int)h->ob);
     case K_TRSMU:
       return launch_trsm_u(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->ob, (int)L.aux, h->sn.p,
                            h->store.p, h->scratch.p, h->swaps.p, kSwapStride);
