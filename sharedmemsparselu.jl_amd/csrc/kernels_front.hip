@@ -617,6 +617,7 @@ __global__ __launch_bounds__(64) void k_panel_wave(const int32_t* __restrict__ l
   }
 }
 
+typedef double v4d __attribute__((ext_vector_type(4)));
 // Tail of the fused panel (k_panel_blk<NWV, true>): the finished tile (x, row positions pos)
 // goes to LDS as k_tri_inv reads it from HBM ([col][row], ld 65, identity outside w x w), wave v
 // forms columns 4v..4v+3 of NL = I - L^-1 and of NU = I - U^-1 with k_tri_inv's arithmetic, and
@@ -666,45 +667,72 @@ __device__ __forceinline__ void panel_fused_tail(const double (&x)[CW], int pos,
     }
   }
   if (!INV) return;
-  // tile inverses (k_tri_inv, parts 0-3 -> NL, 4-7 -> NU; here wave v = part*4 + wave)
-  const int c0 = wv * 4;
-  double* out = tinv + slot * 8192;
-  {
-    double z[4];
+  // tile inverses X_L = L^-1, X_U = U^-1 by 16 x 16 blocks: the diagonal blocks by substitution
+  // (lane = one column of one block), the off-diagonal blocks by the block recurrences
+  //   X_ij = -X_ii sum_{k=j}^{i-1} L_ik X_kj (i > j),   X_ij = -X_ii sum_{k=i+1}^{j} U_ik X_kj (i < j)
+  // on the fp64 matrix cores (distance 1, 2, 3 from the diagonal, one barrier each); then
+  // NL = I - X_L, NU = I - X_U to the tinv slot (the operands of the GEMM-form TRSM launches).
+  __shared__ double XL[64 * 65], XU[64 * 65];   // [col][row], ld 65
+  const int li = lane & 15, lg = lane >> 4;
+  if (wv < 2) {   // wave 0: the four L diagonal blocks, wave 1: the four U diagonal blocks
+    const int b0 = 16 * lg, c = li;
+    double xv[16];
+    if (wv == 0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) z[r] = lane == c0 + r ? 1.0 : 0.0;
-#pragma unroll 4
-    for (int j = 0; j < 63; ++j) {
-      const double lij = sD[j * 65 + lane];
+      for (int i = 0; i < 16; ++i) {
+        double v = i == c ? 1.0 : 0.0;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const double zj = readlane_f64(z[r], j);
-        if (lane > j) z[r] = fma(-lij, zj, z[r]);
+        for (int j = 0; j < i; ++j) v = fma(-sD[(b0 + j) * 65 + b0 + i], xv[j], v);
+        xv[i] = v;
       }
-    }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) out[(int64_t)(c0 + r) * 64 + lane] = lane > c0 + r ? -z[r] : 0.0;
+      for (int i = 0; i < 16; ++i) XL[(b0 + c) * 65 + b0 + i] = xv[i];
+    } else {
+#pragma unroll
+      for (int i = 15; i >= 0; --i) {
+        double v = i == c ? 1.0 : 0.0;
+#pragma unroll
+        for (int j = i + 1; j < 16; ++j) v = fma(-sD[(b0 + j) * 65 + b0 + i], xv[j], v);
+        xv[i] = v * recip(sD[(b0 + i) * 65 + b0 + i]);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) XU[(b0 + c) * 65 + b0 + i] = xv[i];
+    }
   }
-  {
-    double z[4];
+  __syncthreads();
+  // one off-diagonal block (bi, bj) at distance d: T = sum_k F_{bi,k} X_{k,bj}, X = -X_{bi,bi} T.
+  // MFMA 16x16x4: A fragment lane (row li, k lg), B fragment (k lg, col li); D lane holds
+  // (row lg + 4r, col li), which is exactly the B fragment of k-quad r for the second product.
+  auto offdiag = [&](const double* X, double* Xw, int bi, int bj, int k0, int k1) {
+    v4d t = {0.0, 0.0, 0.0, 0.0};
+    for (int kb = k0; kb <= k1; ++kb) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) z[r] = lane == c0 + r ? 1.0 : 0.0;
-    const double rd = recip(sD[lane * 65 + lane]);
-#pragma unroll 4
-    for (int j = 63; j >= 0; --j) {
-      const double uij = sD[j * 65 + lane];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (lane == j) z[r] *= rd;
-        const double yj = readlane_f64(z[r], j);
-        if (lane < j) z[r] = fma(-uij, yj, z[r]);
+      for (int kq = 0; kq < 4; ++kq) {
+        const double fa = sD[(16 * kb + 4 * kq + lg) * 65 + 16 * bi + li];   // F[bi rows][kb cols]
+        const double fb = X[(16 * bj + li) * 65 + 16 * kb + 4 * kq + lg];    // X[kb rows][bj cols]
+        t = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, t, 0, 0, 0);
       }
     }
+    v4d x = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int c = c0 + r;
-      out[4096 + (int64_t)c * 64 + lane] = lane == c ? 1.0 - z[r] : (lane < c ? -z[r] : 0.0);
+    for (int kq = 0; kq < 4; ++kq) {
+      const double fa = -X[(16 * bi + 4 * kq + lg) * 65 + 16 * bi + li];    // -X[bi rows][bi cols]
+      x = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, t[kq], x, 0, 0, 0);
     }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Xw[(16 * bj + li) * 65 + 16 * bi + lg + 4 * r] = x[r];
+  };
+  for (int d = 1; d < 4; ++d) {
+    const int nb = 4 - d;   // blocks at distance d: L (j + d, j), U (j, j + d), j < nb
+    if (wv < nb) offdiag(XL, XL, wv + d, wv, wv, wv + d - 1);
+    else if (wv >= 8 && wv - 8 < nb) offdiag(XU, XU, wv - 8, wv - 8 + d, wv - 8 + 1, wv - 8 + d);
+    __syncthreads();
+  }
+  double* out = tinv + slot * 8192;
+  for (int idx = tid; idx < 4096; idx += 64 * NWV) {
+    const int i = idx & 63, j = idx >> 6;
+    out[(int64_t)j * 64 + i] = i > j ? -XL[j * 65 + i] : 0.0;
+    out[4096 + (int64_t)j * 64 + i] = i == j ? 1.0 - XU[j * 65 + i] : (i < j ? -XU[j * 65 + i] : 0.0);
   }
 }
 

@@ -808,10 +808,11 @@ static int build_schedule(smlu_handle* h) {
   const int64_t spf = std::max<int64_t>(h->sb, h->ob) / 32;   // swap / tile-inverse slots per front
   // fused panels (k_panel_blk<16, true>: panel + tile inverses + in-block row interchanges) for
   // the GEMM-form fronts (every 64-wide panel then belongs to one); SMLU_FUSED_PANEL=0: three launches
-  // 1 (default): panel + the in-block row interchanges (no k_laswp inside the block);
-  // 2: + the tile inverses (no k_tri_inv; one CU computes them: slower); 0: separate launches
+  // 2 (default): panel + the in-block row interchanges (no k_laswp inside the block) + the tile
+  // inverses by 16 x 16 blocks on the matrix cores (no k_tri_inv); 1: without the inverses;
+  // 0: three launches
   const int fuse_mode = !(h->trsm_gemm && h->trsm_gemm64_only && h->ob <= 64 + 16 * 20) ? 0
-                        : std::getenv("SMLU_FUSED_PANEL") ? std::atoi(std::getenv("SMLU_FUSED_PANEL")) : 1;
+                        : std::getenv("SMLU_FUSED_PANEL") ? std::atoi(std::getenv("SMLU_FUSED_PANEL")) : 2;
   const bool fuse_panel = fuse_mode > 0, fuse_inv = fuse_mode == 2;
   // fused U rows at the end of an outer block (k_urows) for the GEMM-form fronts; SMLU_FUSED_UROWS=0:
   // one TRSM + one update launch per sub-panel
