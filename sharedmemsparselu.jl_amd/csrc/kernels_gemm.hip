@@ -808,6 +808,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma2(const GemmTask* __rest
 #ifndef KQR
 #define KQR 4     // k-quads of L fragments per round trip in phase R
 #endif
+#ifndef UROWS_WG_PER_CU
+#define UROWS_WG_PER_CU 2
+#endif
 #define ULDB 80   // LDS row stride of -C_u [k][col]: k, k+1 rows in opposite bank halves
 // Global accesses walk one per-lane pointer (a VGPR pair) per operand in steps of 4 columns,
 // the remaining offsets being instruction immediates; no branch around a load (values outside
@@ -817,7 +820,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma2(const GemmTask* __rest
 __device__ __forceinline__ double sel0(bool c, double x) {
   return __longlong_as_double(__double_as_longlong(x) & (c ? -1LL : 0LL));
 }
-__global__ __launch_bounds__(256, 1) void k_urows(const URowTask* __restrict__ tasks, const SNode* __restrict__ sn,
+__global__ __launch_bounds__(256, UROWS_WG_PER_CU) void k_urows(const URowTask* __restrict__ tasks, const SNode* __restrict__ sn,
                                                   double* __restrict__ store, const double* __restrict__ tinv) {
   __shared__ double Bs[64 * ULDB];
   const URowTask t = tasks[blockIdx.x];
@@ -863,32 +866,33 @@ __global__ __launch_bounds__(256, 1) void k_urows(const URowTask* __restrict__ t
           p += 4 * ld;
         }
       }
-      double na[2][16];   // the wave's NL fragments for every k, one round trip
-      {
-        const gdbl* p = gbl(tinv + (int64_t)(t.slot0 + u) * 8192) + lk * 64 + rb0 + li;
+      __syncthreads();   // -C_u staged
+      // the wave's NL fragments, 8 k-quads per round trip
+      const gdbl* pn = gbl(tinv + (int64_t)(t.slot0 + u) * 8192) + lk * 64 + rb0 + li;
 #pragma unroll
-        for (int kq = 0; kq < 16; ++kq) {
+      for (int h = 0; h < 2; ++h) {
+        double na[2][8];
 #pragma unroll
-          for (int bi = 0; bi < 2; ++bi) {
-            const double x = p[16 * bi];
-            na[bi][kq] = sel0(rb0 + 16 * bi + li < wu && 4 * kq + lk < wu, x);
-          }
-          p += 256;
+        for (int kk = 0; kk < 8; ++kk) {
+#pragma unroll
+          for (int bi = 0; bi < 2; ++bi)
+            na[bi][kk] = sel0(rb0 + 16 * bi + li < wu && 4 * (8 * h + kk) + lk < wu, pn[16 * bi]);
+          pn += 256;
         }
-      }
-      __syncthreads();
 #pragma unroll
-      for (int kq = 0; kq < 16; ++kq) {
-        if (kq >= nkq) continue;
-        const int k = 4 * kq + lk;
-        double fb[2];
+        for (int kk = 0; kk < 8; ++kk) {
+          const int kq = 8 * h + kk;
+          if (kq >= nkq) continue;
+          const int k = 4 * kq + lk;
+          double fb[2];
 #pragma unroll
-        for (int bj = 0; bj < 2; ++bj) fb[bj] = Bs[k * ULDB + cb0 + 16 * bj + li];
+          for (int bj = 0; bj < 2; ++bj) fb[bj] = Bs[k * ULDB + cb0 + 16 * bj + li];
 #pragma unroll
-        for (int bi = 0; bi < 2; ++bi)
+          for (int bi = 0; bi < 2; ++bi)
 #pragma unroll
-          for (int bj = 0; bj < 2; ++bj)
-            acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[bj], na[bi][kq], acc[bi][bj], 0, 0, 0);
+            for (int bj = 0; bj < 2; ++bj)
+              acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[bj], na[bi][kk], acc[bi][bj], 0, 0, 0);
+        }
       }
       __syncthreads();   // every wave is done reading the old -C_u
       {
@@ -915,8 +919,12 @@ __global__ __launch_bounds__(256, 1) void k_urows(const URowTask* __restrict__ t
     const int r0 = kbu + wu, mr = t.ob1 - r0;
     const int nrb = (mr + 15) >> 4;
     if (wv < nrb) {
-      v4d cc[4], cn[4];
-      double fa[16], fan[16];
+      v4d cc[4];
+      double fa[16];
+#if UROWS_WG_PER_CU == 1
+      v4d cn[4];
+      double fan[16];
+#endif
       auto load_blk = [&](int rb, v4d (&c)[4], double (&f)[16]) {
         const gdbl* p = C + (int64_t)lk * ld + r0 + 16 * rb + li;
 #pragma unroll
@@ -931,10 +939,16 @@ __global__ __launch_bounds__(256, 1) void k_urows(const URowTask* __restrict__ t
           pa += 4 * M;
         }
       };
+#if UROWS_WG_PER_CU == 1
       load_blk(wv, cc, fa);
+#endif
 #pragma unroll 1
       for (int rb = wv; rb < nrb; rb += 4) {
+#if UROWS_WG_PER_CU == 1   // one workgroup per CU: the next block's loads in flight
         if (rb + 4 < nrb) load_blk(rb + 4, cn, fan);
+#else                      // two per CU: the other workgroup covers the load latency
+        load_blk(rb, cc, fa);
+#endif
         const bool rin = 16 * rb + li < mr;
         v4d acc[4];
 #pragma unroll
@@ -956,10 +970,12 @@ __global__ __launch_bounds__(256, 1) void k_urows(const URowTask* __restrict__ t
           if (rin && 4 * c4 + lk < nc) *p = acc[c4 >> 2][c4 & 3];
           p += 4 * ld;
         }
+#if UROWS_WG_PER_CU == 1
 #pragma unroll
         for (int j = 0; j < 4; ++j) cc[j] = cn[j];
 #pragma unroll
         for (int j = 0; j < 16; ++j) fa[j] = fan[j];
+#endif
       }
     }
     __syncthreads();   // C_u / C_r stores before the next sub-panel's loads; Bs free
