@@ -396,6 +396,98 @@ __global__ __launch_bounds__(256) void k_bwd_tiny(const int32_t* __restrict__ li
   }
 }
 
+// Micro fronts (M <= 8 rows: the 240k leaves of the 128^3 tree are (M, ns) = (7, 1) or (6, 1)),
+// one right-hand side: eight fronts per wave, lane group g = lane >> 3 holds front g's rows
+// (row i = lane & 7), broadcasts within the group by __shfl.  A wave per front (k_fwd_tiny) left
+// 56 of 64 lanes idle and ran at 3 waves/SIMD; these kernels keep ~32 waves per CU in flight.
+// Exactly k_fwd_tiny's / k_bwd_tiny's operations in the same order per element (bitwise equal;
+// batched solves keep the tiny kernels on the same front lists).
+__global__ __launch_bounds__(256) void k_fwd_micro(const int32_t* __restrict__ list, int cnt,
+                                                   const SNode* __restrict__ sn, const int32_t* __restrict__ chlist,
+                                                   const int32_t* __restrict__ relmap,
+                                                   const int32_t* __restrict__ rowperm,
+                                                   const double* __restrict__ store, double* __restrict__ x,
+                                                   double* __restrict__ vbuf) {
+  __shared__ double sv[32][8];
+  const int lane = threadIdx.x & 63, g = threadIdx.x >> 3, i = threadIdx.x & 7;
+  const int64_t f = (int64_t)blockIdx.x * 32 + g;
+  const bool act = f < cnt;
+  SNode s{};
+  if (act) s = sn[list[f]];
+  const int ns = act ? s.ns : 0, M = act ? s.ns + s.nu : 0;
+  const double* Lp = store + s.Loff;
+  double l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) l[j] = (i < M && j < ns) ? Lp[(int64_t)j * M + i] : 0.0;
+  sv[g][i] = i < ns ? x[s.first + i] : 0.0;
+  wave_lds_sync();
+  for (int c = act ? s.chbeg : 0; c < (act ? s.chend : 0); ++c) {   // parent += child, children in order
+    const SNode ch = sn[chlist[c]];
+    for (int q = i; q < ch.nu; q += 8) {
+      const int t = relmap[ch.rowptr + q];
+      sv[g][t] = sv[g][t] + vbuf[ch.voff + ch.ns + q];
+    }
+    wave_lds_sync();
+  }
+  wave_lds_sync();
+  const int pr = i < ns ? rowperm[s.first + i] : i;
+  double val = i < M ? sv[g][pr] : 0.0;
+  double acc = 0.0;
+  const int gb = lane & ~7;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const double xj = __shfl(val, gb + j, 64);
+    if (j < ns) {
+      if (i > j && i < ns) val = fma(-l[j], xj, val);
+      else if (i >= ns) acc = fma(l[j], xj, acc);
+    }
+  }
+  if (i < ns) {
+    x[s.first + i] = val;
+    vbuf[s.voff + i] = val;
+  } else if (i < M) {
+    vbuf[s.voff + i] = val - acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bwd_micro(const int32_t* __restrict__ list, int cnt,
+                                                   const SNode* __restrict__ sn, const int32_t* __restrict__ rows,
+                                                   const double* __restrict__ store, double* __restrict__ x,
+                                                   double* __restrict__ vbuf) {
+  const int lane = threadIdx.x & 63, i = threadIdx.x & 7;
+  const int64_t f = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
+  const bool act = f < cnt;
+  SNode s{};
+  if (act) s = sn[list[f]];
+  const int ns = act ? s.ns : 0, nu = act ? s.nu : 0;
+  const int64_t M = (int64_t)ns + nu;
+  // x_s - U12 x[R] (columns in order), then the upper chain
+  double acc = 0.0;
+  if (i < ns) {
+    const double* U12 = store + s.Uoff;
+    for (int j = 0; j < nu; ++j) acc = fma(U12[(int64_t)j * ns + i], x[rows[s.rowptr + j]], acc);
+  }
+  const double o = i < ns ? x[s.first + i] : 0.0;
+  double val = o - (nu > 0 ? acc : 0.0);
+  if (!(i < ns)) val = 0.0;
+  const double* Lp = store + s.Loff;
+  double l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) l[j] = (i < ns && j < ns) ? Lp[(int64_t)j * M + i] : 0.0;
+  const double dinv = i < ns ? recip(Lp[(int64_t)i * M + i]) : 1.0;
+  const int gb = lane & ~7;
+#pragma unroll
+  for (int j = 7; j >= 0; --j) {
+    if (j < ns && i == j) val = val * dinv;
+    const double xj = __shfl(val, gb + j, 64);
+    if (j < ns && i < j) val = fma(-l[j], xj, val);
+  }
+  if (i < ns) {
+    x[s.first + i] = val;
+    vbuf[s.voff + i] = val;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Solves for large fronts (ns > 256): the diagonal block sweep is split over workgroups.
 // k_fwd_gather: front vector = own rows + children's update vectors, row permutation.
@@ -891,18 +983,26 @@ hipError_t launch_bwd(hipStream_t st, int cnt, const int32_t* list, const SNode*
 }
 hipError_t launch_fwd_tiny(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
                            const int32_t* chlist, const int32_t* relmap, const int32_t* rowperm,
-                           const double* store, double* x, double* vbuf, Rhs rh) {
+                           const double* store, double* x, double* vbuf, Rhs rh, int micro) {
   if (cnt <= 0) return hipSuccess;
   if (rh.n < 1 || rh.n > kMaxRhs) return hipErrorInvalidValue;
+  if (micro && rh.n == 1) {   // every front of the list has M <= 8
+    k_fwd_micro<<<nblk(cnt, 32), 256, 0, st>>>(list, cnt, sn, chlist, relmap, rowperm, store, x, vbuf);
+    return hipGetLastError();
+  }
   const unsigned g = nblk(cnt, 4);
   if (rh.n == 1) k_fwd_tiny<1><<<g, 256, 0, st>>>(list, cnt, sn, chlist, relmap, rowperm, store, x, vbuf, rh);
   else k_fwd_tiny<kMaxRhs><<<g, 256, 0, st>>>(list, cnt, sn, chlist, relmap, rowperm, store, x, vbuf, rh);
   return hipGetLastError();
 }
 hipError_t launch_bwd_tiny(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
-                           const int32_t* rows, const double* store, double* x, double* vbuf, Rhs rh) {
+                           const int32_t* rows, const double* store, double* x, double* vbuf, Rhs rh, int micro) {
   if (cnt <= 0) return hipSuccess;
   if (rh.n < 1 || rh.n > kMaxRhs) return hipErrorInvalidValue;
+  if (micro && rh.n == 1) {
+    k_bwd_micro<<<nblk(cnt, 32), 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf);
+    return hipGetLastError();
+  }
   const unsigned g = nblk(cnt, 4);
   // the <4> instance also for a single rhs: <1> lets the compiler keep the U12 and U11 slabs live
   // together (256 VGPRs)

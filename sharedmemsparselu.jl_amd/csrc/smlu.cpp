@@ -51,9 +51,9 @@ hipError_t launch_gemm_g(hipStream_t, int64_t, const GemmTask*, int, int, int64_
 hipError_t launch_tri_inv(hipStream_t, int, int, const int32_t*, const SNode*, double*, double*, double*);
 hipError_t launch_urows(hipStream_t, int, const URowTask*, const SNode*, double*, const double*);
 hipError_t launch_fwd_tiny(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
-                           const int32_t*, const double*, double*, double*, Rhs);
+                           const int32_t*, const double*, double*, double*, Rhs, int);
 hipError_t launch_bwd_tiny(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*, double*,
-                           double*, Rhs);
+                           double*, Rhs, int);
 hipError_t launch_fwd_gather(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                              const int32_t*, double*, double*, Rhs);
 hipError_t launch_tri_block(hipStream_t, bool, int64_t, const FrontTile*, int, int, const SNode*,
@@ -109,6 +109,7 @@ constexpr int kSolveBigNs = 256;  // fronts with more pivots use the multi-workg
 // ... and so do fronts whose L panel (M x ns entries) exceeds this: one workgroup streams a
 // tall panel at single-CU bandwidth (a 10^4-row front with 200 pivots took ~350 us per sweep)
 constexpr int64_t kSolveBigWork = 1 << 16;
+constexpr int kSolveMicroM = 8;    // tiny fronts with M <= 8: eight per wave (k_fwd_micro / k_bwd_micro)
 constexpr int kSolveTinyM = 128;   // fronts with M <= 128 rows and ns <= 64: one wave each (k_fwd_tiny / k_bwd_tiny)
 
 struct Launch {
@@ -1710,6 +1711,7 @@ static int build_schedule(smlu_handle* h) {
   };
   auto holder = [&](int64_t c) { return P.dist(c) ? P.blk_owner(c, P.npblk(c) - 1) : P.owner[c]; };
   static const bool no_tiny = std::getenv("SMLU_NO_TINY_SOLVE") != nullptr;   // dev knob
+  static const bool no_micro = std::getenv("SMLU_NO_MICRO_SOLVE") != nullptr;  // dev knob
   // large fronts: one sync-free sweep launch per level and direction (default) or one launch per
   // 64-column block (SMLU_SOLVE_STEPS=1, the previous schedule)
   const bool sweep_solve = !(std::getenv("SMLU_SOLVE_STEPS") && std::atoi(std::getenv("SMLU_SOLVE_STEPS")) == 1);
@@ -1728,12 +1730,16 @@ static int build_schedule(smlu_handle* h) {
       (big ? bigs : tiny_front ? tiny : small).push_back(s);
     }
     std::vector<Launch> bl;
-    if (!tiny.empty()) {   // one wave per front
+    // tiny fronts: one wave per front; micro fronts (M <= 8) eight per wave for a single rhs
+    for (int micro = 1; micro >= 0; --micro) {
       Launch L;
       L.kind = K_FWDT;
+      L.aux = micro;
       L.off = (int64_t)ilist.size();
-      for (auto s : tiny) ilist.push_back((int32_t)s);
-      L.cnt = (int64_t)tiny.size();
+      for (auto s : tiny)
+        if ((P.M(s) <= kSolveMicroM && !no_micro) == (micro == 1)) ilist.push_back((int32_t)s);
+      L.cnt = (int64_t)ilist.size() - L.off;
+      if (L.cnt == 0) continue;
       h->fwd.push_back(L);
       L.kind = K_BWDT;
       bl.push_back(L);
@@ -2655,9 +2661,9 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, d
       return launch_bwd(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->rows.p, h->store.p, w, v, rh);
     case K_FWDT:
       return launch_fwd_tiny(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->chlist.p, h->relmap.p, h->rowperm.p,
-                             h->store.p, w, v, rh);
+                             h->store.p, w, v, rh, (int)L.aux);
     case K_BWDT:
-      return launch_bwd_tiny(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->rows.p, h->store.p, w, v, rh);
+      return launch_bwd_tiny(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->rows.p, h->store.p, w, v, rh, (int)L.aux);
     case K_FWDG:
       return launch_fwd_gather(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->chlist.p, h->relmap.p,
                                h->rowperm.p, w, v, rh);
