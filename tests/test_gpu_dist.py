@@ -41,7 +41,7 @@ def _values3(A):
     return A3.data
 
 
-def _worker(rank, world, port, which, ob, q, transport="auto"):
+def _worker(rank, world, port, which, ob, q, transport="auto", gpu_per_rank=False):
     try:
         import scipy.sparse as sp
         import torch
@@ -52,10 +52,11 @@ def _worker(rank, world, port, which, ob, q, transport="auto"):
         if ob:
             os.environ["SMLU_OB"] = str(ob)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        torch.cuda.set_device(0)
+        dev = rank if gpu_per_rank else 0
+        torch.cuda.set_device(dev)
         A = _matrix(which)
         n = A.shape[0]
-        F = smlu.DistributedSparseLU(A, device=0, transport=transport)
+        F = smlu.DistributedSparseLU(A, device=dev, transport=transport)
         b = np.random.default_rng(11).random(n)
         db = torch.from_numpy(b).cuda()
         dx = torch.empty_like(db)
@@ -230,3 +231,36 @@ def test_dist_rccl_transport_single_rank():
     smlu.ldiv_(xs1, F, b)
     F.close()
     assert np.allclose(x13[0], xs1, rtol=1e-11, atol=1e-13)
+
+
+def _gpu_count():
+    import torch
+    return torch.cuda.device_count()   # counts devices without initialising them
+
+
+@pytest.mark.skipif(_gpu_count() < 2, reason="RCCL needs one GPU per rank (two or more GPUs)")
+def test_dist_rccl_two_ranks_two_gpus():
+    # the production multi-GPU path end to end: two processes, one GPU each, the library's own
+    # RCCL communicator for every exchange and broadcast (xGMI), gloo only for the unique id
+    import smlu
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, "poisson_big", 128, q, "rccl", True)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in ps], key=lambda r: r[0])
+    for p in ps:
+        p.join(timeout=120)
+    errs = [r[4] for r in res if r[4]]
+    assert not errs, errs[0]
+    A = _matrix("poisson_big")
+    n = A.shape[0]
+    b = np.random.default_rng(11).random(n)
+    F = smlu.ParallelSparseLU(A)
+    xs = np.empty(n)
+    smlu.ldiv_(xs, F, b)
+    F.close()
+    for rank, x13, x2, info, _ in res:
+        assert info["transport"] == "rccl" and info["shared_fronts"] > 0
+        assert np.allclose(x13[0], xs, rtol=1e-11, atol=1e-13), rank
