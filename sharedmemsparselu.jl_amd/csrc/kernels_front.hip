@@ -807,6 +807,9 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
           const double cur = x[j];
           const bool cand = has && pos >= k;
           const double akk = readlane_f64(cur, q);
+          // the reciprocal of the diagonal candidate starts at once (the usual pivot; its
+          // dependent fp64 chain overlaps the candidate test)
+          double pinv = recip(akk);
           const bool beats = cand && pos != k && fabs(cur) * diag_tol > fabs(akk);
           int p = q;
           if (__ballot(beats) != 0ull || akk == 0.0) {   // full argmax (rare under dominance)
@@ -825,8 +828,8 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
               p = __builtin_amdgcn_readlane(who, __builtin_amdgcn_readfirstlane(ai));
             }
             p = __builtin_amdgcn_readfirstlane(p);
+            pinv = recip(readlane_f64(cur, p));
           }
-          const double pinv = recip(readlane_f64(cur, p));
           double l = 0.0;
           if (cand && lane != p) {
             l = cur * pinv;
