@@ -96,6 +96,7 @@ struct Rhs {
   int64_t ldx, ldv;
 };
 constexpr int kMultiRhs = 16;   // right-hand sides per solve launch
+constexpr int kSweepWK = 4;     // k_tri_sweep: 64-row blocks (worker waves) per work item
 
 // One dense chunk of the reference's solve layout (src/SharedMemSparseLU.jl:101-243), 0-based:
 // the s x s diagonal block over x[c0, c0+s) at data[tri] (column-major, ld s) and the negated

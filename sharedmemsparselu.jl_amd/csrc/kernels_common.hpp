@@ -177,48 +177,72 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// One wave solves a bw x bw (bw <= 64) diagonal block stored column-major at D (ld M): unit
-// lower (UPPER = false, forward) or upper with its diagonal (UPPER = true, backward); lane i
-// holds x_i.  Row i of the block is loaded into registers up front (64 independent loads, one
-// memory latency), so the 64-step chain only waits on readlane broadcasts, never on memory.
-template <bool UPPER>
-// dinv: 1 / (diagonal entry of row `lane`), used by the upper solve only (one reciprocal per lane,
-// computed before the chain).
-__device__ __forceinline__ double tri64_row(double xi, const double (&row)[64], double dinv, int bw, int lane) {
+// Substitution over one 64x64 diagonal block of a large front for a vector held one element per
+// lane (lanes >= bw hold finite values, e.g. 0).  row: this lane's row of the block strictly below
+// (forward, unit diagonal) or strictly above (backward) the diagonal, zero elsewhere, loaded into
+// registers up front -- so every step is one broadcast and one fma over all lanes (lanes outside
+// the triangle add an exact zero) with no exec-mask changes, and the dependent chain per step is
+// readlane + fma.  Backward: column j of row pre-scaled by 1/u_jj (tri64_scale_upper), x_i = xi_i /
+// u_ii applied once at the end (dinv = this lane's 1/u_ii).  Shared by k_tri_block and k_tri_sweep
+// (bitwise equal schedules).
+template <bool UPPER, class RJ>
+__device__ __forceinline__ double tri64_acc(double xi, RJ&& row, double dinv, int bw) {
+  if (bw == 64) {   // full block (all but a front's last): no per-step guard in the chain
+    if (!UPPER) {
+#pragma unroll
+      for (int j = 0; j < 64; ++j) xi = fma(-row(j), readlane_f64(xi, j), xi);
+      return xi;
+    }
+#pragma unroll
+    for (int j = 63; j >= 0; --j) xi = fma(-row(j), readlane_f64(xi, j), xi);
+    return xi * dinv;
+  }
   if (!UPPER) {
 #pragma unroll
-    for (int j = 0; j < 64; ++j) {
-      if (j < bw) {
-        const double xj = readlane_f64(xi, j);
-        if (lane > j) xi = fma(-row[j], xj, xi);
-      }
-    }
-  } else {
-#pragma unroll
-    for (int j = 63; j >= 0; --j) {
-      if (j < bw) {
-        if (lane == j) xi = xi * dinv;
-        const double xj = readlane_f64(xi, j);
-        if (lane < j) xi = fma(-row[j], xj, xi);
-      }
-    }
+    for (int j = 0; j < 64; ++j)
+      if (j < bw) xi = fma(-row(j), readlane_f64(xi, j), xi);
+    return xi;
   }
-  return xi;
-}
-__device__ __forceinline__ void load_row64(double (&row)[64], const double* __restrict__ D, int64_t M, int bw,
-                                           int lane) {
 #pragma unroll
-  for (int j = 0; j < 64; ++j) row[j] = (lane < bw && j < bw) ? D[(int64_t)j * M + lane] : 0.0;
+  for (int j = 63; j >= 0; --j)
+    if (j < bw) xi = fma(-row(j), readlane_f64(xi, j), xi);
+  return xi * dinv;
+}
+template <bool UPPER>
+__device__ __forceinline__ double tri64_row(double xi, const double (&row)[64], double dinv, int bw) {
+  return tri64_acc<UPPER>(xi, [&](int j) { return row[j]; }, dinv, bw);
+}
+// row[j] *= 1/u_jj (held by lane j as dinv), j < bw: the backward row for tri64_row.
+__device__ __forceinline__ void tri64_scale_upper(double (&row)[64], double dinv, int bw) {
+#pragma unroll
+  for (int j = 0; j < 64; ++j)
+    if (j < bw) row[j] *= readlane_f64(dinv, j);
+}
+// This lane's row of the diagonal block D (ld M) for tri64_row: its strictly lower / upper part.
+template <bool UPPER>
+__device__ __forceinline__ void load_tri_row64(double (&row)[64], const double* __restrict__ D, int64_t M, int bw,
+                                               int lane) {
+#pragma unroll
+  for (int j = 0; j < 64; ++j)
+    row[j] = (lane < bw && j < bw && (UPPER ? j > lane : j < lane)) ? D[(int64_t)j * M + lane] : 0.0;
 }
 __device__ __forceinline__ double diag_recip(const double* __restrict__ D, int64_t M, int bw, int lane) {
   return lane < bw ? recip(D[(int64_t)lane * M + lane]) : 1.0;
 }
-template <bool UPPER>
-__device__ __forceinline__ double tri64(double xi, const double* __restrict__ D, int64_t M, int bw,
-                                        int lane) {
-  double row[64];
-  load_row64(row, D, M, bw, lane);
-  return tri64_row<UPPER>(xi, row, UPPER ? diag_recip(D, M, bw, lane) : 1.0, bw, lane);
+
+// sum_{j < bw} d[j] * xj(j) as eight interleaved partial sums (j mod 8) combined pairwise: the
+// dependent fp64 chain is 8 + 3 operations deep instead of 64 (~32 cycles each on gfx950).  The
+// one row-block product of the large-front solves (k_tri_block, k_tri_sweep), so a column of a
+// batched solve stays bitwise equal to the single-vector solve.
+template <class XJ>
+__device__ __forceinline__ double dot64_split(const double (&d)[64], int bw, XJ&& xj) {
+  double a[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a[k] = 0.0;
+#pragma unroll
+  for (int j = 0; j < 64; ++j)
+    if (j < bw) a[j & 7] = fma(d[j], xj(j), a[j & 7]);
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
 // acc += sum_{j < bw} D[j*M + i] * xs[j] (bw <= 64) in ascending j: all loads issued up front.

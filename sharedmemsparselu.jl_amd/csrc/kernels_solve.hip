@@ -507,6 +507,39 @@ __global__ __launch_bounds__(256) void k_fwd_gather(const int32_t* __restrict__ 
   fwd_gather_front<1>(s, sn, chlist, relmap, rowperm, x + r * rh.ldx, vbuf + r * rh.ldv, rh, 1, threadIdx.x);
 }
 
+// Large-front gather, one thread per front row i over as many workgroups as the rows need (the
+// one-workgroup-per-front k_fwd_gather left a 16k-row root to a single CU): the row's pre-pivoting
+// source j = rowperm(i) for pivot rows, itself for update rows; value = own x_j (pivot rows) or 0,
+// plus the children's update-vector entries that map to j, in child order -- per element exactly the
+// additions of k_fwd_gather (bitwise equal).  Writes v only: x is not touched before the forward
+// solve writes every pivot row (the sweep and k_tri_block read v), so no row's original x is
+// overwritten while other workgroups read it.  gptr (per front row, offset ft.pad) -> gent (vbuf
+// index of each contribution).
+template <int NR>
+__global__ __launch_bounds__(256) void k_fwd_pull(const FrontTile* __restrict__ ft, int nft, const SNode* __restrict__ sn,
+                                                  const int32_t* __restrict__ rowperm, const int32_t* __restrict__ gptr,
+                                                  const int32_t* __restrict__ gent, const double* __restrict__ x,
+                                                  double* __restrict__ vbuf, Rhs rh) {
+  const int64_t b = blockIdx.x;
+  const int fi = find_front_tile(ft, nft, b);
+  const SNode s = sn[ft[fi].s];
+  const int64_t i = (b - ft[fi].wg0) * 256 + threadIdx.x;
+  const int64_t M = (int64_t)s.ns + s.nu, ns = s.ns;
+  if (i >= M) return;
+  const int64_t j = i < ns ? rowperm[s.first + i] : i;
+  const int32_t* P = gptr + ft[fi].pad;
+  const int32_t p0 = P[j], p1 = P[j + 1];
+  const int nr = NR == 1 ? 1 : rh.n;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    if (r < nr) {
+      double val = j < ns ? x[r * rh.ldx + s.first + j] : 0.0;
+      for (int32_t p = p0; p < p1; ++p) val = val + vbuf[r * rh.ldv + gent[p]];
+      vbuf[r * rh.ldv + s.voff + i] = val;
+    }
+  }
+}
+
 // One 64-column step of a large front: the first CW waves of every workgroup solve the 64x64
 // diagonal block for the right-hand sides (tri64, the diagonal block's rows loaded once per wave,
 // CW right-hand sides at a time; each workgroup re-solves it, no inter-workgroup hand-off); the
@@ -540,13 +573,14 @@ void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step, const SNod
       xi[k] = (r < nr && lane < bw) ? vbuf[r * rh.ldv + s.voff + jb + lane] : 0.0;
     }
     double row[64];   // the diagonal block's row `lane`, loaded once for all right-hand sides
-    load_row64(row, Lp + jb * M + jb, M, bw, lane);
+    load_tri_row64<UPPER>(row, Lp + jb * M + jb, M, bw, lane);
     const double dinv = UPPER ? diag_recip(Lp + jb * M + jb, M, bw, lane) : 1.0;
+    if (UPPER) tri64_scale_upper(row, dinv, bw);
 #pragma unroll
     for (int k = 0; k < PR; ++k) {
       const int r = wv + k * CW;
       if (r < nr) {
-        const double y = tri64_row<UPPER>(xi[k], row, dinv, bw, lane);
+        const double y = tri64_row<UPPER>(xi[k], row, dinv, bw);
         if (lane < bw) {
           xs[lane][r] = y;
           if (chunk == 0) x[r * rh.ldx + s.first + jb + lane] = y;
@@ -571,10 +605,7 @@ void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step, const SNod
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       if (r < nr) {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < 64; ++j)
-          if (j < bw) acc = fma(d[j], xs[j][r], acc);
+        const double acc = dot64_split(d, bw, [&](int j) { return xs[j][r]; });
         vbuf[r * rh.ldv + s.voff + i] = o[r] - acc;
       }
     }
@@ -686,23 +717,17 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
     for (int j = 0; j < 64; ++j)
       drow[j] = (piv && j < bw && (UPPER ? j > li : j < li)) ? Lp[(64 * b + j) * M + row] : 0.0;
     if (UPPER && piv) dinv = recip(Lp[(64 * b + li) * M + row]);
+    if (UPPER) tri64_scale_upper(drow, dinv, bw);
   }
   double d[64];   // my row of the column block being applied, loaded before its x is available
   auto load_tile = [&](int64_t c, int bw) {
 #pragma unroll
     for (int j = 0; j < 64; ++j) d[j] = j < bw ? Lp[(64 * c + j) * M + row] : 0.0;
   };
-  auto fma_tile = [&](int bw) {   // o -= L[row, block] * x_block (x in xs)
+  auto fma_tile = [&](int bw) {   // o -= L[row, block] * x_block (x in xs), k_tri_block's dot64_split
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      if (r < nr) {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < 64; ++j)
-          if (j < bw) acc = fma(d[j], xs[j][r], acc);
-        o[r] -= acc;
-      }
-    }
+    for (int r = 0; r < NR; ++r)
+      if (r < nr) o[r] -= dot64_split(d, bw, [&](int j) { return xs[j][r]; });
   };
   // external blocks (solved by earlier chunks): forward 0 .. min(4q, nblk)-1, backward nblk-1
   // down to nblk-4q; every row of this chunk lies beyond them
@@ -731,9 +756,9 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
         if (r < nr) {
-          const double y = tri64_row<UPPER>(o[r], drow, dinv, bw, lane);
-          o[r] = y;
+          const double y = tri64_row<UPPER>(o[r], drow, dinv, bw);
           const bool mine = lane < bw && has;
+          if (mine) o[r] = y;
           atomic_write_f64(xhf + (b * kMultiRhs + r) * 64 + lane, mine ? y : 0.0);
           if (mine) {
             xs[lane][r] = y;
@@ -1010,6 +1035,18 @@ hipError_t launch_bwd_tiny(hipStream_t st, int cnt, const int32_t* list, const S
   else k_bwd_tiny<kMaxRhs><<<g, 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf, rh);
   return hipGetLastError();
 }
+hipError_t launch_fwd_pull(hipStream_t st, int64_t nwg, const FrontTile* ft, int nft, const SNode* sn,
+                           const int32_t* rowperm, const int32_t* gptr, const int32_t* gent, const double* x,
+                           double* vbuf, Rhs rh) {
+  if (nwg <= 0) return hipSuccess;
+#define PULL(NR) k_fwd_pull<NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, sn, rowperm, gptr, gent, x, vbuf, rh)
+  if (rh.n <= 1) PULL(1);
+  else if (rh.n <= 4) PULL(4);
+  else if (rh.n <= 8) PULL(8);
+  else PULL(16);
+#undef PULL
+  return hipGetLastError();
+}
 hipError_t launch_fwd_gather(hipStream_t st, int cnt, const int32_t* list, const SNode* sn,
                              const int32_t* chlist, const int32_t* relmap, const int32_t* rowperm,
                              double* x, double* vbuf, Rhs rh) {
@@ -1171,3 +1208,4 @@ hipError_t launch_unswap(hipStream_t st, int64_t n, const int64_t* pos_first, co
 
 
 }  // namespace smlu
+

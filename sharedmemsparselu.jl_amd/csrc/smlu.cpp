@@ -54,6 +54,8 @@ hipError_t launch_fwd_tiny(hipStream_t, int, const int32_t*, const SNode*, const
                            const int32_t*, const double*, double*, double*, Rhs, int);
 hipError_t launch_bwd_tiny(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*, double*,
                            double*, Rhs, int);
+hipError_t launch_fwd_pull(hipStream_t, int64_t, const FrontTile*, int, const SNode*, const int32_t*,
+                           const int32_t*, const int32_t*, const double*, double*, Rhs);
 hipError_t launch_fwd_gather(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                              const int32_t*, double*, double*, Rhs);
 hipError_t launch_tri_block(hipStream_t, bool, int64_t, const FrontTile*, int, int, const SNode*,
@@ -99,7 +101,7 @@ thread_local std::string g_last_error;
 enum Kind : int {
   K_MEMSET_STORE, K_MEMSET_SCRATCH, K_SCATTER, K_EXTADD, K_FRONT_LDS, K_PANEL, K_TRSMU, K_TRSML,
   K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_GEMM22, K_LASWP, K_STEPTRSM, K_GEMMU,
-  K_GEMMO, K_FORK, K_JOIN, K_TRIINV, K_BWDU12C, K_VCOPY, K_FWDT, K_BWDT, K_SWEEPF, K_SWEEPB, K_UROWS, K_NKIND
+  K_GEMMO, K_FORK, K_JOIN, K_TRIINV, K_BWDU12C, K_VCOPY, K_FWDT, K_BWDT, K_SWEEPF, K_SWEEPB, K_UROWS, K_FWDP, K_NKIND
 };
 const char* kKindName[K_NKIND] = {"memset", "memset", "assemble", "assemble", "small", "panel",
                                   "trsm", "trsm", "gemm", "solve", "solve", "solve", "solve",
@@ -352,6 +354,7 @@ struct smlu_handle {
   DBuf<XContrib> xtasks;
   DBuf<int2> aents;
   DBuf<FrontTile> ftiles;
+  DBuf<int32_t> gptr, gent;       // pull lists of the large fronts' forward gather (k_fwd_pull)
   DBuf<int32_t> ssync, sstatus;   // sync-free solve sweeps: block flags (epochs, never reset); timeouts
   DBuf<unsigned long long> stick; // ... one monotone ticket counter per sweep launch
   DBuf<double> sxh;               // ... hand-off slots: 64 x kMultiRhs doubles per flag
@@ -449,6 +452,8 @@ struct smlu_handle {
     xtasks.free();
     aents.free();
     ftiles.free();
+    gptr.free();
+    gent.free();
     ssync.free();
     sstatus.free();
     stick.free();
@@ -626,6 +631,7 @@ static int build_schedule(smlu_handle* h) {
   std::vector<int32_t> ilist;
   std::vector<XContrib> xt;
   std::vector<FrontTile> ft;
+  std::vector<int32_t> gptr, gent;   // k_fwd_pull lists
   std::vector<GemmTask> gt;
   std::vector<SwapTask> st_tasks;
   std::vector<URowTask> ur_tasks;
@@ -1755,11 +1761,38 @@ static int build_schedule(smlu_handle* h) {
       bl.push_back(L);
     }
     if (!bigs.empty()) {
+      // gather: one thread per front row pulls its own value and the children's contributions (in
+      // child order) -- k_fwd_pull; pull lists per front row: gptr (CSR, relative to the front's
+      // block) -> gent (vbuf index of each contribution)
       Launch L;
-      L.kind = K_FWDG;
-      L.off = (int64_t)ilist.size();
-      for (auto s : bigs) ilist.push_back((int32_t)s);
+      L.kind = K_FWDP;
+      L.off = (int64_t)ft.size();
+      int64_t wgp = 0;
+      for (auto s : bigs) {
+        const SNode& r = h->hsn[s];
+        const int64_t M = (int64_t)r.ns + r.nu;
+        ft.push_back(FrontTile{(int32_t)s, (int32_t)gptr.size(), wgp});
+        wgp += (M + 255) / 256;
+        std::vector<int32_t> cnt(M + 1, 0);
+        for (int c = r.chbeg; c < r.chend; ++c) {
+          const SNode& ch = h->hsn[P.ch_list[c]];
+          const int32_t* rm = P.relmap.data() + ch.rowptr;
+          for (int32_t k = 0; k < ch.nu; ++k) ++cnt[rm[k] + 1];
+        }
+        for (int64_t t = 0; t < M; ++t) cnt[t + 1] += cnt[t];
+        const int64_t base = (int64_t)gent.size();
+        for (int64_t t = 0; t <= M; ++t) gptr.push_back((int32_t)(base + cnt[t]));
+        gent.resize(base + cnt[M]);
+        for (int c = r.chbeg; c < r.chend; ++c) {
+          const SNode& ch = h->hsn[P.ch_list[c]];
+          const int32_t* rm = P.relmap.data() + ch.rowptr;
+          for (int32_t k = 0; k < ch.nu; ++k) gent[base + cnt[rm[k]]++] = (int32_t)(ch.voff + ch.ns + k);
+        }
+        if ((int64_t)gptr.size() >= INT32_MAX || (int64_t)gent.size() >= INT32_MAX || r.voff + M >= INT32_MAX)
+          return fail(h, SMLU_ERR_ALLOC, "solve gather lists exceed 32-bit indices");
+      }
       L.cnt = (int64_t)bigs.size();
+      L.nwg = wgp;
       h->fwd.push_back(L);
       int64_t nb = 0;
       for (auto s : bigs) nb = std::max<int64_t>(nb, (h->hsn[s].ns + 63) / 64);
@@ -1786,7 +1819,7 @@ static int build_schedule(smlu_handle* h) {
         for (auto s : bigs) {
           const SNode& r = h->hsn[s];
           ft.push_back(FrontTile{(int32_t)s, fb, wf});
-          wf += ((int64_t)r.ns + r.nu + 255) / 256;
+          wf += ((int64_t)r.ns + r.nu + 64 * kSweepWK - 1) / (64 * kSweepWK);
           fb += (r.ns + 63) / 64;
         }
         F.cnt = (int64_t)bigs.size();
@@ -1802,7 +1835,7 @@ static int build_schedule(smlu_handle* h) {
           const SNode& r = h->hsn[s];
           const int64_t nbs = (r.ns + 63) / 64;
           ft.push_back(FrontTile{(int32_t)s, fb, wb});
-          wb += (nbs + 3) / 4;
+          wb += (nbs + kSweepWK - 1) / kSweepWK;
           fb += (int32_t)nbs;
         }
         B.cnt = (int64_t)bigs.size();
@@ -2126,11 +2159,21 @@ static int build_schedule(smlu_handle* h) {
     }
   }
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
+  if (!gptr.empty()) {
+    HIPCHK(h->gptr.upload(gptr.data(), gptr.size(), st));
+    HIPCHK(h->gent.upload(gent.data(), gent.size(), st));
+  }
   h->ssync_n = ssync_n;
   if (ssync_n > 0) {   // zeroed once per schedule: the sweeps never reset them (epochs, kernels_solve.hip)
     HIPCHK(h->ssync.alloc((size_t)ssync_n));
     HIPCHK(h->stick.alloc((size_t)ntick));
     HIPCHK(h->sxh.alloc((size_t)ssync_n * 64 * kMultiRhs));
+    {   // hand-off slots start as the sweep's sentinel (kernels_solve.hip: k_tri_sweep)
+      const long long sent = 0x7ff4dead5eed0001ll;
+      double sv;
+      std::memcpy(&sv, &sent, sizeof sv);
+      HIPCHK(launch_fill(st, ssync_n * 64 * kMultiRhs, h->sxh.p, sv));
+    }
     HIPCHK(hipMemsetAsync(h->ssync.p, 0, sizeof(int32_t) * ssync_n, st));
     HIPCHK(hipMemsetAsync(h->stick.p, 0, sizeof(unsigned long long) * ntick, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -2595,6 +2638,8 @@ static void release_schedule(smlu_handle* h) {
   h->xtasks.free();
   h->aents.free();
   h->ftiles.free();
+  h->gptr.free();
+  h->gent.free();
   h->ssync.free();
   h->stick.free();
   h->sxh.free();
@@ -2664,6 +2709,9 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, d
                              h->store.p, w, v, rh, (int)L.aux);
     case K_BWDT:
       return launch_bwd_tiny(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->rows.p, h->store.p, w, v, rh, (int)L.aux);
+    case K_FWDP:
+      return launch_fwd_pull(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->sn.p, h->rowperm.p, h->gptr.p, h->gent.p,
+                             w, v, rh);
     case K_FWDG:
       return launch_fwd_gather(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->chlist.p, h->relmap.p,
                                h->rowperm.p, w, v, rh);
