@@ -20,18 +20,22 @@ __device__ __forceinline__ void stage_block(double* __restrict__ sD, const doubl
     if (i < bw) sD[j * 65 + i] = D[(int64_t)j * M + i];
   }
 }
+// Branch-free chain: every lane computes the update and keeps it by a select (no exec-mask changes
+// per step); the upper solve's reciprocal of lane j's pivot is computed before the chain.  Same
+// values as the guarded loop (the selected operation is the same fma / multiply), bitwise.
 template <bool UPPER>
 __device__ __forceinline__ double tri_lds(double xi, const double* __restrict__ sD, int bw, int lane) {
   if (!UPPER) {
     for (int j = 0; j < bw; ++j) {
-      const double xj = readlane_f64(xi, j);
-      if (lane > j && lane < bw) xi = fma(-sD[j * 65 + lane], xj, xi);
+      const double t = fma(-sD[j * 65 + lane], readlane_f64(xi, j), xi);
+      xi = (lane > j && lane < bw) ? t : xi;
     }
   } else {
+    const double dinv = lane < bw ? recip(sD[lane * 65 + lane]) : 1.0;
     for (int j = bw - 1; j >= 0; --j) {
-      if (lane == j) xi = xi * recip(sD[j * 65 + j]);
-      const double xj = readlane_f64(xi, j);
-      if (lane < j) xi = fma(-sD[j * 65 + lane], xj, xi);
+      xi = lane == j ? xi * dinv : xi;
+      const double t = fma(-sD[j * 65 + lane], readlane_f64(xi, j), xi);
+      xi = lane < j ? t : xi;
     }
   }
   return xi;
@@ -669,6 +673,23 @@ __device__ __forceinline__ void sweep_wait(int32_t* f, int32_t epoch, int32_t* s
   __syncthreads();
 }
 
+// Dev instrumentation (tools/sweep_trace.py): one launch shape (grid, direction) records per work item
+// and wave the 100 MHz real-time clock at its start, after its external blocks, before and after its
+// own substitution, after publishing, and at its end.  Compiled in with -DSMLU_SWEEP_TRACE only.
+struct SweepTrace {
+  long long* buf;
+  int nwg, upper;
+};
+__device__ SweepTrace g_sweep_trace;
+__device__ __forceinline__ void sweep_mark(bool upper, int64_t item, int wv, int k) {
+#ifndef SMLU_SWEEP_TRACE   // dev builds only: make CXXFLAGS+=-DSMLU_SWEEP_TRACE
+  return;
+#endif
+  const SweepTrace t = g_sweep_trace;
+  if (t.buf && (int)gridDim.x == t.nwg && (int)upper == t.upper && (threadIdx.x & 63) == 0)
+    t.buf[(item * kSweepWK + wv) * 8 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+}
+
 template <bool UPPER, int NR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* __restrict__ tick,
@@ -682,6 +703,7 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
   __syncthreads();
   const int64_t item = (int64_t)(s_ticket % gridDim.x);
   const int32_t epoch = (int32_t)(s_ticket / gridDim.x) + 1;
+  sweep_mark(UPPER, item, wv, 0);
   const int fi = find_front_tile(ft, nft, item);
   const SNode s = sn[ft[fi].s];
   int32_t* flags = flags0 + ft[fi].pad;
@@ -743,6 +765,7 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
     if (has) fma_tile(bw);
     __syncthreads();
   }
+  sweep_mark(UPPER, item, wv, 1);
   // internal blocks: wave t solves block b and publishes it, the waves beyond apply it
   for (int t = 0; t < 4; ++t) {
     const int64_t b = UPPER ? nblk - 1 - 4 * q - t : 4 * q + t;
@@ -753,6 +776,7 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
     const bool applies = has && (wv > t || (wv == t && myblk >= nblk));
     if (applies) load_tile(b, bw);
     if (wv == t) {
+      sweep_mark(UPPER, item, wv, 2);
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
         if (r < nr) {
@@ -767,13 +791,16 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
           }
         }
       }
+      sweep_mark(UPPER, item, wv, 3);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
     if (tid == 0) (void)__hip_atomic_fetch_max(flags + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) sweep_mark(UPPER, item, t, 4);
     if (applies) fma_tile(bw);
     __syncthreads();
   }
+  sweep_mark(UPPER, item, wv, 5);
   // forward: the update rows leave their value for the parent
   if (!UPPER && has && myblk >= nblk) {
 #pragma unroll
@@ -1209,3 +1236,21 @@ hipError_t launch_unswap(hipStream_t st, int64_t n, const int64_t* pos_first, co
 
 }  // namespace smlu
 
+
+// Dev hook for tools/sweep_trace.py: nwg > 0 arms the trace for sweeps of that grid and direction
+// (n records of 8 clocks); nwg == 0 copies the records to out and disarms.
+extern "C" int smlu_dev_sweep_trace(int nwg, int upper, long long* out, long long n) {
+  static long long* buf = nullptr;
+  using namespace smlu;
+  SweepTrace t{nullptr, 0, 0};
+  if (nwg > 0) {
+    if (buf) (void)hipFree(buf);
+    if (hipMalloc(&buf, sizeof(long long) * 8 * n) != hipSuccess) return -1;
+    (void)hipMemset(buf, 0, sizeof(long long) * 8 * n);
+    t = SweepTrace{buf, nwg, upper};
+  } else if (buf) {
+    (void)hipDeviceSynchronize();
+    if (out && hipMemcpy(out, buf, sizeof(long long) * 8 * n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  }
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_sweep_trace), &t, sizeof t) == hipSuccess ? 0 : -1;
+}

@@ -103,10 +103,11 @@ enum Kind : int {
   K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_GEMM22, K_LASWP, K_STEPTRSM, K_GEMMU,
   K_GEMMO, K_FORK, K_JOIN, K_TRIINV, K_BWDU12C, K_VCOPY, K_FWDT, K_BWDT, K_SWEEPF, K_SWEEPB, K_UROWS, K_FWDP, K_NKIND
 };
-const char* kKindName[K_NKIND] = {"memset", "memset", "assemble", "assemble", "small", "panel",
+const char* kKindName[] = {"memset", "memset", "assemble", "assemble", "small", "panel",
                                   "trsm", "trsm", "gemm", "solve", "solve", "solve", "solve",
                                   "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "sync", "sync", "trsm", "solve", "solve",
-                                  "solve", "solve", "solve", "solve", "urows"};
+                                  "solve", "solve", "solve", "solve", "urows", "solve"};
+static_assert(sizeof(kKindName) / sizeof(kKindName[0]) == K_NKIND, "one kKindName entry per launch kind");
 constexpr int kSolveBigNs = 256;  // fronts with more pivots use the multi-workgroup solve
 // ... and so do fronts whose L panel (M x ns entries) exceeds this: one workgroup streams a
 // tall panel at single-CU bandwidth (a 10^4-row front with 200 pivots took ~350 us per sweep)

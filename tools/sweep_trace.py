@@ -3,7 +3,7 @@ own clock marks (smlu_dev_sweep_trace): per work item (chunk of kSweepWK blocks)
 real-time clock at start / external blocks applied / before and after the substitution / published /
 end.  Prints the per-block chain intervals and the cross-chunk hand-off gaps.
 
-    python tools/sweep_trace.py [--side 128] [--wk 4]
+    (library built with -DSMLU_SWEEP_TRACE) python tools/sweep_trace.py [--side 128] [--wk 4]
 """
 import argparse
 import ctypes
