@@ -419,7 +419,7 @@ def main():
                        "dense_flops": dense_flops, "ordering": args.ordering,
                        "parallelism": (f"tree-partition{world} (proportional mapping, RCCL p2p)"
                                        if partitioned else f"replicas{world}" if world > 1 else "single")},
-            "roofline": {"bound": "mfma", "kernel": "Schur-complement GEMM group: k_gemm128_mfma2 (MFMA 128x128 tile) + k_gemm128_mfma (edge tiles) + k_gemm_k64 + k_gemm (fp64); rocBLAS only with SMLU_ROCBLAS",
+            "roofline": {"bound": "mfma", "kernel": "Schur-complement GEMM group: k_gemm128_mfma2 (fp64 MFMA 128x128 tile) + k_gemm_k64 (k <= 64) + k_gemm (VALU 64x64, small launches)",
                          "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic,

@@ -97,7 +97,9 @@ int smlu_create_with_pivots(int64_t n, const int64_t* colptr, const int64_t* row
  * pattern, new values (nzval in A's original CSC order, host memory). */
 int smlu_refactor(smlu_handle* h, const double* nzval);
 
-/* Same, values already resident in device memory (HBM). */
+/* Same, values already resident in device memory (HBM).  The pivoting mode is re-decided on the
+ * new values (a dominance reduction on the device, read back with one stream synchronisation;
+ * on a partitioned handle the ranks agree on it through the transport's allreduce). */
 int smlu_refactor_device(smlu_handle* h, const double* d_nzval);
 
 /* lu!(F, A) where A's pattern may differ: re-analyses when it does (the reference's

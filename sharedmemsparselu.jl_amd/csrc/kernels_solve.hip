@@ -659,14 +659,22 @@ __device__ __forceinline__ void atomic_write_f64(double* p, double v) {
   (void)__hip_atomic_exchange(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void sweep_wait(int32_t* f, int32_t epoch, int32_t* status) {
+// Bounded wait for flag f to reach the epoch.  A wait that gives up raises *status; the host reads
+// it after every solve and re-runs the solve on the per-block schedule (smlu.cpp: run_solve_dev), so
+// a timed-out chunk's values are never returned.  spin <= 0 reports every wait as timed out (the
+// tests' forced-fallback knob SMLU_SWEEP_SPIN=0).
+__device__ __forceinline__ void sweep_wait(int32_t* f, int32_t epoch, int32_t* status, int spin) {
   if (threadIdx.x == 0) {
-    int n = 0;
-    while (atomic_read_i32(f) < epoch) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++n > (1 << 22)) {
-        (void)__hip_atomic_fetch_max(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
+    if (spin <= 0) {
+      (void)__hip_atomic_fetch_max(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      int n = 0;
+      while (atomic_read_i32(f) < epoch) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++n > spin) {
+          (void)__hip_atomic_fetch_max(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
       }
     }
   }
@@ -675,27 +683,29 @@ __device__ __forceinline__ void sweep_wait(int32_t* f, int32_t epoch, int32_t* s
 
 // Dev instrumentation (tools/sweep_trace.py): one launch shape (grid, direction) records per work item
 // and wave the 100 MHz real-time clock at its start, after its external blocks, before and after its
-// own substitution, after publishing, and at its end.  Compiled in with -DSMLU_SWEEP_TRACE only.
+// own substitution, after publishing, and at its end.  Compiled in with -DSMLU_SWEEP_TRACE only
+// (make CXXFLAGS+=-DSMLU_SWEEP_TRACE); the product build has neither the buffer nor the hook.
+#ifdef SMLU_SWEEP_TRACE
 struct SweepTrace {
   long long* buf;
   int nwg, upper;
 };
 __device__ SweepTrace g_sweep_trace;
 __device__ __forceinline__ void sweep_mark(bool upper, int64_t item, int wv, int k) {
-#ifndef SMLU_SWEEP_TRACE   // dev builds only: make CXXFLAGS+=-DSMLU_SWEEP_TRACE
-  return;
-#endif
   const SweepTrace t = g_sweep_trace;
   if (t.buf && (int)gridDim.x == t.nwg && (int)upper == t.upper && (threadIdx.x & 63) == 0)
     t.buf[(item * kSweepWK + wv) * 8 + k] = (long long)__builtin_amdgcn_s_memrealtime();
 }
+#else
+__device__ __forceinline__ void sweep_mark(bool, int64_t, int, int) {}
+#endif
 
 template <bool UPPER, int NR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* __restrict__ tick,
                  int32_t* __restrict__ flags0, double* __restrict__ xh, int32_t* __restrict__ status,
                  const SNode* __restrict__ sn, const double* __restrict__ store, double* __restrict__ x,
-                 double* __restrict__ vbuf, Rhs rh) {
+                 double* __restrict__ vbuf, Rhs rh, int spin) {
   __shared__ double xs[64][NR];
   __shared__ unsigned long long s_ticket;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -758,9 +768,9 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
     const int64_t c = UPPER ? nblk - 1 - e : e;
     const int bw = (int)min<int64_t>(64, ns - 64 * c);
     if (has) load_tile(c, bw);
-    sweep_wait(flags + c, epoch, status);
+    sweep_wait(flags + c, epoch, status, spin);
     if (wv == 0)
-      for (int r = 0; r < nr; ++r) xs[lane][r] = atomic_read_f64(xhf + (c * kMultiRhs + r) * 64 + lane);
+      for (int r = 0; r < min(nr, NR); ++r) xs[lane][r] = atomic_read_f64(xhf + (c * kMultiRhs + r) * 64 + lane);
     __syncthreads();
     if (has) fma_tile(bw);
     __syncthreads();
@@ -1110,16 +1120,12 @@ hipError_t launch_bwd_u12(hipStream_t st, int64_t nwg, const FrontTile* ft, int 
 }
 hipError_t launch_tri_sweep(hipStream_t st, bool upper, int64_t nwg, const FrontTile* ft, int nft,
                             unsigned long long* tick, int32_t* flags, double* xh, int32_t* status, const SNode* sn,
-                            const double* store, double* x, double* vbuf, Rhs rh) {
+                            const double* store, double* x, double* vbuf, Rhs rh, int spin) {
   if (nwg <= 0) return hipSuccess;
-#define SWEEP(NR)                                                                                                   \
-  (upper ? (k_tri_sweep<true, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh)) \
-         : (k_tri_sweep<false, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh)))
-  if (rh.n <= 1) SWEEP(1);
-  else if (rh.n <= 4) SWEEP(4);
-  else if (rh.n <= 8) SWEEP(8);
-  else SWEEP(16);
-#undef SWEEP
+  // one right-hand side: batches take the per-block schedule (k_tri_block), DESIGN §4
+  if (rh.n != 1) return hipErrorInvalidValue;
+  if (upper) k_tri_sweep<true, 1><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh, spin);
+  else k_tri_sweep<false, 1><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh, spin);
   return hipGetLastError();
 }
 hipError_t launch_residual(hipStream_t st, int64_t n, const int64_t* rowptr, const int32_t* ent,
@@ -1237,6 +1243,7 @@ hipError_t launch_unswap(hipStream_t st, int64_t n, const int64_t* pos_first, co
 }  // namespace smlu
 
 
+#ifdef SMLU_SWEEP_TRACE
 // Dev hook for tools/sweep_trace.py: nwg > 0 arms the trace for sweeps of that grid and direction
 // (n records of 8 clocks); nwg == 0 copies the records to out and disarms.
 extern "C" int smlu_dev_sweep_trace(int nwg, int upper, long long* out, long long n) {
@@ -1254,3 +1261,4 @@ extern "C" int smlu_dev_sweep_trace(int nwg, int upper, long long* out, long lon
   }
   return hipMemcpyToSymbol(HIP_SYMBOL(g_sweep_trace), &t, sizeof t) == hipSuccess ? 0 : -1;
 }
+#endif

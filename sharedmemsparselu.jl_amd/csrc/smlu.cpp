@@ -63,7 +63,7 @@ hipError_t launch_tri_block(hipStream_t, bool, int64_t, const FrontTile*, int, i
 hipError_t launch_bwd_u12(hipStream_t, int64_t, const FrontTile*, int, const SNode*, const int32_t*,
                           const double*, const double*, double*, Rhs);
 hipError_t launch_tri_sweep(hipStream_t, bool, int64_t, const FrontTile*, int, unsigned long long*, int32_t*, double*,
-                            int32_t*, const SNode*, const double*, double*, double*, Rhs);
+                            int32_t*, const SNode*, const double*, double*, double*, Rhs, int);
 hipError_t launch_fwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                       const int32_t*, const double*, double*, double*, Rhs);
 hipError_t launch_bwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*,
@@ -366,7 +366,9 @@ struct smlu_handle {
   DBuf<XCol> xcols;
   // schedule
   std::vector<Launch> fac, fwd, bwd;
-  std::vector<Launch> fwdm, bwdm;   // one GPU, batched right-hand sides: per-block launches instead of sweeps
+  std::vector<Launch> fwdm, bwdm;   // per-block launches instead of sweeps: batched right-hand sides (one
+                                    // GPU) and the re-run of a solve whose sweep wait timed out
+  std::vector<size_t> fwdm_seg, bwdm_seg;   // their segment starts (the comm steps of fwd / bwd)
   std::vector<SNode> hsn;
   double gemm_flops = 0, gemm22_flops = 0, dense_flops = 0;
   int64_t gemm_launches = 0, gemm128_launches = 0;
@@ -379,6 +381,10 @@ struct smlu_handle {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   std::vector<int> ev_kind;
   int32_t* hinfo = nullptr;  // pinned
+  int32_t* hsstat = nullptr; // pinned copy of sstatus, read after every solve that ran sweeps
+  int64_t sweep_timeouts = 0;   // solves re-run on the per-block schedule after a sweep wait timed out
+  int sweep_spin = 1 << 22;     // polls before a sweep wait gives up (SMLU_SWEEP_SPIN; 0 = always, tests)
+  DBuf<double> bstash;          // the solve's input when the final step overwrites it (x === b, lsolve!/rsolve!)
   std::vector<std::pair<int, hipGraphExec_t>> sol_execs;   // captured solve sweeps, keyed by mode/rhs count
   std::vector<hipGraphExec_t> fac_execs;   // one captured graph per factor segment
   int fac_exec_profile = -1;
@@ -434,7 +440,7 @@ struct smlu_handle {
     if (stream) (void)hipSetDevice(device);
     release_graphs();
     DBuf<double>* d[] = {&A, &Rs, &store, &scratch, &wrk, &wrk2, &vbuf, &vbufm, &wrkm, &wrk2m, &growth, &ref_b, &ref_r, &ref_d, &ref_nrm,
-                         &tinv, &ch_data};
+                         &tinv, &ch_data, &bstash};
     ch_desc.free();
     ch_p.free();
     ch_q.free();
@@ -497,6 +503,8 @@ struct smlu_handle {
     ev_kind.clear();
     if (hinfo) (void)hipHostFree(hinfo);
     hinfo = nullptr;
+    if (hsstat) (void)hipHostFree(hsstat);
+    hsstat = nullptr;
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     ev_fork = ev_join = nullptr;
@@ -2121,10 +2129,11 @@ static int build_schedule(smlu_handle* h) {
   HIPCHK(h->aents.upload(ae.data(), ae.size(), st));
   // batched right-hand sides (one GPU): the sweep's single chain wave per block would run the NR
   // chains one after another, so batches keep the per-64-column-block launches (k_tri_block: the
-  // diagonal block solved by four chain waves for four right-hand sides at a time)
+  // diagonal block solved by four chain waves for four right-hand sides at a time).  The same
+  // per-block sequences (with the comm segments of fwd / bwd) re-run a solve whose sweep timed out.
   h->fwdm.clear();
   h->bwdm.clear();
-  if (h->nranks == 1) {
+  {
     auto expand = [&](const Launch& S, bool upper, std::vector<Launch>& out) {
       std::vector<int32_t> fr;
       for (int64_t i = S.off; i < S.off + S.cnt; ++i) fr.push_back(ft[i].s);
@@ -2150,14 +2159,20 @@ static int build_schedule(smlu_handle* h) {
         out.push_back(F);
       }
     };
-    for (const Launch& L : h->fwd) {
-      if (L.kind == K_SWEEPF) expand(L, false, h->fwdm);
-      else h->fwdm.push_back(L);
-    }
-    for (const Launch& L : h->bwd) {
-      if (L.kind == K_SWEEPB) expand(L, true, h->bwdm);
-      else h->bwdm.push_back(L);
-    }
+    auto expand_all = [&](const std::vector<Launch>& in, const std::vector<size_t>& seg, bool upper,
+                          std::vector<Launch>& out, std::vector<size_t>& oseg) {
+      std::vector<size_t> at(in.size() + 1);
+      for (size_t i = 0; i < in.size(); ++i) {
+        at[i] = out.size();
+        if (in[i].kind == (upper ? K_SWEEPB : K_SWEEPF)) expand(in[i], upper, out);
+        else out.push_back(in[i]);
+      }
+      at[in.size()] = out.size();
+      oseg.clear();
+      for (size_t k : seg) oseg.push_back(at[std::min(k, in.size())]);
+    };
+    expand_all(h->fwd, h->fwd_seg, false, h->fwdm, h->fwdm_seg);
+    expand_all(h->bwd, h->bwd_seg, true, h->bwdm, h->bwdm_seg);
   }
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
   if (!gptr.empty()) {
@@ -2183,6 +2198,9 @@ static int build_schedule(smlu_handle* h) {
     HIPCHK(h->sstatus.alloc(1));
     HIPCHK(hipMemsetAsync(h->sstatus.p, 0, sizeof(int32_t), st));
   }
+  if (!h->hsstat) HIPCHK(hipHostMalloc((void**)&h->hsstat, sizeof(int32_t), 0));
+  *h->hsstat = 0;
+  if (const char* e = std::getenv("SMLU_SWEEP_SPIN")) h->sweep_spin = std::atoi(e);
   if (h->nranks > 1) max_list = std::max<int64_t>(max_list, dist_slots);
   if (!tinv_patch.empty() || h->nranks > 1) {   // operands in the tile-inverse slots: patch in the buffer address
     HIPCHK(h->tinv.alloc((size_t)max_list * 8192));
@@ -2729,7 +2747,7 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, d
     case K_SWEEPB:
       return launch_tri_sweep(st, L.kind == K_SWEEPB, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->stick.p + L.aux2,
                               h->ssync.p + L.aux, h->sxh.p + L.aux * 64 * kMultiRhs, h->sstatus.p, h->sn.p, h->store.p,
-                              w, v, rh);
+                              w, v, rh, h->sweep_spin);
     case K_BWDU12C:
       return launch_bwd_u12_cols(st, h->sn.p, L.node, h->hsn[L.node].ns, L.aux, L.aux2, (int)L.cnt, h->rows.p,
                                  h->store.p, w, h->vbuf.p);
@@ -2762,9 +2780,25 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
     v = h->vbufm.p;
     rh.n = nrhs;
   }
-  if (mode == 0) HIPCHK(launch_perm_in(st, P.n, h->p0.p, h->Rs.p, db, w, nrhs, ldb > 0 ? ldb : P.n, rh.ldx));
-  if (mode == 1) HIPCHK(launch_unswap(st, P.n, h->posfirst.p, h->rowperm.p, dx, w));
-  if (mode == 2) HIPCHK(hipMemcpyAsync(w, dx, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st));
+  const bool batch = rh.n > 1 && h->nranks == 1;
+  // The sync-free sweeps' waits are bounded: a wait that gives up raises sstatus, which is read back
+  // after every solve that ran them; the solve is then re-run on the per-block schedule (fwdm / bwdm,
+  // bitwise the same arithmetic), so a timed-out sweep never returns a wrong x.  Partitioned handles
+  // agree on the re-run (allreduce of the flag: the per-block sequences hold the same comm steps).
+  const bool check = !batch && (h->ssync_n > 0 || h->nranks > 1);
+  const double* src = mode == 0 ? db : dx;
+  auto load_input = [&](const double* in) -> hipError_t {
+    if (mode == 0) return launch_perm_in(st, P.n, h->p0.p, h->Rs.p, in, w, nrhs, ldb > 0 ? ldb : P.n, rh.ldx);
+    if (mode == 1) return launch_unswap(st, P.n, h->posfirst.p, h->rowperm.p, in, w);
+    return hipMemcpyAsync(w, in, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st);
+  };
+  const double* rerun_src = src;
+  if (check && (mode != 0 || db == dx)) {   // the final step overwrites the input: keep a copy for a re-run
+    if (!h->bstash.p) HIPCHK(h->bstash.alloc((size_t)P.n));
+    HIPCHK(hipMemcpyAsync(h->bstash.p, src, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st));
+    rerun_src = h->bstash.p;
+  }
+  HIPCHK(load_input(src));
   // launches between communication steps (one GPU: a single segment each)
   auto run_seq = [&](const std::vector<Launch>& seq, const std::vector<size_t>& seg, const std::vector<int>& cm) {
     for (size_t k = 0; k < seg.size(); ++k) {
@@ -2777,18 +2811,20 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
     }
     return (int)SMLU_OK;
   };
-  auto sweeps = [&]() {
-    const bool batch = rh.n > 1 && h->nranks == 1;
-    static const std::vector<size_t> seg0(1, 0);
+  auto sweeps = [&](bool steps) {   // steps: the per-block sequences instead of the sweeps
     if (mode != 2) {
-      int rc = batch ? run_seq(h->fwdm, seg0, h->fwd_comm) : run_seq(h->fwd, h->fwd_seg, h->fwd_comm);
+      int rc = steps ? run_seq(h->fwdm, h->fwdm_seg, h->fwd_comm) : run_seq(h->fwd, h->fwd_seg, h->fwd_comm);
       if (rc != SMLU_OK) return rc;
     }
     if (mode != 1) {
-      int rc = batch ? run_seq(h->bwdm, seg0, h->bwd_comm) : run_seq(h->bwd, h->bwd_seg, h->bwd_comm);
+      int rc = steps ? run_seq(h->bwdm, h->bwdm_seg, h->bwd_comm) : run_seq(h->bwd, h->bwd_seg, h->bwd_comm);
       if (rc != SMLU_OK) return rc;
     }
     return (int)SMLU_OK;
+  };
+  auto finish = [&]() -> hipError_t {
+    if (mode == 0) return launch_perm_out(st, P.n, h->q.p, w, dx, nrhs, rh.ldx, ldx > 0 ? ldx : P.n);
+    return hipMemcpyAsync(dx, w, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st);
   };
   // One GPU: the forward and backward sweeps (~1,400 launches at 128^3, fixed pointers: the
   // handle's wrk / vbuf) are captured once per (mode, rhs count) into a hipGraph and replayed;
@@ -2802,7 +2838,7 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
     if (!ex) {
       hipGraph_t g = nullptr;
       HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
-      int rc = sweeps();
+      int rc = sweeps(batch);
       hipError_t ec = hipStreamEndCapture(st, &g);
       if (rc == SMLU_OK && ec == hipSuccess && g) ec = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
       if (g) (void)hipGraphDestroy(g);
@@ -2816,18 +2852,33 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
     }
     if (ex) HIPCHK(hipGraphLaunch(ex, st));
     else {
-      int rc = sweeps();
+      int rc = sweeps(batch);
       if (rc != SMLU_OK) return rc;
     }
   } else {
-    int rc = sweeps();
+    int rc = sweeps(batch);
     if (rc != SMLU_OK) return rc;
   }
-  if (mode == 0) HIPCHK(launch_perm_out(st, P.n, h->q.p, w, dx, nrhs, rh.ldx, ldx > 0 ? ldx : P.n));
-  else HIPCHK(hipMemcpyAsync(dx, w, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st));
+  if (check) HIPCHK(hipMemcpyAsync(h->hsstat, h->sstatus.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  HIPCHK(finish());
   HIPCHK(tm.end(stop));
   HIPCHK(hipStreamSynchronize(st));
   tm.collect();
+  if (check) {
+    double bad = *h->hsstat != 0 ? 1.0 : 0.0;
+    if (h->nranks > 1 && h->tr.allreduce_max(h->tr.ctx, &bad, 1) != 0)
+      return fail(h, SMLU_ERR_HIP, "transport allreduce failed (sweep status)");
+    if (bad != 0) {
+      ++h->sweep_timeouts;
+      *h->hsstat = 0;
+      HIPCHK(hipMemsetAsync(h->sstatus.p, 0, sizeof(int32_t), st));
+      HIPCHK(load_input(rerun_src));
+      int rc = sweeps(true);
+      if (rc != SMLU_OK) return rc;
+      HIPCHK(finish());
+      HIPCHK(hipStreamSynchronize(st));
+    }
+  }
   h->solve_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return SMLU_OK;
 }
@@ -2991,9 +3042,15 @@ static int ensure_residual(smlu_handle* h);
 
 // Pivoting mode per refactor: dominant values take the diagonal-tile path for
 // the mid-size fronts; a handle left in full-candidate mode by a re-pivoting refactor returns to
-// the fast schedule once the values are dominant again.  Every rank of a partitioned handle sees
-// the same values and takes the same decision.
+// the fast schedule once the values are dominant again.  The ranks of a partitioned handle agree
+// on the decision (any rank seeing non-dominant values makes it non-dominant for all): a rebuild
+// on only some ranks would split the collective schedule.
 static int apply_dominance(smlu_handle* h, bool dom) {
+  if (h->nranks > 1) {
+    double nd = dom ? 0.0 : 1.0;
+    if (h->tr.allreduce_max(h->tr.ctx, &nd, 1) != 0) return fail(h, SMLU_ERR_HIP, "transport allreduce failed (dominance)");
+    dom = nd == 0.0;
+  }
   bool changed = false;
   if (dom != h->dominant) {
     h->dominant = dom;
@@ -4018,7 +4075,10 @@ double smlu_stat(const smlu_handle* h, const char* key) {
     return c;
   }
   if (k == "repivots") return (double)h->repivots;
-  if (k == "sweep_timeouts") {   // a sync-free solve sweep's wait ever timed out (never expected)
+  if (k == "sweep_timeouts") {   // solves re-run on the per-block schedule after a sweep wait timed out
+    return (double)h->sweep_timeouts;
+  }
+  if (k == "sweep_status") {     // the device flag itself (cleared whenever a solve reports it)
     int32_t v = 0;
     if (h->sstatus.p && hipMemcpy(&v, h->sstatus.p, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return -1;
     return v;

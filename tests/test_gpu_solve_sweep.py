@@ -88,3 +88,46 @@ def test_single_batch_single_sequence_bitwise(gpu):
     assert np.abs(A @ xh - bh).max() <= 1e-12 * np.abs(bh).max()
     assert F.stat("sweep_timeouts") == 0
     F.close()
+
+
+@pytest.mark.parametrize("name", ["poisson3d_28", "dense_1100"])
+def test_forced_sweep_timeout_reruns_per_block(gpu, monkeypatch, name):
+    """A sweep wait that gives up must never leave a wrong x: with SMLU_SWEEP_SPIN=0
+    every wait reports a timeout; each solve reads the flag back, re-runs on the per-block schedule
+    and returns the per-block schedule's x bitwise -- for ldiv! into a separate x, in place
+    (x === b, the input kept for the re-run), and for the in-place lsolve!/rsolve!."""
+    import torch
+    A = _cases()[name]
+    n = A.shape[0]
+    F = smlu.ParallelSparseLU(A)                        # normal spin bound
+    monkeypatch.setenv("SMLU_SWEEP_SPIN", "0")
+    Ft = smlu.ParallelSparseLU(A)                       # every sweep wait times out
+    monkeypatch.delenv("SMLU_SWEEP_SPIN")
+    assert Ft.stat("solve_sweeps") > 0
+    b = np.random.default_rng(5).random(n)
+    x = np.empty(n)
+    smlu.ldiv_(x, F, b)
+    xt = np.empty(n)
+    smlu.ldiv_(xt, Ft, b)
+    assert Ft.stat("sweep_timeouts") == 1 and Ft.stat("sweep_status") == 0
+    assert np.array_equal(x, xt)
+    # x === b on the device
+    dev = torch.device("cuda:0")
+    bd = torch.from_numpy(b).to(dev)
+    Ft.solve_device(bd, bd)
+    assert np.array_equal(bd.cpu().numpy(), x)
+    assert Ft.stat("sweep_timeouts") == 2
+    # lsolve!/rsolve! in place
+    w = np.random.default_rng(6).random(n)
+    wl, wlt = w.copy(), w.copy()
+    smlu.lsolve_(F, wl)
+    smlu.lsolve_(Ft, wlt)
+    assert np.array_equal(wl, wlt)
+    wu, wut = w.copy(), w.copy()
+    smlu.rsolve_(F, wu)
+    smlu.rsolve_(Ft, wut)
+    assert np.array_equal(wu, wut)
+    assert Ft.stat("sweep_timeouts") == 4
+    assert F.stat("sweep_timeouts") == 0
+    F.close()
+    Ft.close()
