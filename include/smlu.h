@@ -54,8 +54,9 @@ typedef struct smlu_opts {
     int32_t scale;        /* 1 = UMFPACK SUM row scaling Rs[i] = 1/sum_j |a_ij| (default), 0 = none */
     int32_t relax;        /* 1 = relaxed supernode amalgamation (default) */
     double  pivot_tol;    /* threshold partial pivoting tolerance (UMFPACK default 0.1) */
-    double  diag_pivot_tol; /* diagonal preference: keep a_kk unless some candidate exceeds
-                               |a_kk|/diag_pivot_tol (default 0.1; UMFPACK's symmetric default 0.001) */
+    double  diag_pivot_tol; /* diagonal preference: keep a_kk when |a_kk| >= diag_pivot_tol times the
+                               largest candidate (default 0.001 = UMFPACK's symmetric-strategy
+                               SYM_PIVOT_TOLERANCE); otherwise the largest candidate is taken */
     int32_t device;       /* HIP device ordinal (default 0) */
     int32_t profile;      /* 1 = record per-kernel-class HIP events during refactor/solve */
     int64_t leaf_size;    /* nested-dissection leaf size (default 64) */

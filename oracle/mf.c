@@ -14,9 +14,12 @@
  *  - fronts are assembled from the scaled entries Rs[i]*a_ij of (Rs.*A)[p0, q] and the
  *    children's Schur complements, children in ascending (postorder) order;
  *  - each front eliminates its ns fully-summed columns with threshold partial pivoting over a
- *    candidate set of its fully-summed rows (UMFPACK's rule, pivot_tol 0.1, with diagonal
- *    preference): the diagonal entry a_kk is kept unless a candidate exceeds |a_kk|/diag_tol or
- *    a_kk == 0; otherwise the candidate of largest magnitude (smallest position on ties);
+ *    candidate set of its fully-summed rows.  The diagonal test is UMFPACK's symmetric-strategy
+ *    rule (its published default Control[UMFPACK_SYM_PIVOT_TOLERANCE] = 0.001, the library's
+ *    default diag_tol): a_kk is kept when |a_kk| >= diag_tol * max|candidate| and a_kk != 0;
+ *    otherwise the candidate of largest magnitude (smallest position on ties).  UMFPACK would
+ *    instead take, among the candidates passing its 0.1 threshold, the row of least degree -- a
+ *    sparsity criterion that has no meaning inside a dense front;
  *  - candidate set per front mode: 0/1 = every remaining fully-summed row, 2 = the remaining rows
  *    of the 64 x 64 diagonal tile holding the column;
  *  - flags per front: 1 = a candidate column is entirely zero (singular), 2 = a weak pivot: a

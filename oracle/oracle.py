@@ -176,7 +176,7 @@ class MultifrontalOracle:
     smlu_plan_fronts plus the column order `q`; `mode`: candidate set per front (None: every
     fully-summed row).  factor(values) -> status (0 ok, 1 zero candidate column)."""
 
-    def __init__(self, A, q, fronts, mode=None, diag_tol=0.1, pivot_tol=0.1, threads=1):
+    def __init__(self, A, q, fronts, mode=None, diag_tol=0.001, pivot_tol=0.1, threads=1):
         A, cp, ri, _ = _csc(A)
         self.n = A.shape[0]
         self._keep = [np.ascontiguousarray(v, dtype=np.int64) for v in
@@ -240,7 +240,7 @@ def front_modes(fronts, pivmode, dominant_values, full_piv_ns=None):
 
 
 def gpu_pivot_choice(A, q, fronts, *, pivmode=0, dominant_values=None, given=False, pivot_tol=0.1,
-                     diag_tol=0.1, full_piv_ns=None, values=None):
+                     diag_tol=0.001, full_piv_ns=None, values=None):
     """Independent restatement of the GPU path's whole pivot decision for one factorization:
     the candidate modes, threshold partial pivoting inside every front (mf.c), and the
     re-pivoting refactor (a zero or weak pivot while diagonal-tile fronts exist -> every blocked

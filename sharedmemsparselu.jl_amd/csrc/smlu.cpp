@@ -3006,7 +3006,7 @@ void smlu_default_opts(smlu_opts* o) {
   o->scale = 1;
   o->relax = 1;
   o->pivot_tol = 0.1;
-  o->diag_pivot_tol = 0.1;
+  o->diag_pivot_tol = 0.001;   // UMFPACK's symmetric-strategy default (SYM_PIVOT_TOLERANCE)
   o->device = 0;
   o->profile = 0;
   o->leaf_size = 64;
@@ -4075,6 +4075,8 @@ double smlu_stat(const smlu_handle* h, const char* key) {
     return c;
   }
   if (k == "repivots") return (double)h->repivots;
+  if (k == "pivot_tol") return h->opts.pivot_tol;
+  if (k == "diag_pivot_tol") return h->plan.given_order ? 0.0 : h->opts.diag_pivot_tol;
   if (k == "sweep_timeouts") {   // solves re-run on the per-block schedule after a sweep wait timed out
     return (double)h->sweep_timeouts;
   }

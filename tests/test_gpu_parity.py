@@ -132,6 +132,9 @@ def _tile_pivoting_matrix(n, seed):
         blk = rng.random((b1 - b0, b1 - b0)) * n
         np.fill_diagonal(blk, 1e-3)
         D[b0:b1, b0:b1] += blk
+    # diagonal entries below 0.001 x the tile's column maxima: exchanges under UMFPACK's symmetric
+    # diagonal tolerance (0.001, the default) as well
+    np.fill_diagonal(D, 1e-3 * rng.random(n))
     return D
 
 

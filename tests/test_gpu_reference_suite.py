@@ -139,3 +139,19 @@ def test_golden_with_given_pivots(gpu, path):
     x = np.empty(n)
     smlu.ldiv_(x, F, z["b"])
     np.testing.assert_allclose(x, z["x"], rtol=1e-10, atol=1e-12)
+
+
+def test_c1_fixture_default_analysis(gpu):
+    """C1 (BASELINE configs[0]) through the default constructor: the GPU's own
+    analysis and pivot choice reproduce the fixture's (p, q) bit for bit, its L/U pattern hashes,
+    and its sampled values / column sums and solution to 1e-12."""
+    from test_oracle import C1, check_c1_digest
+    z = np.load(C1, allow_pickle=False)
+    n = int(z["n"])
+    A = sp.csc_matrix((z["A_data"], z["A_indices"], z["A_indptr"]), shape=(n, n))
+    F = smlu.ParallelSparseLU(A)
+    assert np.array_equal(F.q, z["q"]) and np.array_equal(F.p, z["p"])
+    x = np.empty(n)
+    smlu.ldiv_(x, F, z["b"])
+    check_c1_digest(z, F.L, F.U, F.Rs, x, 1e-12)
+    F.close()

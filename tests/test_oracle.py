@@ -3,6 +3,7 @@ known answers, the reference's chunked-solve layout, and the reference's own six
 (test/runtests.jl:38-188) restated with the oracle as the factorization."""
 import glob
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -56,6 +57,41 @@ def test_oracle_matches_golden(path):
     x = np.empty(A.shape[0])
     F.ldiv(x, z["b"])
     np.testing.assert_allclose(x, z["x"], rtol=1e-13, atol=1e-14)
+
+
+C1 = os.path.join(HERE, "golden", "c1", "c1_random_1000.npz")
+
+
+def check_c1_digest(z, L, U, Rs, x, rtol):
+    """The C1 fixture's digests (tests/golden/make_golden.py: save_c1) against factors L, U."""
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from make_golden import factor_digest, pattern_hash
+    assert np.array_equal(Rs, z["Rs"]), "row scaling must be bitwise identical"
+    for tag, M in (("L", L), ("U", U)):
+        assert M.nnz == int(z[f"{tag}_nnz"]) and pattern_hash(M) == str(z[f"{tag}_hash"]), f"{tag} pattern differs"
+        cs, sq, vals = factor_digest(M, z[f"{tag}_pick"])
+        np.testing.assert_allclose(vals, z[f"{tag}_pickval"], rtol=rtol, atol=rtol)
+        np.testing.assert_allclose(cs, z[f"{tag}_colsum"], rtol=rtol, atol=rtol * np.abs(z[f"{tag}_colsum"]).max())
+        np.testing.assert_allclose(sq, z[f"{tag}_colsq"], rtol=rtol, atol=rtol * np.abs(z[f"{tag}_colsq"]).max())
+    np.testing.assert_allclose(x, z["x"], rtol=rtol, atol=rtol)
+
+
+def test_c1_fixture_oracle_and_plan():
+    """C1 (n=1000, seed 47).  The generator is deterministic: the matrix, the
+    plan's default column order and the oracle's factors reproduce the committed digests."""
+    from smlu import matrices as mats
+    from smlu.plan import Plan
+    z = np.load(C1, allow_pickle=False)
+    n = int(z["n"])
+    A = sp.csc_matrix((z["A_data"], z["A_indices"], z["A_indptr"]), shape=(n, n))
+    A0 = mats.random_dominant(1000, 0.01, 47)
+    assert np.array_equal(A0.indptr, A.indptr) and np.array_equal(A0.indices, A.indices)
+    assert np.array_equal(A0.data, A.data)
+    assert np.array_equal(Plan(A).q(), z["q"]), "the analysis' column order changed"
+    F = O.OracleLU(A, z["p"], z["q"])
+    x = np.empty(n)
+    F.ldiv(x, z["b"])
+    check_c1_digest(z, F.L, F.U, F.Rs, x, 1e-14)
 
 
 def _rand_sparse(rng, n, dens):
