@@ -18,6 +18,8 @@
 
 #include "plan.hpp"
 
+#include <cstdio>
+
 namespace smlu {
 
 int64_t Plan::local_index(int64_t s, int64_t g) const {
@@ -647,11 +649,15 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
 }
 
 // ---------------------------------------------------------------------------------------
-// Multi-GPU partition of the assembly tree (subtree-to-rank mapping).  Repeatedly split the
-// heaviest subtree into its children (the split front stays above, as a "top" front) until no
-// subtree exceeds the per-rank share; bin-pack the subtrees onto the ranks (largest first,
-// least-loaded rank); a top front goes to the rank of its heaviest child, so the largest
-// update block never crosses GPUs.
+// Multi-GPU partition of the assembly tree: proportional mapping by recursive bisection.  A set of
+// subtrees is mapped onto a contiguous rank range [r0, r1): one rank takes them all; a single
+// subtree on several ranks makes its root a shared ("top") front of the whole range and maps its
+// children onto the same range; several subtrees are split into two sets of balanced work (largest
+// first, onto the lighter set) and the range is cut in proportion to the two sets' work.  Sibling
+// shared fronts therefore have DISJOINT rank groups and run concurrently, and every group is a
+// contiguous range (nested or disjoint: a rank belongs to at most one shared front per tree level).
+// (Rounds 1-3 bin-packed the subtrees onto ranks, which put one rank under several siblings and
+// serialised their shared fronts: 2.70x projected at 128^3 on 8 ranks, SMLU_PARTITION=binpack.)
 // ---------------------------------------------------------------------------------------
 void Plan::compute_owners(int np, int64_t block) {
   nparts = std::max(1, np);
@@ -662,43 +668,107 @@ void Plan::compute_owners(int np, int64_t block) {
   std::vector<double> W(front_flops.begin(), front_flops.end());   // subtree work
   for (int64_t s = 0; s < nsup; ++s)
     if (s_parent[s] >= 0) W[s_parent[s]] += W[s];
-  std::vector<int64_t> S;                                           // subtree roots
+  std::vector<char> top(nsup, 0);
+  std::vector<int32_t> sub_owner(nsup, -1);
+  static const bool binpack = std::getenv("SMLU_PARTITION") && std::string(std::getenv("SMLU_PARTITION")) == "binpack";
+  if (!binpack) {
+    std::vector<int32_t> lo(nsup, -1), hi(nsup, -1);   // rank range of each top front
+    struct Job { std::vector<int64_t> sub; int r0, r1; };
+    std::vector<Job> stack;
+    {
+      Job j{{}, 0, nparts};
+      for (int64_t s = 0; s < nsup; ++s)
+        if (s_parent[s] < 0) j.sub.push_back(s);
+      stack.push_back(std::move(j));
+    }
+    while (!stack.empty()) {
+      Job j = std::move(stack.back());
+      stack.pop_back();
+      if (j.sub.empty()) continue;
+      if (j.r1 - j.r0 == 1) {
+        for (auto v : j.sub) sub_owner[v] = j.r0;
+        continue;
+      }
+      if (j.sub.size() == 1) {
+        const int64_t v = j.sub[0];
+        if (ch_ptr[v] == ch_ptr[v + 1]) {   // a leaf front cannot be split further
+          sub_owner[v] = j.r0;
+          continue;
+        }
+        top[v] = 1;
+        lo[v] = j.r0;
+        hi[v] = j.r1;
+        Job c{{}, j.r0, j.r1};
+        for (int64_t e = ch_ptr[v]; e < ch_ptr[v + 1]; ++e) c.sub.push_back(ch_list[e]);
+        stack.push_back(std::move(c));
+        continue;
+      }
+      std::sort(j.sub.begin(), j.sub.end(), [&](int64_t a, int64_t b) { return W[a] != W[b] ? W[a] > W[b] : a < b; });
+      Job A{{}, 0, 0}, B{{}, 0, 0};
+      double wa = 0, wb = 0;
+      for (auto v : j.sub) {
+        if (wa <= wb) { A.sub.push_back(v); wa += W[v]; }
+        else { B.sub.push_back(v); wb += W[v]; }
+      }
+      const int k = j.r1 - j.r0;
+      int ka = (int)std::lround(k * wa / std::max(wa + wb, 1e-300));
+      ka = std::min(std::max(ka, 1), k - 1);
+      if (B.sub.empty()) ka = k;
+      A.r0 = j.r0; A.r1 = j.r0 + ka;
+      B.r0 = j.r0 + ka; B.r1 = j.r1;
+      stack.push_back(std::move(A));
+      if (!B.sub.empty()) stack.push_back(std::move(B));
+    }
+    for (int64_t s = nsup - 1; s >= 0; --s) {   // parents before children
+      if (top[s]) continue;
+      if (sub_owner[s] >= 0) owner[s] = sub_owner[s];
+      else if (s_parent[s] >= 0) owner[s] = owner[s_parent[s]];
+    }
+    for (int64_t s = 0; s < nsup; ++s) {
+      if (!top[s]) {
+        group[s].assign(1, owner[s]);
+        continue;
+      }
+      group[s].clear();
+      for (int r = lo[s]; r < hi[s]; ++r) group[s].push_back(r);
+      owner[s] = -1;
+    }
+    return;
+  }
+  // bin-packing (rounds 1-3, kept for comparison): split the heaviest subtree into its children
+  // until every subtree fits the per-rank share, bin-pack the subtrees (largest first, least-loaded
+  // rank); a top front's group is the union of its children's groups
+  std::vector<int64_t> S;
   for (int64_t s = 0; s < nsup; ++s)
     if (s_parent[s] < 0) S.push_back(s);
-  std::vector<char> top(nsup, 0);
   auto heaviest = [&]() {
     size_t bi = 0;
     for (size_t i = 1; i < S.size(); ++i)
       if (W[S[i]] > W[S[bi]]) bi = i;
     return bi;
   };
-  // split the heaviest subtree into its children until every subtree fits the per-rank share
   for (int it = 0; it < 64 * nparts && !S.empty(); ++it) {
     double sub = 0;
     for (auto v : S) sub += W[v];
     const size_t bi = heaviest();
     const int64_t v = S[bi];
     if ((int)S.size() >= nparts && W[v] <= 1.05 * sub / nparts) break;
-    if (ch_ptr[v] == ch_ptr[v + 1]) break;   // a leaf cannot be split further
+    if (ch_ptr[v] == ch_ptr[v + 1]) break;
     top[v] = 1;
     S.erase(S.begin() + (long)bi);
     for (int64_t e = ch_ptr[v]; e < ch_ptr[v + 1]; ++e) S.push_back(ch_list[e]);
   }
-  // bin-pack the subtrees onto ranks (largest first, least-loaded rank)
   std::sort(S.begin(), S.end(), [&](int64_t a, int64_t b) { return W[a] != W[b] ? W[a] > W[b] : a < b; });
   std::vector<double> load(nparts, 0.0);
-  std::vector<int32_t> sub_owner(nsup, -1);
   for (auto v : S) {
     const int r = (int)(std::min_element(load.begin(), load.end()) - load.begin());
     load[r] += W[v];
     sub_owner[v] = r;
   }
-  // subtree fronts take their root's rank (parents before children: walk down from the top)
   for (int64_t s = nsup - 1; s >= 0; --s) {
     if (sub_owner[s] >= 0) owner[s] = sub_owner[s];
     else if (!top[s] && s_parent[s] >= 0) owner[s] = owner[s_parent[s]];
   }
-  // top fronts (children before parents): the union of the children's groups
   for (int64_t s = 0; s < nsup; ++s) {
     if (!top[s]) {
       group[s].assign(1, owner[s]);
@@ -889,6 +959,10 @@ double project_partition(const Plan& P, double tflops, double gbs, double lat_us
       }
       double tend = 0;
       for (int r : G) tend = std::max(tend, c[r] + pend[r]);
+      static const bool dbg = std::getenv("SMLU_PROJECT_DEBUG") != nullptr;
+      if (dbg)
+        std::fprintf(stderr, "shared front %lld level %d ns %lld M %lld group %zu: start %.4f end %.4f (flops %.3e)\n",
+                     (long long)s, l, (long long)P.ns(s), (long long)P.M(s), G.size(), t, tend, P.front_flops[s]);
       for (int r : G) clk[r] = tend;
     }
   return *std::max_element(clk.begin(), clk.end());

@@ -29,6 +29,8 @@ def _matrix(which):
         return sp.csc_matrix(mats.poisson3d(14))
     if which == "poisson_big":
         return sp.csc_matrix(mats.poisson3d(24))
+    if which == "poisson40":
+        return sp.csc_matrix(mats.poisson3d(40))
     return sp.csc_matrix(mats.random_dominant(3000, 0.003, seed=5))
 
 
@@ -85,7 +87,8 @@ def _worker(rank, world, port, which, ob, q, transport="auto", gpu_per_rank=Fals
 
 
 @pytest.mark.parametrize("world,which,ob", [(2, "poisson", 0), (4, "poisson", 0), (3, "random", 0),
-                                            (2, "poisson_big", 128), (4, "poisson_big", 64)])
+                                            (2, "poisson_big", 128), (4, "poisson_big", 64),
+                                            (8, "poisson40", 64)])
 def test_dist_factor_solve_matches_single_gpu(world, which, ob):
     import scipy.sparse as sp
     import smlu
@@ -95,7 +98,8 @@ def test_dist_factor_solve_matches_single_gpu(world, which, ob):
     ps = [ctx.Process(target=_worker, args=(r, world, port, which, ob, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = [q.get(timeout=240) for _ in ps]
+    # world 8: the rank count of the driver's 8-GPU scaling run (its partition and schedule)
+    res = [q.get(timeout=420) for _ in ps]
     for p in ps:
         p.join(timeout=120)
     errs = [r[4] for r in res if r[4]]
