@@ -31,13 +31,6 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def _fit_power(xs, ts):
-    """Least-squares fit of log t = log a + alpha log x; returns (a, alpha)."""
-    lx, lt = np.log(np.asarray(xs, float)), np.log(np.asarray(ts, float))
-    alpha, la = np.polyfit(lx, lt, 1)
-    return float(np.exp(la)), float(alpha)
-
-
 def cpu_threads():
     """Host threads for the CPU baseline: OMP_NUM_THREADS when set (the GPU box sets it to its CPU
     share, 16), else every core this process may run on."""
@@ -46,15 +39,18 @@ def cpu_threads():
     return max(1, min(aff, int(env))) if env and env.isdigit() else aff
 
 
-def cpu_baseline(N_head, flops_head, nnz_head, grid_hint, samples=(48, 64, 80)):
+def cpu_baseline(N_head, flops_head, nnz_head, grid_hint, samples=(64, 108), reps=(3, 1)):
     """CPU baseline on the GPU box's host, reported beside the GPU number:
 
     * value: the multifrontal CPU port (oracle/mf.c: the same assembly tree as the GPU plan,
       threshold partial pivoting inside every front, AVX2 register-blocked updates, OpenMP tasks
-      over the assembly tree and inside the large fronts) factoring ONE matrix on all host threads
-      (`cores`), timed on 3D Poisson 48^3 / 64^3 / 80^3 with the GPU's ordering; log(time) fitted
-      in log(dense flops of the plan) and extrapolated to the headline 128^3 (17x the 80^3 sample's
-      flops).  The reference's own path (UMFPACK through Julia) does not exist on the box.
+      over the assembly tree and inside the large fronts) refactoring ONE matrix on all host threads
+      (`cores`).  Each sample size is factored once untimed (heap growth, page faults), then timed
+      `reps` times (median).  The headline is the 108^3 refactor scaled by the flop ratio to 128^3
+      (2.8x: the CPU's rate still rises with size, so this is a conservative, i.e. fast, CPU
+      estimate); 64^3 gives the rate's size trend.  The reference's own path (UMFPACK through Julia)
+      does not exist on the box.  tools/cpu_c3.py times the full 128^3 refactor directly (a
+      profile, not the default bench: ~2 minutes).
     * single_core: the same port on one thread at 40^3 (the reference's UMFPACK runs single-threaded).
     * superlu: scipy's SuperLU (splu, MMD on A'+A, diag_pivot_thresh 0.1) at C2, a third-party anchor.
     * c1_chunked_solve: the reference's own dense-chunk solve (oracle.ChunkedSolve, a line-by-line
@@ -66,39 +62,43 @@ def cpu_baseline(N_head, flops_head, nnz_head, grid_hint, samples=(48, 64, 80)):
     from smlu import matrices as mats
     threads = cpu_threads()
 
-    def mf_time(N, th):
+    def mf_time(N, th, nrep=1):
         A = mats.poisson3d(N)
         A.sort_indices()
         P = smlu.Plan(A, grid=(N,) * 3 if grid_hint else None)
         first, parent, rowptr, rows, p0 = P.fronts()
         fr = dict(first=first, parent=parent, rowptr=rowptr, rows=rows, p0=p0)
         mf = O.MultifrontalOracle(A, P.q(), fr, None, threads=th)
-        st = mf.factor(A.data)   # first factorization untimed: page faults of the factor store and heap
-        t0 = time.perf_counter()
-        st = mf.factor(A.data)   # the timed refactor (same pattern, as lu!)
-        dt = time.perf_counter() - t0
+        st = mf.factor(A.data)   # untimed: heap growth and page faults of the first factorization
+        ts = []
+        for _ in range(nrep):
+            t0 = time.perf_counter()
+            st = mf.factor(A.data)   # the timed refactor (same pattern, as lu!)
+            ts.append(time.perf_counter() - t0)
         mf.close()
         assert st == 0
-        return {"N": N, "seconds": dt, "dense_flops": P.stat("dense_flops"), "upd": P.stat("upd"),
+        dt = float(np.median(ts))
+        return {"N": N, "seconds": dt, "timings": ts, "dense_flops": P.stat("dense_flops"), "upd": P.stat("upd"),
                 "nnzLU": P.stat("nnzLU"), "nnzLU_per_s": P.stat("nnzLU") / dt,
                 "gflops": P.stat("dense_flops") / dt / 1e9}
 
     rows = []
-    for N in samples:
-        rows.append(mf_time(N, threads))
-        log(f"cpu baseline {N}^3 on {threads} threads: {rows[-1]['seconds']:.2f} s, "
+    for N, k in zip(samples, reps):
+        rows.append(mf_time(N, threads, k))
+        log(f"cpu baseline {N}^3 on {threads} threads: {rows[-1]['timings']} s, "
             f"{rows[-1]['gflops']:.1f} GFLOP/s")
-    a, alpha = _fit_power([r["dense_flops"] for r in rows], [r["seconds"] for r in rows])
-    t_head = a * flops_head ** alpha
+    big = rows[-1]
+    ratio = flops_head / big["dense_flops"]
+    t_head = big["seconds"] * ratio
+    alpha = float(np.log(big["seconds"] / rows[0]["seconds"]) / np.log(big["dense_flops"] / rows[0]["dense_flops"]))
     res = {"value": nnz_head / t_head, "unit": "nnz(L+U)/s", "cores": threads, "kind": "port",
            "nproc": os.cpu_count(),
            "sample": (f"multifrontal CPU port (oracle/mf.c, same plan, partial pivoting, OpenMP on "
-                      f"{threads} threads, AVX2) on 3D Poisson {'/'.join(f'{N}^3' for N in samples)}; "
-                      f"time fitted as {a:.3g} * flops^{alpha:.3f} and extrapolated to {N_head}^3 "
-                      f"({flops_head / rows[-1]['dense_flops']:.1f}x the largest sample's flops): "
-                      f"{t_head:.1f} s per refactor"),
-           "extrapolated": True, "extrapolation_factor": flops_head / rows[-1]["dense_flops"],
-           "headline_seconds": t_head, "fit": {"a": a, "alpha": alpha}, "samples": rows}
+                      f"{threads} threads, AVX2): 3D Poisson {big['N']}^3 refactor "
+                      f"{big['seconds']:.1f} s ({big['gflops']:.0f} GFLOP/s), scaled by the flop ratio "
+                      f"{ratio:.2f}x to {N_head}^3: {t_head:.1f} s per refactor"),
+           "extrapolated": True, "extrapolation_factor": ratio, "headline_seconds": t_head,
+           "time_vs_flops_exponent_64_to_largest": alpha, "samples": rows}
     one = mf_time(40, 1)
     res["single_core"] = dict(one, cores=1)
     log(f"cpu baseline 40^3 on 1 thread: {one['seconds']:.2f} s")

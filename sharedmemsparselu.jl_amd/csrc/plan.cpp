@@ -689,6 +689,12 @@ void Plan::compute_owners(int np, int64_t block) {
         for (auto v : j.sub) sub_owner[v] = j.r0;
         continue;
       }
+      static const bool dbg = std::getenv("SMLU_PROJECT_DEBUG") != nullptr;
+      if (dbg && j.r1 - j.r0 >= 2) {
+        std::fprintf(stderr, "map ranks [%d,%d):", j.r0, j.r1);
+        for (auto v : j.sub) std::fprintf(stderr, " %lld(W %.3e ns %lld)", (long long)v, W[v], (long long)ns(v));
+        std::fprintf(stderr, "\n");
+      }
       if (j.sub.size() == 1) {
         const int64_t v = j.sub[0];
         if (ch_ptr[v] == ch_ptr[v + 1]) {   // a leaf front cannot be split further
