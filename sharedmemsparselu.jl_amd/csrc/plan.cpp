@@ -649,11 +649,10 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
 }
 
 // ---------------------------------------------------------------------------------------
-// Multi-GPU partition of the assembly tree: proportional mapping by recursive bisection.  A set of
-// subtrees is mapped onto a contiguous rank range [r0, r1): one rank takes them all; a single
-// subtree on several ranks makes its root a shared ("top") front of the whole range and maps its
-// children onto the same range; several subtrees are split into two sets of balanced work (largest
-// first, onto the lighter set) and the range is cut in proportion to the two sets' work.  Sibling
+// Multi-GPU partition of the assembly tree: proportional mapping.  A set of subtrees is mapped onto
+// a contiguous rank range [r0, r1): one rank takes them all; a single subtree on several ranks
+// makes its root a shared ("top") front of the whole range and maps its children onto the same
+// range; several subtrees are packed into bins whose rank counts follow their work (below).  Sibling
 // shared fronts therefore have DISJOINT rank groups and run concurrently, and every group is a
 // contiguous range (nested or disjoint: a rank belongs to at most one shared front per tree level).
 // (Rounds 1-3 bin-packed the subtrees onto ranks, which put one rank under several siblings and
@@ -709,21 +708,46 @@ void Plan::compute_owners(int np, int64_t block) {
         stack.push_back(std::move(c));
         continue;
       }
+      // several subtrees on k ranks: pack them into m bins (largest first onto the lightest bin),
+      // deal the k ranks to the bins by the largest-quotient rule (D'Hondt: each next rank to the
+      // bin of largest work per rank), and keep the m (2 <= m <= k) of smallest makespan
+      // max(bin work / bin ranks); every bin becomes a job on its own contiguous rank range
       std::sort(j.sub.begin(), j.sub.end(), [&](int64_t a, int64_t b) { return W[a] != W[b] ? W[a] > W[b] : a < b; });
-      Job A{{}, 0, 0}, B{{}, 0, 0};
-      double wa = 0, wb = 0;
-      for (auto v : j.sub) {
-        if (wa <= wb) { A.sub.push_back(v); wa += W[v]; }
-        else { B.sub.push_back(v); wb += W[v]; }
-      }
       const int k = j.r1 - j.r0;
-      int ka = (int)std::lround(k * wa / std::max(wa + wb, 1e-300));
-      ka = std::min(std::max(ka, 1), k - 1);
-      if (B.sub.empty()) ka = k;
-      A.r0 = j.r0; A.r1 = j.r0 + ka;
-      B.r0 = j.r0 + ka; B.r1 = j.r1;
-      stack.push_back(std::move(A));
-      if (!B.sub.empty()) stack.push_back(std::move(B));
+      const int mmax = (int)std::min<size_t>(j.sub.size(), (size_t)k);
+      double best = -1;
+      std::vector<int> best_bin, best_r;
+      for (int m = 2; m <= mmax; ++m) {
+        std::vector<double> bw(m, 0.0);
+        std::vector<int> bin(j.sub.size());
+        for (size_t i = 0; i < j.sub.size(); ++i) {
+          const int b = (int)(std::min_element(bw.begin(), bw.end()) - bw.begin());
+          bin[i] = b;
+          bw[b] += W[j.sub[i]];
+        }
+        std::vector<int> r(m, 1);
+        for (int extra = k - m; extra > 0; --extra) {
+          int bi = 0;
+          for (int b = 1; b < m; ++b)
+            if (bw[b] / r[b] > bw[bi] / r[bi]) bi = b;
+          ++r[bi];
+        }
+        double mk = 0;
+        for (int b = 0; b < m; ++b) mk = std::max(mk, bw[b] / r[b]);
+        if (best < 0 || mk < best * (1 - 1e-12)) {
+          best = mk;
+          best_bin = bin;
+          best_r = r;
+        }
+      }
+      int r0 = j.r0;
+      for (size_t b = 0; b < best_r.size(); ++b) {
+        Job c{{}, r0, r0 + best_r[b]};
+        for (size_t i = 0; i < j.sub.size(); ++i)
+          if (best_bin[i] == (int)b) c.sub.push_back(j.sub[i]);
+        r0 += best_r[b];
+        stack.push_back(std::move(c));
+      }
     }
     for (int64_t s = nsup - 1; s >= 0; --s) {   // parents before children
       if (top[s]) continue;

@@ -67,3 +67,19 @@ def factor_parity(A, F, rtol=1e-12, prev_pivmode=0, full_piv_ns=None):
     E = L @ U - B
     assert abs(E).max() <= 1e-10 * max(abs(B).max(), 1.0)
     return ref
+
+
+def tile_pivoting_matrix(n, seed):
+    """Dense matrix whose 64x64 diagonal blocks dominate their rows but whose diagonal entries are
+    tiny (below 0.001 x the tile's column maxima, so rows are exchanged under UMFPACK's symmetric
+    diagonal tolerance as well): the diagonal-tile panel (mode 2, ns > 512) must exchange rows
+    inside every tile."""
+    rng = np.random.default_rng(seed)
+    D = rng.random((n, n))
+    for b0 in range(0, n, 64):
+        b1 = min(n, b0 + 64)
+        blk = rng.random((b1 - b0, b1 - b0)) * n
+        np.fill_diagonal(blk, 1e-3)
+        D[b0:b1, b0:b1] += blk
+    np.fill_diagonal(D, 1e-3 * rng.random(n))
+    return D

@@ -24,7 +24,7 @@ import scipy.sparse.linalg as spla
 import smlu
 from smlu import matrices as mats
 
-from _parity import DENSE_TOL, TOL, factor_parity, isapprox
+from _parity import DENSE_TOL, TOL, factor_parity, isapprox, tile_pivoting_matrix
 
 pytestmark = pytest.mark.gpu
 
@@ -113,14 +113,7 @@ def _dominant_dense(n, seed):
 
 
 def _tile_pivoting_matrix(n, seed):
-    rng = np.random.default_rng(seed)
-    D = rng.random((n, n))
-    for b0 in range(0, n, 64):
-        b1 = min(n, b0 + 64)
-        blk = rng.random((b1 - b0, b1 - b0)) * n
-        np.fill_diagonal(blk, 1e-3)
-        D[b0:b1, b0:b1] += blk
-    return D
+    return tile_pivoting_matrix(n, seed)
 
 
 @pytest.mark.parametrize("variant", ["mfma128", "valu64"])

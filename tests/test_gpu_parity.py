@@ -12,7 +12,7 @@ from smlu import matrices as mats
 
 pytestmark = pytest.mark.gpu
 
-from _parity import DENSE_TOL, TOL, assert_same_pattern, factor_parity, isapprox  # noqa: F401
+from _parity import DENSE_TOL, TOL, assert_same_pattern, factor_parity, isapprox, tile_pivoting_matrix  # noqa: F401
 
 
 @pytest.mark.parametrize("N", [4, 10, 23])
@@ -123,19 +123,7 @@ def test_blocked_tile_mode_dominant(gpu):
 
 
 def _tile_pivoting_matrix(n, seed):
-    """Dense matrix whose 64x64 diagonal blocks dominate their rows but whose diagonal entries are
-    tiny, so the diagonal-tile panel (mode 2, ns > 512) must exchange rows inside every tile."""
-    rng = np.random.default_rng(seed)
-    D = rng.random((n, n))
-    for b0 in range(0, n, 64):
-        b1 = min(n, b0 + 64)
-        blk = rng.random((b1 - b0, b1 - b0)) * n
-        np.fill_diagonal(blk, 1e-3)
-        D[b0:b1, b0:b1] += blk
-    # diagonal entries below 0.001 x the tile's column maxima: exchanges under UMFPACK's symmetric
-    # diagonal tolerance (0.001, the default) as well
-    np.fill_diagonal(D, 1e-3 * rng.random(n))
-    return D
+    return tile_pivoting_matrix(n, seed)
 
 
 @pytest.mark.parametrize("n", [700, 1100])
