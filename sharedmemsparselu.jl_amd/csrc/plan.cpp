@@ -9,6 +9,7 @@
 //    (Rs.*A)[p,q] and nothing else.
 #include <algorithm>
 #include <cstdlib>
+#include <functional>
 #include <map>
 #include <chrono>
 #include <cmath>
@@ -672,6 +673,63 @@ void Plan::compute_owners(int np, int64_t block) {
   static const bool binpack = std::getenv("SMLU_PARTITION") && std::string(std::getenv("SMLU_PARTITION")) == "binpack";
   if (!binpack) {
     std::vector<int32_t> lo(nsup, -1), hi(nsup, -1);   // rank range of each top front
+    // Cost model of a subtree set on k ranks (flop units): one rank does all of it; a single
+    // subtree shares its root front over the k ranks (front flops / k) and maps its children on
+    // the same k ranks; several subtrees take the best bin split.  A split deals the ranks one at
+    // a time to the bin of largest cost at its current count (a bin whose subtrees cannot use
+    // more ranks -- one leaf -- stops gaining), so it sees that a heavy subtree left on one rank
+    // bounds the makespan, which plain work-proportional shares do not.
+    std::map<std::pair<int64_t, int>, double> memo;
+    std::function<double(const std::vector<int64_t>&, int)> cost;
+    std::function<double(const std::vector<int64_t>&, int, std::vector<int>*, std::vector<int>*)> split;
+    cost = [&](const std::vector<int64_t>& S, int k) -> double {
+      double w = 0;
+      for (auto v : S) w += W[v];
+      if (k <= 1 || S.empty()) return w;
+      if (S.size() == 1) {
+        const int64_t v = S[0];
+        if (ch_ptr[v] == ch_ptr[v + 1]) return w;
+        auto key = std::make_pair(v, k);
+        auto it = memo.find(key);
+        if (it != memo.end()) return it->second;
+        std::vector<int64_t> ch(ch_list.begin() + ch_ptr[v], ch_list.begin() + ch_ptr[v + 1]);
+        std::sort(ch.begin(), ch.end(), [&](int64_t a, int64_t b) { return W[a] != W[b] ? W[a] > W[b] : a < b; });
+        const double c = front_flops[v] / k + cost(ch, k);
+        memo[key] = c;
+        return c;
+      }
+      return split(S, k, nullptr, nullptr);
+    };
+    split = [&](const std::vector<int64_t>& S, int k, std::vector<int>* obin, std::vector<int>* orank) -> double {
+      const int mmax = (int)std::min<size_t>(S.size(), (size_t)k);
+      double best = -1;
+      for (int m = 2; m <= mmax; ++m) {
+        std::vector<double> bw(m, 0.0);
+        std::vector<int> bin(S.size());
+        std::vector<std::vector<int64_t>> sets(m);
+        for (size_t i = 0; i < S.size(); ++i) {
+          const int b = (int)(std::min_element(bw.begin(), bw.end()) - bw.begin());
+          bin[i] = b;
+          bw[b] += W[S[i]];
+          sets[b].push_back(S[i]);
+        }
+        std::vector<int> r(m, 1);
+        std::vector<double> c(m);
+        for (int b = 0; b < m; ++b) c[b] = cost(sets[b], 1);
+        for (int extra = k - m; extra > 0; --extra) {
+          const int bi = (int)(std::max_element(c.begin(), c.end()) - c.begin());
+          ++r[bi];
+          c[bi] = cost(sets[bi], r[bi]);
+        }
+        const double mk = *std::max_element(c.begin(), c.end());
+        if (best < 0 || mk < best * (1 - 1e-12)) {
+          best = mk;
+          if (obin) *obin = bin;
+          if (orank) *orank = r;
+        }
+      }
+      return best;
+    };
     struct Job { std::vector<int64_t> sub; int r0, r1; };
     std::vector<Job> stack;
     {
@@ -708,44 +766,17 @@ void Plan::compute_owners(int np, int64_t block) {
         stack.push_back(std::move(c));
         continue;
       }
-      // several subtrees on k ranks: pack them into m bins (largest first onto the lightest bin),
-      // deal the k ranks to the bins by the largest-quotient rule (D'Hondt: each next rank to the
-      // bin of largest work per rank), and keep the m (2 <= m <= k) of smallest makespan
-      // max(bin work / bin ranks); every bin becomes a job on its own contiguous rank range
-      std::sort(j.sub.begin(), j.sub.end(), [&](int64_t a, int64_t b) { return W[a] != W[b] ? W[a] > W[b] : a < b; });
-      const int k = j.r1 - j.r0;
-      const int mmax = (int)std::min<size_t>(j.sub.size(), (size_t)k);
-      double best = -1;
-      std::vector<int> best_bin, best_r;
-      for (int m = 2; m <= mmax; ++m) {
-        std::vector<double> bw(m, 0.0);
-        std::vector<int> bin(j.sub.size());
-        for (size_t i = 0; i < j.sub.size(); ++i) {
-          const int b = (int)(std::min_element(bw.begin(), bw.end()) - bw.begin());
-          bin[i] = b;
-          bw[b] += W[j.sub[i]];
-        }
-        std::vector<int> r(m, 1);
-        for (int extra = k - m; extra > 0; --extra) {
-          int bi = 0;
-          for (int b = 1; b < m; ++b)
-            if (bw[b] / r[b] > bw[bi] / r[bi]) bi = b;
-          ++r[bi];
-        }
-        double mk = 0;
-        for (int b = 0; b < m; ++b) mk = std::max(mk, bw[b] / r[b]);
-        if (best < 0 || mk < best * (1 - 1e-12)) {
-          best = mk;
-          best_bin = bin;
-          best_r = r;
-        }
-      }
+      // several subtrees on k ranks: pack them into m bins (largest first onto the lightest bin) and
+      // deal the ranks to the bins by the cost model below; keep the m (2 <= m <= k) of smallest
+      // makespan.  Every bin becomes a job on its own contiguous rank range.
+      std::vector<int> bin, r;
+      split(j.sub, j.r1 - j.r0, &bin, &r);
       int r0 = j.r0;
-      for (size_t b = 0; b < best_r.size(); ++b) {
-        Job c{{}, r0, r0 + best_r[b]};
+      for (size_t b = 0; b < r.size(); ++b) {
+        Job c{{}, r0, r0 + r[b]};
         for (size_t i = 0; i < j.sub.size(); ++i)
-          if (best_bin[i] == (int)b) c.sub.push_back(j.sub[i]);
-        r0 += best_r[b];
+          if (bin[i] == (int)b) c.sub.push_back(j.sub[i]);
+        r0 += r[b];
         stack.push_back(std::move(c));
       }
     }
