@@ -59,11 +59,13 @@ hipError_t launch_fwd_pull(hipStream_t, int64_t, const FrontTile*, int, const SN
 hipError_t launch_fwd_gather(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                              const int32_t*, double*, double*, Rhs);
 hipError_t launch_tri_block(hipStream_t, bool, int64_t, const FrontTile*, int, int, const SNode*,
-                            const double*, double*, double*, Rhs);
+                            const double*, double*, double*, Rhs, DiagInv);
 hipError_t launch_bwd_u12(hipStream_t, int64_t, const FrontTile*, int, const SNode*, const int32_t*,
                           const double*, const double*, double*, Rhs);
+hipError_t launch_diag_inv(hipStream_t, bool, int64_t, const int32_t*, const int64_t*, const SNode*, const double*,
+                           double*);
 hipError_t launch_tri_sweep(hipStream_t, bool, int64_t, const FrontTile*, int, unsigned long long*, int32_t*, double*,
-                            int32_t*, const SNode*, const double*, double*, double*, Rhs, int);
+                            int32_t*, const SNode*, const double*, double*, double*, Rhs, int, DiagInv);
 hipError_t launch_fwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                       const int32_t*, const double*, double*, double*, Rhs);
 hipError_t launch_bwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*,
@@ -356,6 +358,10 @@ struct smlu_handle {
   DBuf<int2> aents;
   DBuf<FrontTile> ftiles;
   DBuf<int32_t> gptr, gent;       // pull lists of the large fronts' forward gather (k_fwd_pull)
+  DBuf<int64_t> invbase;          // large fronts' diagonal-block inverses (k_diag_inv): first block per front
+  DBuf<int32_t> invfront;         // ... front of each block
+  DBuf<double> dinvbuf;           // ... L and U inverses, 2 x 4096 doubles per block
+  int64_t ninv = 0;
   DBuf<int32_t> ssync, sstatus;   // sync-free solve sweeps: block flags (epochs, never reset); timeouts
   DBuf<unsigned long long> stick; // ... one monotone ticket counter per sweep launch
   DBuf<double> sxh;               // ... hand-off slots: 64 x kMultiRhs doubles per flag
@@ -461,6 +467,9 @@ struct smlu_handle {
     ftiles.free();
     gptr.free();
     gent.free();
+    invbase.free();
+    invfront.free();
+    dinvbuf.free();
     ssync.free();
     sstatus.free();
     stick.free();
@@ -641,6 +650,8 @@ static int build_schedule(smlu_handle* h) {
   std::vector<XContrib> xt;
   std::vector<FrontTile> ft;
   std::vector<int32_t> gptr, gent;   // k_fwd_pull lists
+  std::vector<int64_t> invbase;      // k_diag_inv: first block of each large front (-1: none)
+  std::vector<int32_t> invfront;
   std::vector<GemmTask> gt;
   std::vector<SwapTask> st_tasks;
   std::vector<URowTask> ur_tasks;
@@ -1773,6 +1784,11 @@ static int build_schedule(smlu_handle* h) {
       // gather: one thread per front row pulls its own value and the children's contributions (in
       // child order) -- k_fwd_pull; pull lists per front row: gptr (CSR, relative to the front's
       // block) -> gent (vbuf index of each contribution)
+      if (invbase.empty()) invbase.assign((size_t)h->nnodes, -1);
+      for (auto s : bigs) {   // diagonal-block inverses for the solves of this front
+        invbase[s] = (int64_t)invfront.size();
+        for (int64_t b = 0; b < ((int64_t)h->hsn[s].ns + 63) / 64; ++b) invfront.push_back((int32_t)s);
+      }
       Launch L;
       L.kind = K_FWDP;
       L.off = (int64_t)ft.size();
@@ -2175,6 +2191,13 @@ static int build_schedule(smlu_handle* h) {
     expand_all(h->bwd, h->bwd_seg, true, h->bwdm, h->bwdm_seg);
   }
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
+  h->ninv = (int64_t)invfront.size();
+  if (h->ninv > 0 && !std::getenv("SMLU_NO_DIAG_INV")) {   // dev knob: substitution on the diagonal blocks
+    // (finish_factor launches k_diag_inv after every factorization: inverses of the current factors)
+    HIPCHK(h->invbase.upload(invbase.data(), invbase.size(), st));
+    HIPCHK(h->invfront.upload(invfront.data(), invfront.size(), st));
+    HIPCHK(h->dinvbuf.alloc((size_t)h->ninv * 2 * 4096));
+  }
   if (!gptr.empty()) {
     HIPCHK(h->gptr.upload(gptr.data(), gptr.size(), st));
     HIPCHK(h->gent.upload(gent.data(), gent.size(), st));
@@ -2545,6 +2568,10 @@ static int factor_segment(smlu_handle* h, Timer& tm, int seg) {
 static int finish_factor(smlu_handle* h, Timer& tm, std::chrono::steady_clock::time_point t0) {
   Plan& P = h->plan;
   hipStream_t st = h->stream;
+  if (h->dinvbuf.p) {   // the large fronts' diagonal-block inverses of the new factors, for the solves
+    HIPCHK(launch_diag_inv(st, false, h->ninv, h->invfront.p, h->invbase.p, h->sn.p, h->store.p, h->dinvbuf.p));
+    HIPCHK(launch_diag_inv(st, true, h->ninv, h->invfront.p, h->invbase.p, h->sn.p, h->store.p, h->dinvbuf.p));
+  }
   HIPCHK(hipMemcpyAsync(h->hinfo, h->info.p, sizeof(int32_t) * h->nnodes, hipMemcpyDeviceToHost, st));
   double g = 0;
   HIPCHK(hipMemcpyAsync(&g, h->growth.p, sizeof(double), hipMemcpyDeviceToHost, st));
@@ -2659,6 +2686,9 @@ static void release_schedule(smlu_handle* h) {
   h->ftiles.free();
   h->gptr.free();
   h->gent.free();
+  h->invbase.free();
+  h->invfront.free();
+  h->dinvbuf.free();
   h->ssync.free();
   h->stick.free();
   h->sxh.free();
@@ -2736,10 +2766,10 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, d
                                h->rowperm.p, w, v, rh);
     case K_TRIF:
       return launch_tri_block(st, false, L.nwg, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p,
-                              h->store.p, w, v, rh);
+                              h->store.p, w, v, rh, DiagInv{h->invbase.p, h->dinvbuf.p});
     case K_TRIB:
       return launch_tri_block(st, true, L.nwg, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p,
-                              h->store.p, w, v, rh);
+                              h->store.p, w, v, rh, DiagInv{h->invbase.p, h->dinvbuf.p});
     case K_BWDU:
       return launch_bwd_u12(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->sn.p, h->rows.p, h->store.p, w, v,
                             rh);
@@ -2747,7 +2777,7 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, d
     case K_SWEEPB:
       return launch_tri_sweep(st, L.kind == K_SWEEPB, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->stick.p + L.aux2,
                               h->ssync.p + L.aux, h->sxh.p + L.aux * 64 * kMultiRhs, h->sstatus.p, h->sn.p, h->store.p,
-                              w, v, rh, h->sweep_spin);
+                              w, v, rh, h->sweep_spin, DiagInv{h->invbase.p, h->dinvbuf.p});
     case K_BWDU12C:
       return launch_bwd_u12_cols(st, h->sn.p, L.node, h->hsn[L.node].ns, L.aux, L.aux2, (int)L.cnt, h->rows.p,
                                  h->store.p, w, h->vbuf.p);
@@ -2780,25 +2810,31 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
     v = h->vbufm.p;
     rh.n = nrhs;
   }
-  const bool batch = rh.n > 1 && h->nranks == 1;
+  // batches of up to 8 right-hand sides run the sweeps (NR-wide hand-off slots), wider ones the
+  // per-block launches (fwdm / bwdm)
+  const bool steps = rh.n > 8 && h->nranks == 1;
   // The sync-free sweeps' waits are bounded: a wait that gives up raises sstatus, which is read back
   // after every solve that ran them; the solve is then re-run on the per-block schedule (fwdm / bwdm,
   // bitwise the same arithmetic), so a timed-out sweep never returns a wrong x.  Partitioned handles
   // agree on the re-run (allreduce of the flag: the per-block sequences hold the same comm steps).
-  const bool check = !batch && (h->ssync_n > 0 || h->nranks > 1);
+  const bool check = !steps && (h->ssync_n > 0 || h->nranks > 1);
   const double* src = mode == 0 ? db : dx;
-  auto load_input = [&](const double* in) -> hipError_t {
-    if (mode == 0) return launch_perm_in(st, P.n, h->p0.p, h->Rs.p, in, w, nrhs, ldb > 0 ? ldb : P.n, rh.ldx);
+  const int64_t lds = mode == 0 && ldb > 0 ? ldb : P.n;
+  auto load_input = [&](const double* in, int64_t ld) -> hipError_t {
+    if (mode == 0) return launch_perm_in(st, P.n, h->p0.p, h->Rs.p, in, w, nrhs, ld, rh.ldx);
     if (mode == 1) return launch_unswap(st, P.n, h->posfirst.p, h->rowperm.p, in, w);
     return hipMemcpyAsync(w, in, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st);
   };
   const double* rerun_src = src;
+  int64_t rerun_ld = lds;
   if (check && (mode != 0 || db == dx)) {   // the final step overwrites the input: keep a copy for a re-run
-    if (!h->bstash.p) HIPCHK(h->bstash.alloc((size_t)P.n));
-    HIPCHK(hipMemcpyAsync(h->bstash.p, src, sizeof(double) * P.n, hipMemcpyDeviceToDevice, st));
+    if (!h->bstash.p) HIPCHK(h->bstash.alloc((size_t)P.n * kMultiRhs));
+    HIPCHK(hipMemcpy2DAsync(h->bstash.p, sizeof(double) * P.n, src, sizeof(double) * lds, sizeof(double) * P.n,
+                            (size_t)nrhs, hipMemcpyDeviceToDevice, st));
     rerun_src = h->bstash.p;
+    rerun_ld = P.n;
   }
-  HIPCHK(load_input(src));
+  HIPCHK(load_input(src, lds));
   // launches between communication steps (one GPU: a single segment each)
   auto run_seq = [&](const std::vector<Launch>& seq, const std::vector<size_t>& seg, const std::vector<int>& cm) {
     for (size_t k = 0; k < seg.size(); ++k) {
@@ -2838,7 +2874,7 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
     if (!ex) {
       hipGraph_t g = nullptr;
       HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
-      int rc = sweeps(batch);
+      int rc = sweeps(steps);
       hipError_t ec = hipStreamEndCapture(st, &g);
       if (rc == SMLU_OK && ec == hipSuccess && g) ec = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
       if (g) (void)hipGraphDestroy(g);
@@ -2852,11 +2888,11 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
     }
     if (ex) HIPCHK(hipGraphLaunch(ex, st));
     else {
-      int rc = sweeps(batch);
+      int rc = sweeps(steps);
       if (rc != SMLU_OK) return rc;
     }
   } else {
-    int rc = sweeps(batch);
+    int rc = sweeps(steps);
     if (rc != SMLU_OK) return rc;
   }
   if (check) HIPCHK(hipMemcpyAsync(h->hsstat, h->sstatus.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
@@ -2872,7 +2908,7 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
       ++h->sweep_timeouts;
       *h->hsstat = 0;
       HIPCHK(hipMemsetAsync(h->sstatus.p, 0, sizeof(int32_t), st));
-      HIPCHK(load_input(rerun_src));
+      HIPCHK(load_input(rerun_src, rerun_ld));
       int rc = sweeps(true);
       if (rc != SMLU_OK) return rc;
       HIPCHK(finish());
