@@ -702,7 +702,19 @@ void Plan::compute_owners(int np, int64_t block) {
     };
     split = [&](const std::vector<int64_t>& S, int k, std::vector<int>* obin, std::vector<int>* orank) -> double {
       const int mmax = (int)std::min<size_t>(S.size(), (size_t)k);
-      double best = -1;
+      // m = 1: the heaviest subtree (S is sorted) on all k ranks, the light rest packed whole onto the
+      // range's first rank (bin -1), which also works on the heavy one: no rank is taken from it
+      double best;
+      {
+        double rest = 0;
+        for (size_t i = 1; i < S.size(); ++i) rest += W[S[i]];
+        best = cost(std::vector<int64_t>{S[0]}, k) + rest;
+        if (obin) {
+          obin->assign(S.size(), -1);
+          (*obin)[0] = 0;
+        }
+        if (orank) orank->assign(1, k);
+      }
       for (int m = 2; m <= mmax; ++m) {
         std::vector<double> bw(m, 0.0);
         std::vector<int> bin(S.size());
@@ -771,6 +783,8 @@ void Plan::compute_owners(int np, int64_t block) {
       // makespan.  Every bin becomes a job on its own contiguous rank range.
       std::vector<int> bin, r;
       split(j.sub, j.r1 - j.r0, &bin, &r);
+      for (size_t i = 0; i < j.sub.size(); ++i)
+        if (bin[i] < 0) sub_owner[j.sub[i]] = j.r0;   // light subtrees packed onto the first rank
       int r0 = j.r0;
       for (size_t b = 0; b < r.size(); ++b) {
         Job c{{}, r0, r0 + r[b]};

@@ -103,10 +103,10 @@ def test_proportional_mapping_groups(nparts, case):
         ch = kids.get(int(s), [])
         for i in range(len(ch)):
             for j in range(i + 1, len(ch)):
-                # siblings share a rank only when both are packed whole onto it
+                # siblings share a rank only when one of them is packed whole onto it
                 if R[ch[i]] & R[ch[j]]:
-                    assert len(R[ch[i]]) == 1 and len(R[ch[j]]) == 1, (s, ch[i], ch[j])
-    for lv in np.unique(level):
+                    assert min(len(R[ch[i]]), len(R[ch[j]])) == 1, (s, ch[i], ch[j])
+    for lv in np.unique(level):   # shared fronts of one tree level never share a rank
         seen = set()
         for s in np.flatnonzero((owner == -1) & (level == lv)):
             assert not (seen & R[s]), lv
