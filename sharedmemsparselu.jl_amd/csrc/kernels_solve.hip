@@ -869,11 +869,16 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
         }
       }
       sweep_mark(UPPER, item, wv, 3);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
-    if (tid == 0) (void)__hip_atomic_fetch_max(flags + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tid == 0) sweep_mark(UPPER, item, t, 4);
+    __syncthreads();   // xs (LDS) visible to the waves that apply block b
+    if (wv == t) {
+      // publish: raise the flag once this wave's slot writes have completed (vmcnt counts every
+      // lane's atomics of the wave); the other waves apply the block meanwhile, so the write
+      // round trip is off the chunk's own chain
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) (void)__hip_atomic_fetch_max(flags + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) sweep_mark(UPPER, item, t, 4);
+    }
     if (applies) fma_tile(bw);
     __syncthreads();
   }

@@ -781,6 +781,7 @@ void Plan::compute_owners(int np, int64_t block) {
       // several subtrees on k ranks: pack them into m bins (largest first onto the lightest bin) and
       // deal the ranks to the bins by the cost model below; keep the m (2 <= m <= k) of smallest
       // makespan.  Every bin becomes a job on its own contiguous rank range.
+      std::sort(j.sub.begin(), j.sub.end(), [&](int64_t a, int64_t b) { return W[a] != W[b] ? W[a] > W[b] : a < b; });
       std::vector<int> bin, r;
       split(j.sub, j.r1 - j.r0, &bin, &r);
       for (size_t i = 0; i < j.sub.size(); ++i)
