@@ -736,14 +736,15 @@ __device__ __forceinline__ void panel_fused_tail(const double (&x)[CW], int pos,
   }
 }
 
-// Column-block variant of k_panel_cols (the default for 64-wide panels): wave w owns the
+// Column-block panel (the 64-wide panels; round 2's per-column-barrier variant k_panel_cols was
+// dropped in round 4): wave w owns the
 // CW = 64/NWV consecutive columns [w*CW, (w+1)*CW) in registers (lane = candidate row).  The
 // owner of a block factors its CW columns wave-locally -- pivot search, scaling, rank-1 updates
 // of its own later columns, no workgroup barrier -- and publishes the block's pivots and
 // multipliers through LDS (double-buffered); after ONE barrier every later wave applies the CW
 // rank-1 updates to its columns in column order, and every wave replays the transpositions.
 // One barrier per CW columns instead of one per column.  Same pivot choices and the same
-// element-wise FMAs in the same order as k_panel_cols (bitwise-identical panel).
+// element-wise FMAs in the same order as k_panel_wave (bitwise-identical panel).
 //
 // FUSED = true (GEMM-form fronts, nb = 64): the same panel, then in the same workgroup the two
 // tile inverses k_tri_inv computes (same per-column arithmetic: bitwise-identical NL/NU in the
@@ -905,140 +906,6 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
   }
 }
 
-// Column-split variant of k_panel_wave<64> (R <= 64 candidate rows, up to 64 columns): NWV waves,
-// lane = row as before, columns dealt round-robin (column c lives in wave c % NWV at register
-// c / NWV, so the column loop unrolls with static register indices).  Per column k the owning
-// wave does the pivot search and scaling exactly as k_panel_wave and publishes (pivot lane,
-// multipliers) through LDS; every wave then updates its own columns right of k.  Same pivot
-// choices and the same element-wise FMAs as k_panel_wave (bitwise-identical panel); each wave's
-// per-column chain is 64/NWV readlane+FMA pairs instead of 64.
-template <int NWV>
-__global__ __launch_bounds__(64 * NWV) void k_panel_cols(const int32_t* __restrict__ list, int step,
-                                                         const SNode* __restrict__ sn,
-                                                         double* __restrict__ store,
-                                                         double* __restrict__ scratch,
-                                                         int32_t* __restrict__ rowperm,
-                                                         int32_t* __restrict__ swaps,
-                                                         int64_t swap_stride,
-                                                         int32_t* __restrict__ info,
-                                                         double* __restrict__ growth, double diag_tol) {
-  constexpr int CW = 64 / NWV;
-  __shared__ double s_l[2][64];
-  __shared__ int s_p[2];
-  __shared__ int s_flag[NWV], s_err[NWV];
-  const int sid = list[2 * blockIdx.x];
-  const SNode s = sn[sid];
-  FrontPtrs f = front_ptrs(s, store, scratch);
-  const int64_t M = f.M;
-  const int ns = (int)f.ns;
-  const int kb = step * s.nb;
-  const int w = min(s.nb, ns - kb);
-  const int R = (s.mode == 1) ? ns - kb : w;
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool has = lane < R;
-  gdbl* P = f.L + (int64_t)kb * M + kb;
-  double x[CW];
-#pragma unroll
-  for (int j = 0; j < CW; ++j) {
-    const int c = j * NWV + wv;
-    x[j] = (has && c < w) ? P[(int64_t)c * M + lane] : 0.0;
-  }
-  int pos = lane, who = lane;   // replicated in every wave
-  int flag = 0, err = -1;
-  double lmax = 0.0;
-#pragma unroll
-  for (int k = 0; k < 64; ++k) {
-    if (k < w) {
-      const int buf = k & 1;
-      const int kk = k / NWV;   // register of column k in its owner wave
-      const int q = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(who, k));
-      if (wv == k % NWV) {   // owner of column k (wave-uniform)
-        const double cur = x[kk];
-        const bool cand = has && pos >= k;
-        const double akk = readlane_f64(cur, q);
-        const bool beats = cand && pos != k && fabs(cur) * diag_tol > fabs(akk);
-        int p = q;
-        if (__ballot(beats) != 0ull || akk == 0.0) {   // full argmax (rare under dominance)
-          double am = cand ? fabs(cur) : -1.0;
-          int ai = cand ? pos : 0x7fffffff;
-#pragma unroll
-          for (int o = 32; o > 0; o >>= 1) {
-            const double ov = __shfl_xor(am, o, 64);
-            const int oi = __shfl_xor(ai, o, 64);
-            if (ov > am || (ov == am && oi < ai)) { am = ov; ai = oi; }
-          }
-          if (am <= 0.0) {
-            flag |= 1;
-            if (err < 0) err = kb + k;
-          } else {
-            p = __builtin_amdgcn_readlane(who, __builtin_amdgcn_readfirstlane(ai));
-          }
-          p = __builtin_amdgcn_readfirstlane(p);
-        }
-        const double pinv = recip(readlane_f64(cur, p));
-        double l = 0.0;
-        if (cand && lane != p) {
-          l = cur * pinv;
-          lmax = fmax(lmax, fabs(l));
-          x[kk] = l;
-        }
-        s_l[buf][lane] = l;
-        if (lane == 0) s_p[buf] = p;
-      }
-      __syncthreads();
-      const int p = __builtin_amdgcn_readfirstlane(s_p[buf]);
-      const double l = s_l[buf][lane];
-      if (l != 0.0) {
-#pragma unroll
-        for (int j = 0; j < CW; ++j)
-          if (j * NWV + NWV - 1 > k && j * NWV + wv > k) x[j] = fma(-l, readlane_f64(x[j], p), x[j]);
-      }
-      if (p != q) {               // transposition of positions k and ppos
-        const int ppos = __builtin_amdgcn_readlane(pos, p);
-        if (lane == p) pos = k;
-        else if (lane == q) pos = ppos;
-        if (lane == k) who = p;
-        else if (lane == ppos) who = q;
-      }
-    }
-  }
-  if (has) {
-#pragma unroll
-    for (int j = 0; j < CW; ++j) {
-      const int c = j * NWV + wv;
-      if (c < w) P[(int64_t)c * M + pos] = x[j];
-    }
-  }
-  lmax = wave_max(lmax);
-  if (lane == 0) {
-    if (lmax > 0.0) atomic_max_pos(&growth[0], lmax);
-    s_flag[wv] = flag;
-    s_err[wv] = err;
-  }
-  __syncthreads();
-  if (wv != 0) return;
-  int32_t* rp = rowperm + s.first + kb;
-  const int old = has ? rp[lane] : 0;
-  if (has) rp[pos] = old;
-  int32_t* sw = swaps + (int64_t)list[2 * blockIdx.x + 1] * swap_stride;
-  const bool mv = has && pos != lane;
-  const unsigned long long m = __ballot(mv);
-  if (mv) {
-    const int o = __popcll(m & ((1ull << lane) - 1ull));
-    sw[1 + 2 * o] = pos;
-    sw[2 + 2 * o] = lane;
-  }
-  if (lane == 0) {
-    sw[0] = __popcll(m);
-    int fl = 0, er = -1;
-    for (int v = 0; v < NWV; ++v) {   // first failing column over all waves
-      fl |= s_flag[v];
-      if (s_err[v] >= 0 && (er < 0 || s_err[v] < er)) er = s_err[v];
-    }
-    if (fl) publish_info(info + sid, fl, er);
-  }
-}
 
 // Row swaps (LAPACK laswp) of the panels of a SwapTask on its column set; one workgroup per 64
 // columns.  Within a workgroup the panels' swap lists are applied in order.  A list moves at
@@ -1473,32 +1340,15 @@ hipError_t launch_panel1(hipStream_t st, int cnt, int lds_doubles, int rmax, int
   size_t lds = (size_t)lds_doubles * sizeof(double);
 #define PANEL1_ARGS list, step, sn, store, scratch, rowperm, swaps, swap_stride, info, growth, diag_tol
   (void)lds;
-  static const bool lds_panel = std::getenv("SMLU_LDS_PANEL") != nullptr;
-  // 64-wide panels: column-split kernel (16 waves by default -- 16/8/4 waves: 27/30/35 ms per
-  // 128^3 refactor; SMLU_PANEL_COLS=8 or 4 selects those); SMLU_PANEL_COLS=1: single-wave kernel
-  static const int cols_waves = [] {
-    const char* e = std::getenv("SMLU_PANEL_COLS");
-    return e ? std::atoi(e) : 16;
-  }();
-  // column-block panel (one barrier per 64/NWV columns) unless SMLU_PANEL_BLK=0
-  static const int blk_waves = [] {
-    const char* e = std::getenv("SMLU_PANEL_BLK");
-    return e ? std::atoi(e) : 16;
-  }();
   if (fused) {   // GEMM-form fronts: panel + in-block row interchanges (+ tile inverses if fused == 2)
     if (wmax <= 32 || ob > 64 + 16 * 20 || (fused == 2 && !tinv)) return hipErrorInvalidValue;
     if (fused == 2) k_panel_blk<16, 2><<<cnt, 1024, 0, st>>>(PANEL1_ARGS, tinv, ob);
     else k_panel_blk<16, 1><<<cnt, 1024, 0, st>>>(PANEL1_ARGS, tinv, ob);
   }
-  else if (wmax > 32 && !lds_panel && blk_waves == 16) k_panel_blk<16, 0><<<cnt, 1024, 0, st>>>(PANEL1_ARGS, nullptr, 0);
-  else if (wmax > 32 && !lds_panel && blk_waves == 8) k_panel_blk<8, 0><<<cnt, 512, 0, st>>>(PANEL1_ARGS, nullptr, 0);
-  else if (wmax > 32 && !lds_panel && cols_waves == 16) k_panel_cols<16><<<cnt, 1024, 0, st>>>(PANEL1_ARGS);
-  else if (wmax > 32 && !lds_panel && cols_waves == 8) k_panel_cols<8><<<cnt, 512, 0, st>>>(PANEL1_ARGS);
-  else if (wmax > 32 && !lds_panel && cols_waves == 4) k_panel_cols<4><<<cnt, 256, 0, st>>>(PANEL1_ARGS);
-  else if (wmax > 32 && !lds_panel) k_panel_wave<64><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
-  else if (wmax > 32) k_panel_reg<64, 1><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
-  else if (rmax <= 64 && !lds_panel) k_panel_wave<32><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
-  else if (rmax <= 64) k_panel_reg<32, 1><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
+  // 64-wide panels: the column-block kernel (16 waves, one barrier per 4 columns)
+  else if (wmax > 32) k_panel_blk<16, 0><<<cnt, 1024, 0, st>>>(PANEL1_ARGS, nullptr, 0);
+  // 32-wide panels (full-candidate fronts): one wave up to 64 rows, register tiles up to 512
+  else if (rmax <= 64) k_panel_wave<32><<<cnt, 64, 0, st>>>(PANEL1_ARGS);
   else if (rmax <= 128) k_panel_reg<32, 2><<<cnt, 128, 0, st>>>(PANEL1_ARGS);
   else if (rmax <= 256) k_panel_reg<32, 4><<<cnt, 256, 0, st>>>(PANEL1_ARGS);
   else if (rmax <= 512) k_panel_reg<32, 8><<<cnt, 512, 0, st>>>(PANEL1_ARGS);

@@ -459,164 +459,6 @@ __device__ __forceinline__ void gemm128_mfma_body(const GemmTask& t, int m0, int
   if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
 }
 
-// Interior tiles (m, n in range), fast path.  Every global access is (wave-uniform 64-bit base
-// in SGPRs) + (per-lane 32-bit byte offset fixed for the whole tile), so an operand load costs
-// one instruction and its address arithmetic is scalar; the 16 staging loads of the next slice
-// are spread over the first two k-quads of the current one, and each k-quad's LDS fragments are
-// read while the previous quad's MFMAs run.  MODE: 0 = no next slice, 1 = next slice complete
-// (no guards), 2 = next slice partial (k guards).  Same staging, fragments and accumulation
-// order as gemm128_mfma_body (bitwise-identical results).
-__device__ __forceinline__ double ldu(const char* ubase, uint32_t off) {
-  return *gbl(reinterpret_cast<const double*>(ubase + off));
-}
-template <int MODE>
-__device__ __forceinline__ void mfma_slice(const GemmTask& t, int m0, int n0, int k0n, int cur,
-                                           double (&As)[2][HBK_][HBM_], double (&Bs)[2][HBK_][HLDB_],
-                                           v4d (&acc)[4][4], uint32_t a_lo, uint32_t b_lo, int ak, int bk) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = (wv & 1) * 64, wc = (wv >> 1) * 64;
-  const int li = lane & 15, lk = lane >> 4;
-  const int ar = tid & 127, bc = tid >> 4;
-  double ra[8], rb[8];
-  double fa[2][4], fb[2][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    fa[0][i] = As[cur][lk][wr + 16 * i + li];
-    fb[0][i] = Bs[cur][lk][wc + 16 * i + li];
-  }
-#pragma unroll
-  for (int kq = 0; kq < HBK_ / 4; ++kq) {
-    const int c = kq & 1;
-    if (MODE != 0 && kq < 2) {
-#pragma unroll
-      for (int r = 4 * kq; r < 4 * kq + 4; ++r) {
-        const char* ua = reinterpret_cast<const char*>(t.A) + ((int64_t)(k0n + 2 * r) * t.lda + m0) * 8;
-        const char* ub = reinterpret_cast<const char*>(t.B) + ((int64_t)(n0 + 16 * r) * t.ldb + k0n) * 8;
-        if (MODE == 1) {
-          ra[r] = ldu(ua, a_lo);
-          rb[r] = ldu(ub, b_lo);
-        } else {
-          const int kk = k0n + ak + 2 * r;
-          ra[r] = kk < t.k ? ldu(ua, a_lo) : 0.0;
-          rb[r] = k0n + bk < t.k ? ldu(ub, b_lo) : 0.0;
-        }
-      }
-    }
-    if (kq + 1 < HBK_ / 4) {
-      const int k = (kq + 1) * 4 + lk;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        fa[c ^ 1][i] = As[cur][k][wr + 16 * i + li];
-        fb[c ^ 1][i] = Bs[cur][k][wc + 16 * i + li];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[c][j], fa[c][i], acc[i][j], 0, 0, 0);
-  }
-  if (MODE != 0) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      As[cur ^ 1][ak + 2 * r][ar] = ra[r];
-      Bs[cur ^ 1][bk][bc + 16 * r] = -rb[r];
-    }
-  }
-}
-
-template <bool TRSM>
-__device__ __forceinline__ void gemm128_mfma_interior(const GemmTask& t, int m0, int n0,
-                                                      double (&As)[2][HBK_][HBM_], double (&Bs)[2][HBK_][HLDB_],
-                                                      const GrowthArgs& ga) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = (wv & 1) * 64, wc = (wv >> 1) * 64;
-  const int li = lane & 15, lk = lane >> 4;
-  const int ar = tid & 127, ak = tid >> 7;
-  const int bk = tid & 15, bc = tid >> 4;
-  const int K = t.k;
-  // C: lane part (lk * ldc + li) * 8, uniform part per (i, j, r)
-  const uint32_t c_lo = (uint32_t)(((int64_t)lk * t.ldc + li) * 8);
-  v4d acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const char* uc = reinterpret_cast<const char*>(t.C) +
-                         ((int64_t)(n0 + wc + 16 * j + 4 * r) * t.ldc + m0 + wr + 16 * i) * 8;
-        acc[i][j][r] = ldu(uc, c_lo);
-      }
-  const uint32_t a_lo = (uint32_t)(((int64_t)ak * t.lda + ar) * 8);
-  const uint32_t b_lo = (uint32_t)(((int64_t)bc * t.ldb + bk) * 8);
-  const int nk = (K + HBK_ - 1) / HBK_;
-  const int nfull = K / HBK_;
-  {   // slice 0
-    double ra[8], rb[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const char* ua = reinterpret_cast<const char*>(t.A) + ((int64_t)(2 * r) * t.lda + m0) * 8;
-      const char* ub = reinterpret_cast<const char*>(t.B) + ((int64_t)(n0 + 16 * r) * t.ldb) * 8;
-      ra[r] = ak + 2 * r < K ? ldu(ua, a_lo) : 0.0;
-      rb[r] = bk < K ? ldu(ub, b_lo) : 0.0;
-    }
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      As[0][ak + 2 * r][ar] = ra[r];
-      Bs[0][bk][bc + 16 * r] = -rb[r];
-    }
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const int k0n = (kt + 1) * HBK_;
-    if (kt + 1 < nfull) mfma_slice<1>(t, m0, n0, k0n, cur, As, Bs, acc, a_lo, b_lo, ak, bk);
-    else if (kt + 1 < nk) mfma_slice<2>(t, m0, n0, k0n, cur, As, Bs, acc, a_lo, b_lo, ak, bk);
-    else mfma_slice<0>(t, m0, n0, k0n, cur, As, Bs, acc, a_lo, b_lo, ak, bk);
-    __syncthreads();
-  }
-  double gmax = 0.0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        char* uc = reinterpret_cast<char*>(t.C) + ((int64_t)(n0 + wc + 16 * j + 4 * r) * t.ldc + m0 + wr + 16 * i) * 8;
-        *gbl(reinterpret_cast<double*>(uc + c_lo)) = acc[i][j][r];
-        if (TRSM) gmax = fmax(gmax, fabs(acc[i][j][r]));
-      }
-  if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
-}
-
-template <bool TRSM>
-__global__ __launch_bounds__(256, 2) void k_gemm128_mfma(const GemmTask* __restrict__ tasks, int ntask,
-                                                         GrowthArgs ga) {
-  __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
-  __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
-  const int64_t b = blockIdx.x;
-  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
-  int tm, tn;
-  tile_rc<HBM_>(t, b - t.tile0, tm, tn);
-  const int m0 = tm * HBM_, n0 = tn * HBM_;
-  if (m0 + HBM_ <= t.m && n0 + HBM_ <= t.n) gemm128_mfma_body<TRSM, true>(t, m0, n0, As, Bs, ga);
-  else gemm128_mfma_body<TRSM, false>(t, m0, n0, As, Bs, ga);
-}
-
-template <bool TRSM>
-__global__ __launch_bounds__(256, 2) void k_gemm128_mfma6(const GemmTask* __restrict__ tasks, int ntask,
-                                                          GrowthArgs ga) {
-  __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
-  __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
-  const int64_t b = blockIdx.x;
-  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
-  int tm, tn;
-  tile_rc<HBM_>(t, b - t.tile0, tm, tn);
-  const int m0 = tm * HBM_, n0 = tn * HBM_;
-  if (m0 + HBM_ <= t.m && n0 + HBM_ <= t.n) gemm128_mfma_interior<TRSM>(t, m0, n0, As, Bs, ga);
-  else gemm128_mfma_body<TRSM, false>(t, m0, n0, As, Bs, ga);
-}
 
 // ------------------------------------------------------------------------------------
 // MFMA tile v2 (tile code 130; the default Schur-update kernel): the same 128 x 128 output tile
@@ -1072,10 +914,6 @@ hipError_t launch_gemm_g(hipStream_t st, int64_t ntiles, const GemmTask* tasks, 
   const bool trsm = info != nullptr;
   if (tile == 130 && trsm) k_gemm128_mfma2<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 130) k_gemm128_mfma2<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 138 && trsm) k_gemm128_mfma6<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 138) k_gemm128_mfma6<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 129 && trsm) k_gemm128_mfma<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 129) k_gemm128_mfma<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 128)   // VALU 128 tile (SMLU_VALU_GEMM only; never used for the TRSM form)
     k_gemm128<<<(unsigned)(maxwg > 0 ? std::min<int64_t>(ntiles, maxwg) : ntiles), 256, 0, st>>>(
         tasks, ntask, ntiles);

@@ -725,8 +725,8 @@ static int build_schedule(smlu_handle* h) {
   if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
   if (const char* e = std::getenv("SMLU_T128MIN")) h->t128_min = std::atoll(e);
   h->small_k = !(std::getenv("SMLU_SMALLK") && std::atoi(std::getenv("SMLU_SMALLK")) == 0);
-  // MFMA 128 tile: 130 = v2 (16-byte operand traffic, kernels_gemm.hip), 129 = v1 (SMLU_MFMA_TILE)
-  const int mfma_tile = std::getenv("SMLU_MFMA_TILE") ? std::atoi(std::getenv("SMLU_MFMA_TILE")) : 130;
+  // MFMA 128 tile: code 130 (v2: 16-byte operand traffic, kernels_gemm.hip)
+  const int mfma_tile = 130;
   // GEMM-form TRSM (k_tri_inv + GEMM tasks) needs the growth epilogue of the MFMA/64 tiles
   {
     const char* e = std::getenv("SMLU_TRSM_GEMM");
@@ -4133,8 +4133,8 @@ double smlu_stat(const smlu_handle* h, const char* key) {
     for (const Launch& L : h->fac) {
       const bool gemm = L.kind == K_GEMM || L.kind == K_GEMMU || L.kind == K_GEMMO || L.kind == K_GEMM22;
       const bool trsm = L.kind == K_TRSML;
-      if (v == "mfma128" && gemm && (L.aux == 129 || L.aux == 130)) ++c;
-      else if (v == "mfma128_trsm" && trsm && (L.aux == 129 || L.aux == 130)) ++c;
+      if (v == "mfma128" && gemm && L.aux == 130) ++c;
+      else if (v == "mfma128_trsm" && trsm && L.aux == 130) ++c;
       else if (v == "valu128" && gemm && L.aux == 128) ++c;
       else if (v == "k64" && gemm && L.aux == 65) ++c;
       else if (v == "k64_trsm" && trsm && L.aux == 65) ++c;

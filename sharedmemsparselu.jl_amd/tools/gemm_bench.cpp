@@ -23,8 +23,8 @@ int main(int argc, char** argv) {
       if (sscanf(argv[a], "%d,%d,%d,%d,%d,%d", &x.m, &x.n, &x.k, &x.lda, &x.ldb, &x.ldc) >= 3) sv.push_back(x);
     }
   }
-  // variants: tile codes of launch_gemm (GB_TILES="129,130"); the first one is the reference
-  std::vector<int> tiles_list = {64, 128, 129};
+  // variants: tile codes of launch_gemm (GB_TILES="128,130"); the first one is the reference
+  std::vector<int> tiles_list = {64, 128, 130};
   if (const char* e = std::getenv("GB_TILES")) {
     tiles_list.clear();
     for (const char* p = e; *p;) { tiles_list.push_back(std::atoi(p)); while (*p && *p != ',') ++p; if (*p) ++p; }

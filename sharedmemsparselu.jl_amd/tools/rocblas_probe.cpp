@@ -41,7 +41,7 @@ int main(int argc, char** argv) {
     int64_t tiles = (int64_t)t.tiles_m * ((n + 127) / 128);
     CK(hipMemcpy(dt, &t, sizeof t, hipMemcpyHostToDevice));
     const double alpha = -1.0, beta = 1.0;
-    auto ours = [&](double* C) { (void)C; CK(launch_gemm(st, tiles, dt, 1, 129, 0)); };
+    auto ours = [&](double* C) { (void)C; CK(launch_gemm(st, tiles, dt, 1, 130, 0)); };
     auto vend = [&](double* C) {
       RB(rocblas_dgemm(hb, rocblas_operation_none, rocblas_operation_none, m, n, k, &alpha, A, lda, B, ldb, &beta, C, ldc));
     };
