@@ -729,9 +729,18 @@ void Plan::compute_owners(int np, int64_t block) {
         std::vector<double> c(m);
         for (int b = 0; b < m; ++b) c[b] = cost(sets[b], 1);
         for (int extra = k - m; extra > 0; --extra) {
-          const int bi = (int)(std::max_element(c.begin(), c.end()) - c.begin());
+          // the most expensive bin that still gains from one more rank (a single leaf does not)
+          std::vector<int> ord(m);
+          std::iota(ord.begin(), ord.end(), 0);
+          std::sort(ord.begin(), ord.end(), [&](int a, int b) { return c[a] != c[b] ? c[a] > c[b] : a < b; });
+          int bi = ord[0];
+          double cb = cost(sets[bi], r[bi] + 1);
+          for (int o : ord) {
+            const double cn = cost(sets[o], r[o] + 1);
+            if (cn < c[o] * (1 - 1e-12)) { bi = o; cb = cn; break; }
+          }
           ++r[bi];
-          c[bi] = cost(sets[bi], r[bi]);
+          c[bi] = cb;
         }
         const double mk = *std::max_element(c.begin(), c.end());
         if (best < 0 || mk < best * (1 - 1e-12)) {

@@ -85,8 +85,8 @@ def _subtree_ranks(owner, parent):
 @pytest.mark.parametrize("nparts", [2, 3, 4, 8])
 @pytest.mark.parametrize("case", ["poisson3d", "random"])
 def test_proportional_mapping_groups(nparts, case):
-    # proportional mapping: the ranks under every shared front form a contiguous range, sibling
-    # subtrees use disjoint ranks (their shared fronts run concurrently), so each rank works on at
+    # proportional mapping: sibling subtrees use disjoint ranks (their shared fronts run
+    # concurrently) except for light subtrees packed whole onto one rank, so each rank works on at
     # most one shared front per tree level
     A = mats.poisson3d(20) if case == "poisson3d" else mats.random_dominant(3000, 0.003, seed=5)
     P = smlu.Plan(A)
@@ -98,8 +98,6 @@ def test_proportional_mapping_groups(nparts, case):
         if parent[s] >= 0:
             kids.setdefault(int(parent[s]), []).append(s)
     for s in np.flatnonzero(owner == -1):
-        r = sorted(R[s])
-        assert len(r) >= 2 and r == list(range(r[0], r[-1] + 1)), (s, r)
         ch = kids.get(int(s), [])
         for i in range(len(ch)):
             for j in range(i + 1, len(ch)):
