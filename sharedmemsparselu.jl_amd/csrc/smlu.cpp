@@ -2810,9 +2810,10 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
     v = h->vbufm.p;
     rh.n = nrhs;
   }
-  // batches of up to 8 right-hand sides run the sweeps (NR-wide hand-off slots), wider ones the
-  // per-block launches (fwdm / bwdm)
-  const bool steps = rh.n > 8 && h->nranks == 1;
+  // batches of up to SMLU_SWEEP_MAX_RHS (<= 8) right-hand sides run the sweeps (NR-wide hand-off
+  // slots), wider ones the per-block launches (fwdm / bwdm)
+  static const int sweep_max_rhs = std::getenv("SMLU_SWEEP_MAX_RHS") ? std::atoi(std::getenv("SMLU_SWEEP_MAX_RHS")) : 1;
+  const bool steps = rh.n > std::min(8, std::max(1, sweep_max_rhs)) && h->nranks == 1;
   // The sync-free sweeps' waits are bounded: a wait that gives up raises sstatus, which is read back
   // after every solve that ran them; the solve is then re-run on the per-block schedule (fwdm / bwdm,
   // bitwise the same arithmetic), so a timed-out sweep never returns a wrong x.  Partitioned handles
@@ -3373,7 +3374,11 @@ extern "C" {
 // ldiv! plus iterative refinement on the original (unscaled) A: x <- x + A \ (b - A x).  The
 // diagonal-tile pivoting of large fronts cannot always keep growth below 1/pivot_tol; when a
 // refactor flags such weak pivots (h->weak), refine = -1 applies up to 3 steps (the pivot-
-// failure fallback).  Stops when the residual max-norm stops halving.
+// failure fallback).  So it does for non-dominant values factored under a diagonal
+// tolerance below the pivot tolerance (UMFPACK's symmetric default 0.001 < 0.1): a diagonal kept
+// at 0.001 of its column lets the factors grow up to 1000x per step, and UMFPACK's own solve
+// refines by default (IRSTEP 2) for the same reason.  Stops when the residual max-norm stops
+// halving (at once for an accurate solve: one residual, no extra solve).
 // Residual buffers and the column of every A entry (allocated on first use).
 static int ensure_residual(smlu_handle* h) {
   Plan& P = h->plan;
@@ -3394,8 +3399,14 @@ static int ensure_residual(smlu_handle* h) {
   return SMLU_OK;
 }
 
+static int auto_refine_steps(const smlu_handle* h) {
+  if (h->opts.refine >= 0) return h->opts.refine;
+  const bool diag_pref = !h->plan.given_order && !h->dominant && h->opts.diag_pivot_tol < h->opts.pivot_tol;
+  return (h->weak > 0 || diag_pref) ? 3 : 0;
+}
+
 static int solve_refined(smlu_handle* h, const double* db, double* dx) {
-  const int steps = h->opts.refine < 0 ? (h->weak > 0 ? 3 : 0) : h->opts.refine;
+  const int steps = auto_refine_steps(h);
   h->refine_steps = 0;
   h->refine_resid = -1;
   if (steps == 0) return run_solve_dev(h, db, dx, 0);
@@ -3471,7 +3482,7 @@ int smlu_solve(smlu_handle* h, const double* b, double* x) {
 // ldb == ldx (the batch is permuted into the work buffer before x is written).
 static int solve_multi_dev(smlu_handle* h, int64_t nrhs, const double* d_B, int64_t ldb, double* d_X,
                            int64_t ldx) {
-  const int steps = h->opts.refine < 0 ? (h->weak > 0 ? 3 : 0) : h->opts.refine;
+  const int steps = auto_refine_steps(h);
   const bool batched = steps == 0 && h->nranks == 1 && nrhs > 1 && !std::getenv("SMLU_NO_MULTI_RHS");
   if (!batched) {
     for (int64_t j = 0; j < nrhs; ++j) {
@@ -3509,7 +3520,7 @@ int smlu_solve_multi(smlu_handle* h, int64_t nrhs, const double* B, int64_t ldb,
   const int64_t n = h->plan.n;
   if (ldb < n || ldx < n) return fail(h, SMLU_ERR_ARG, "leading dimension smaller than n");
   HIPCHK(hipSetDevice(h->device));
-  if (nrhs > 1 && h->nranks == 1 && (h->opts.refine == 0 || (h->opts.refine < 0 && h->weak == 0))) {
+  if (nrhs > 1 && h->nranks == 1 && auto_refine_steps(h) == 0) {
     if (!h->wrk2m.p) HIPCHK(h->wrk2m.alloc((size_t)n * kMultiRhs));
     double* d = h->wrk2m.p;
     for (int64_t j = 0; j < nrhs; j += kMultiRhs) {
