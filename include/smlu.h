@@ -202,9 +202,11 @@ int smlu_get_fronts(smlu_handle* h, int64_t* first, int64_t* parent, int64_t* ro
 /* F.L, F.U, F.p, F.q, F.Rs of a ComplexF64 handle (src/SharedMemSparseLU.jl:47-52: L and U are
  * SparseMatrixCSC{ComplexF64}): the complex n x n factors, values as interleaved (re, im) doubles
  * (2*nnz), same conventions as smlu_get_factors (L unit diagonal first, U diagonal last, rows
- * sorted; F.L*F.U == (F.Rs .* A)[F.p, F.q]).  Folded exactly from the real-equivalent factors;
- * available when the pivot sequence kept every complex row pair together (always under diagonal
- * pivoting), else SMLU_ERR_STATE (smlu_get_factors still gives the 2n x 2n real-equivalent ones). */
+ * sorted; F.L*F.U == (F.Rs .* A)[F.p, F.q]).  Folded from the real-equivalent factors: a complex
+ * handle pivots K pair by pair (rows 2i, 2i+1 stay adjacent; the diagonal pair is kept when its
+ * complex magnitude passes diag_pivot_tol, else the largest pair; inside a pair the larger entry
+ * leads, a swap that folds back as a row rotation by -i), so the complex factors always exist
+ * (SMLU_ERR_STATE only if a zero-free-diagonal row transversal was needed, which breaks pairs). */
 int smlu_get_sizes_z(smlu_handle* h, int64_t* n, int64_t* nnz_L, int64_t* nnz_U);
 int smlu_get_factors_z(smlu_handle* h, int64_t* Lcolptr, int64_t* Lrowval, double* Lnzval,
                        int64_t* Ucolptr, int64_t* Urowval, double* Unzval,
@@ -243,9 +245,10 @@ void smlu_plan_destroy(smlu_plan* plan);
 
 /* ---- multi-GPU partition ---------------------------------------------------
  * One process per GPU; every rank calls the same functions with the same matrix (collective).
- * The assembly tree is split by proportional mapping: subtrees are bin-packed onto ranks and
- * factored with no communication; each front above them is shared by the ranks owning its
- * subtrees as a 1D block-cyclic column partition (blocks of 384 columns): the owner of a pivot
+ * The assembly tree is split by proportional mapping (each subtree set gets a contiguous rank
+ * range sized by a cost model; sibling subtrees get disjoint ranges, so their shared fronts run
+ * concurrently); a subtree on one rank is factored with no communication; each front above them
+ * is shared by its range as a 1D block-cyclic column partition (blocks of 384 columns): the owner of a pivot
  * block factors it and broadcasts it (L block, pivots, tile inverses) to the group, every
  * member updates the column blocks it owns; the children's F22 columns move to the owners of
  * the parent's columns before its assembly.  Each rank allocates only its own fronts and

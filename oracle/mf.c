@@ -61,6 +61,7 @@ struct oracle_mf {
   int64_t *colptr, *rowval;     /* pattern copy (row scaling) */
   double diag_tol, piv_tol;
   int nthreads;
+  int pairs;                    /* ComplexF64 real-equivalent: pair-preserving pivots (below) */
   double* work;                 /* flops of each front's subtree (task cut-off) */
 };
 
@@ -296,15 +297,82 @@ static void gemm_sub(int64_t m, int64_t n, int64_t k, const double* A, int64_t l
 /* Factor one assembled front W (M x M, column-major, ld M): ns pivots with the candidate rule of
  * `mode`, blocked right-looking (panels of NBP columns, trailing update by gemm_sub).
  * perm[0..ns): local pre-swap row of each position.  Returns the front's flags. */
+/* Pair-preserving pivot rule of a ComplexF64 handle's real-equivalent K (rows and columns 2i, 2i+1
+ * of complex row/column i stay adjacent; every front starts at an even position).  Even column k:
+ * candidate pairs (e, e+1), e even, of squared magnitude x^2 + y^2 (fma(x, x, y * y), K column k
+ * holds x, y of the complex entry); the diagonal pair is kept when its squared magnitude is at
+ * least diag_tol^2 times the largest and nonzero, else the first largest pair; inside the chosen
+ * pair the row of larger |value| in column k becomes the pivot row (a swap inside the pair is the
+ * complex row times -i up to a sign, folded back at export).  Odd column k: the pair's other row,
+ * no search.  The GPU kernels (kernels_front.hip, SNode.cpair) restate the same rule. */
+static void swap_rows(double* W, int64_t M, int64_t a, int64_t b, int32_t* perm) {
+  if (a == b) return;
+  for (int64_t j = 0; j < M; ++j) {
+    const double t = W[j * M + a];
+    W[j * M + a] = W[j * M + b];
+    W[j * M + b] = t;
+  }
+  const int32_t t = perm[a]; perm[a] = perm[b]; perm[b] = t;
+}
+
 static int factor_front(double* W, int64_t M, int64_t ns, int mode, double diag_tol, double piv_tol,
-                        int32_t* perm, int par) {
+                        int32_t* perm, int par, int pairs) {
   const int64_t NBP = 32;
   int flags = 0;
   for (int64_t i = 0; i < ns; ++i) perm[i] = (int32_t)i;
   for (int64_t kb = 0; kb < ns; kb += NBP) {
     const int64_t ke = kb + NBP < ns ? kb + NBP : ns;
+    int64_t second = -1;   /* pairs: position of the current pair's other row */
     for (int64_t k = kb; k < ke; ++k) {
       double* col = W + k * M;
+      if (pairs) {
+        if ((k & 1) == 0) {
+          int64_t cend = ns;
+          if (mode == 2) {
+            const int64_t t0 = (k / 64) * 64;
+            cend = t0 + 64 < ns ? t0 + 64 : ns;
+          }
+          double am = 0.0, amo = 0.0;
+          int64_t ai = k;
+          for (int64_t e = k; e < cend; e += 2) {
+            const double v = fma(col[e], col[e], col[e + 1] * col[e + 1]);
+            if (v > am) { am = v; ai = e; }
+          }
+          for (int64_t e = cend; e < M; e += 2) {
+            const double v = fma(col[e], col[e], col[e + 1] * col[e + 1]);
+            if (v > amo) amo = v;
+          }
+          const double d2 = fma(col[k], col[k], col[k + 1] * col[k + 1]);
+          int64_t pc = k;
+          if (am <= 0.0) flags |= 1;
+          else if (!(d2 >= diag_tol * diag_tol * am && d2 != 0.0)) pc = ai;
+          const int64_t r1 = fabs(col[pc + 1]) > fabs(col[pc]) ? pc + 1 : pc;
+          const int64_t r2 = 2 * pc + 1 - r1;
+          if (am > 0.0) {
+            const double pm = fma(col[pc], col[pc], col[pc + 1] * col[pc + 1]);
+            if (mode == 0) {
+              if (pm < piv_tol * piv_tol * (am > amo ? am : amo)) flags |= 2;
+            } else if (amo > pm / (piv_tol * piv_tol)) {
+              flags |= 2;
+            }
+          }
+          swap_rows(W, M, k, r1, perm);
+          second = r2 == k ? r1 : r2;
+        } else {
+          swap_rows(W, M, k, second, perm);
+          if (col[k] == 0.0) flags |= 1;
+        }
+        const double pinv = 1.0 / col[k];
+        if (col[k] != 0.0)
+          for (int64_t i = k + 1; i < M; ++i) col[i] *= pinv;
+        for (int64_t j = k + 1; j < ke; ++j) {
+          double* cj = W + j * M;
+          const double u = cj[k];
+          if (u != 0.0)
+            for (int64_t i = k + 1; i < M; ++i) cj[i] -= col[i] * u;
+        }
+        continue;
+      }
       int64_t cend = ns;
       if (mode == 2) {
         const int64_t t0 = (k / 64) * 64;
@@ -390,7 +458,7 @@ static int do_front(oracle_mf* h, const double* nzval, int64_t s, int par) {
     h->f22[ch] = NULL;
   }
   int32_t* perm = h->rowperm + h->first[s];
-  h->flags[s] = factor_front(W, M, ns, h->mode[s], h->diag_tol, h->piv_tol, perm, par);
+  h->flags[s] = factor_front(W, M, ns, h->mode[s], h->diag_tol, h->piv_tol, perm, par, h->pairs);
   memcpy(h->store + h->loff[s], W, (size_t)(M * ns) * sizeof(double));
   for (int64_t j = 0; j < nu; ++j)
     memcpy(h->store + h->uoff[s] + j * ns, W + (ns + j) * M, (size_t)ns * sizeof(double));
@@ -424,6 +492,8 @@ static void front_task(oracle_mf* h, const double* nzval, int64_t s, int* err) {
 
 /* One numeric factorization (row scaling + every front).  Returns 0, or 1 when some front
  * flagged a zero candidate column, negative on allocation failure. */
+void oracle_mf_set_pairs(oracle_mf* h, int pairs) { h->pairs = pairs; }
+
 int oracle_mf_factor(oracle_mf* h, const double* nzval) {
   oracle_rowscale(h->n, h->colptr, h->rowval, nzval, h->Rs);
   int err = 0;

@@ -39,6 +39,8 @@ oracle_mf* oracle_mf_create(int64_t n, const int64_t* colptr, const int64_t* row
                             const int64_t* rowptr, const int64_t* rows, const int32_t* mode,
                             double diag_tol, double piv_tol, int nthreads, int* status);
 int oracle_mf_factor(oracle_mf* h, const double* nzval);
+/* ComplexF64 real-equivalent K: pair-preserving pivots (mf.c: factor_front). */
+void oracle_mf_set_pairs(oracle_mf* h, int pairs);
 void oracle_mf_result(const oracle_mf* h, int32_t* rowperm, int32_t* flags, double* Rs);
 void oracle_mf_destroy(oracle_mf* h);
 int oracle_dominant(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* a);

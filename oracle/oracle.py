@@ -76,6 +76,7 @@ def lib():
         L.oracle_mf_create.argtypes = [ctypes.c_int64, vp, vp, vp, vp, ctypes.c_int64, vp, vp, vp, vp, vp,
                                        ctypes.c_double, ctypes.c_double, ctypes.c_int,
                                        ctypes.POINTER(ctypes.c_int)]
+        L.oracle_mf_set_pairs.argtypes = [vp, ctypes.c_int]
         L.oracle_mf_factor.restype = ctypes.c_int
         L.oracle_mf_factor.argtypes = [vp, vp]
         L.oracle_mf_result.argtypes = [vp, vp, vp, vp]
@@ -176,7 +177,7 @@ class MultifrontalOracle:
     smlu_plan_fronts plus the column order `q`; `mode`: candidate set per front (None: every
     fully-summed row).  factor(values) -> status (0 ok, 1 zero candidate column)."""
 
-    def __init__(self, A, q, fronts, mode=None, diag_tol=0.001, pivot_tol=0.1, threads=1):
+    def __init__(self, A, q, fronts, mode=None, diag_tol=0.001, pivot_tol=0.1, threads=1, pairs=False):
         A, cp, ri, _ = _csc(A)
         self.n = A.shape[0]
         self._keep = [np.ascontiguousarray(v, dtype=np.int64) for v in
@@ -192,6 +193,8 @@ class MultifrontalOracle:
                                          float(diag_tol), float(pivot_tol), int(threads), ctypes.byref(st))
         if not self._h:
             raise RuntimeError(f"oracle_mf_create failed ({st.value})")
+        if pairs:   # ComplexF64 real-equivalent: pair-preserving pivots (mf.c)
+            lib().oracle_mf_set_pairs(self._h, 1)
 
     def factor(self, values):
         v = np.ascontiguousarray(values, dtype=np.float64)
@@ -240,7 +243,7 @@ def front_modes(fronts, pivmode, dominant_values, full_piv_ns=None):
 
 
 def gpu_pivot_choice(A, q, fronts, *, pivmode=0, dominant_values=None, given=False, pivot_tol=0.1,
-                     diag_tol=0.001, full_piv_ns=None, values=None):
+                     diag_tol=0.001, full_piv_ns=None, values=None, pairs=False):
     """Independent restatement of the GPU path's whole pivot decision for one factorization:
     the candidate modes, threshold partial pivoting inside every front (mf.c), and the
     re-pivoting refactor (a zero or weak pivot while diagonal-tile fronts exist -> every blocked
@@ -256,11 +259,13 @@ def gpu_pivot_choice(A, q, fronts, *, pivmode=0, dominant_values=None, given=Fal
                                                                                  shape=A.shape))
     if dominant_values:
         pivmode = 0
+    if pairs:   # a ComplexF64 handle pivots pairs over every fully-summed row of every front
+        pivmode = 1
     dt = 0.0 if given else diag_tol
 
     def run(pm):
         modes = front_modes(fronts, pm, dominant_values, full_piv_ns)
-        mf = MultifrontalOracle(A, q, fronts, modes, diag_tol=dt, pivot_tol=pivot_tol)
+        mf = MultifrontalOracle(A, q, fronts, modes, diag_tol=dt, pivot_tol=pivot_tol, pairs=pairs)
         st = mf.factor(vals)
         out = (mf.p, modes, mf.flags.copy(), st)
         mf.close()
@@ -268,7 +273,7 @@ def gpu_pivot_choice(A, q, fronts, *, pivmode=0, dominant_values=None, given=Fal
 
     p, modes, flags, st = run(pivmode)
     if ((st == 1 or (flags & 2).any()) and pivmode == 0 and (modes == 2).any() and pivot_tol > 0
-            and not given):
+            and not given and not pairs):
         pivmode = 1
         p, modes, flags, st = run(1)
     return p, pivmode, modes, flags

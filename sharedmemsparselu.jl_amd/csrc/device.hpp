@@ -21,6 +21,8 @@ struct SNode {
                               // 2 = blocked + diagonal-tile pivoting with growth check
   int32_t chbeg, chend;       // children in chlist[chbeg, chend)
   int32_t level;
+  int32_t cpair;              // 1: ComplexF64 real-equivalent, pair-preserving pivots (rows and
+                              //    columns 2i, 2i+1 stay adjacent; oracle/mf.c: factor_front)
 };
 
 // C(m x n, ldc) -= A(m x k, lda) * B(k x n, ldb), column-major; tiles of 64 x 64 numbered

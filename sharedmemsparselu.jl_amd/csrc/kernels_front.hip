@@ -236,8 +236,52 @@ __global__ __launch_bounds__(64 * NW) void k_front_small(const int32_t* __restri
   // factorization
   int flag = 0, err = -1;   // wave 0, lane 0
   double gmax = 0.0;
+  __shared__ int s_second;   // pair rule: position of the current pair's other row
   for (int k = 0; k < ns; ++k) {
-    if (wv == 0) {
+    if (s.cpair && wv == 0) {   // ComplexF64 real-equivalent: pair-preserving pivots (mf.c rule)
+      if ((k & 1) == 0) {
+        double am = -1.0, amo = 0.0;
+        int ai = k;
+        for (int e = k + 2 * lane; e < M; e += 128) {
+          const double x = lds[k * ld + e], y = lds[k * ld + e + 1];
+          const double v = fma(x, x, y * y);
+          if (e < ns) {
+            if (v > am) { am = v; ai = e; }
+          } else if (v > amo) {
+            amo = v;
+          }
+        }
+        am = wave_max_idx(am, ai);
+        amo = wave_max(amo);
+        if (lane == 0) {
+          const double x = lds[k * ld + k], y = lds[k * ld + k + 1];
+          const double d2 = fma(x, x, y * y);
+          int pc = k;
+          if (am <= 0.0) {
+            flag |= 1;
+            if (err < 0) err = k;
+          } else if (!(d2 >= diag_tol * diag_tol * am && d2 != 0.0)) {
+            pc = ai;
+          }
+          const int r1 = fabs(lds[k * ld + pc + 1]) > fabs(lds[k * ld + pc]) ? pc + 1 : pc;
+          const int r2 = 2 * pc + 1 - r1;
+          if (am > 0.0) {
+            const double a = lds[k * ld + pc], b = lds[k * ld + pc + 1];
+            const double pm = fma(a, a, b * b);
+            if (pm < piv_tol * piv_tol * fmax(am, amo)) flag |= 2;
+            gmax = fmax(gmax, sqrt(fmax(am, amo) / pm));
+          }
+          s_piv = r1;
+          s_second = r2 == k ? r1 : r2;
+        }
+      } else if (lane == 0) {
+        s_piv = s_second;
+        if (lds[k * ld + s_second] == 0.0) {   // read before the swap: the row that moves to k
+          flag |= 1;
+          if (err < 0) err = k;
+        }
+      }
+    } else if (wv == 0) {
       double am = -1.0, amo = 0.0;
       int ai = k;
       for (int i = k + lane; i < M; i += 64) {
@@ -328,6 +372,8 @@ __global__ __launch_bounds__(64 * NW) void k_panel_reg(const int32_t* __restrict
   __shared__ int s_idx[NW];
   __shared__ int s_any[NW];
   __shared__ int s_piv;
+  __shared__ double s_cv[64 * NW];            // pair rule: the column's values by position
+  int second = 0;                             // pair rule: position of the pair's other row
   const int sid = list[2 * blockIdx.x];       // (front, swap slot) pairs
   const SNode s = sn[sid];
   FrontPtrs f = front_ptrs(s, store, scratch);
@@ -370,8 +416,61 @@ __global__ __launch_bounds__(64 * NW) void k_panel_reg(const int32_t* __restrict
     const bool cand = has && pos >= kabs;
     // optimistic: the diagonal candidate publishes its whole row (the pivot row if accepted)
     if (tid == q) publish(cur, rest, kabs - kk, restb);
+    if (s.cpair && (kabs & 1) == 0 && has) s_cv[pos] = cur[kk];
     __syncthreads();
     const double akk = s_prow[kabs];
+    int p = q;
+    if (s.cpair) {   // ComplexF64 real-equivalent: pair-preserving pivots (oracle/mf.c rule)
+      if ((kabs & 1) == 0) {
+        const double pv = has ? s_cv[pos ^ 1] : 0.0;
+        const double m2 = fma(cur[kk], cur[kk], pv * pv);
+        const bool lead = cand && (pos & 1) == 0;
+        double am = lead ? m2 : -1.0;
+        int ai = lead ? pos : 0x7fffffff;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const double ov = __shfl_xor(am, o, 64);
+          const int oi = __shfl_xor(ai, o, 64);
+          if (ov > am || (ov == am && oi < ai)) { am = ov; ai = oi; }
+        }
+        if (NW > 1) {
+          if (lane == 0) { s_val[wv] = am; s_idx[wv] = ai; }
+          __syncthreads();
+          am = s_val[0];
+          ai = s_idx[0];
+#pragma unroll
+          for (int v = 1; v < NW; ++v)
+            if (s_val[v] > am || (s_val[v] == am && s_idx[v] < ai)) { am = s_val[v]; ai = s_idx[v]; }
+        }
+        const double x = s_cv[kabs], y = s_cv[kabs + 1];
+        const double d2 = fma(x, x, y * y);
+        int pc = kabs;
+        if (am <= 0.0) {
+          flag |= 1;
+          if (err < 0) err = kb + kabs;
+        } else if (!(d2 >= diag_tol * diag_tol * am && d2 != 0.0)) {
+          pc = ai;
+        }
+        const int r1 = fabs(s_cv[pc + 1]) > fabs(s_cv[pc]) ? pc + 1 : pc;
+        const int r2 = 2 * pc + 1 - r1;
+        second = r2 == kabs ? r1 : r2;
+        p = s_who[r1];
+      } else {
+        p = s_who[second];
+      }
+      if (p != q) {             // publish the chosen pivot row
+        __syncthreads();
+        if (tid == p) {
+          publish(cur, rest, kabs - kk, restb);
+          s_piv = pos;
+        }
+        __syncthreads();
+      }
+      if ((kabs & 1) == 1 && s_prow[kabs] == 0.0) {
+        flag |= 1;
+        if (err < 0) err = kb + kabs;
+      }
+    } else {
     const bool beats = cand && pos != kabs && fabs(cur[kk]) * diag_tol > fabs(akk);
     bool any = __ballot(beats) != 0ull;
     if (NW > 1) {
@@ -381,7 +480,6 @@ __global__ __launch_bounds__(64 * NW) void k_panel_reg(const int32_t* __restrict
 #pragma unroll
       for (int v = 0; v < NW; ++v) any |= s_any[v] != 0;
     }
-    int p = q;
     if (any || akk == 0.0) {   // full argmax over the candidates (rare under dominance)
       double am = cand ? fabs(cur[kk]) : -1.0;
       int ai = cand ? pos : 0x7fffffff;
@@ -414,6 +512,7 @@ __global__ __launch_bounds__(64 * NW) void k_panel_reg(const int32_t* __restrict
         }
         __syncthreads();
       }
+    }
     }
     const double pinv = recip(s_prow[kabs]);
     if (cand && tid != p) {
@@ -536,14 +635,50 @@ __global__ __launch_bounds__(64) void k_panel_wave(const int32_t* __restrict__ l
   int pos = lane, who = lane;
   int flag = 0, err = -1;
   double lmax = 0.0;
+  int second = 0;   // pair rule: position of the current pair's other row
   auto column = [&](double (&cur)[32], double (&rest)[32], const int kk, const int kabs,
                     const bool restb) {
     const int q = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(who, kabs));
     const bool cand = has && pos >= kabs;
     const double akk = readlane_f64(cur[kk], q);
-    const bool beats = cand && pos != kabs && fabs(cur[kk]) * diag_tol > fabs(akk);
     int p = q;
-    if (__ballot(beats) != 0ull || akk == 0.0) {   // full argmax (rare under dominance)
+    if (s.cpair) {   // ComplexF64 real-equivalent: pair-preserving pivots (oracle/mf.c rule)
+      if ((kabs & 1) == 0) {
+        const int plane = __shfl(who, pos ^ 1, 64);          // lane holding my pair partner
+        const double pv = __shfl(cur[kk], plane, 64);
+        const double m2 = fma(cur[kk], cur[kk], pv * pv);
+        const bool lead = cand && (pos & 1) == 0;
+        double am = lead ? m2 : -1.0;
+        int ai = lead ? pos : 0x7fffffff;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const double ov = __shfl_xor(am, o, 64);
+          const int oi = __shfl_xor(ai, o, 64);
+          if (ov > am || (ov == am && oi < ai)) { am = ov; ai = oi; }
+        }
+        const double d2 = readlane_f64(m2, q);
+        int pc = kabs;
+        if (am <= 0.0) {
+          flag |= 1;
+          if (err < 0) err = kb + kabs;
+        } else if (!(d2 >= diag_tol * diag_tol * am && d2 != 0.0)) {
+          pc = __builtin_amdgcn_readfirstlane(ai);
+        }
+        const double va = readlane_f64(cur[kk], __builtin_amdgcn_readlane(who, pc));
+        const double vb = readlane_f64(cur[kk], __builtin_amdgcn_readlane(who, pc + 1));
+        const int r1 = fabs(vb) > fabs(va) ? pc + 1 : pc;
+        const int r2 = 2 * pc + 1 - r1;
+        second = r2 == kabs ? r1 : r2;
+        p = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(who, r1));
+      } else {
+        p = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(who, second));
+        if (readlane_f64(cur[kk], p) == 0.0) {
+          flag |= 1;
+          if (err < 0) err = kb + kabs;
+        }
+      }
+    } else if (__ballot(cand && pos != kabs && fabs(cur[kk]) * diag_tol > fabs(akk)) != 0ull || akk == 0.0) {
+      // full argmax (rare under dominance)
       double am = cand ? fabs(cur[kk]) : -1.0;
       int ai = cand ? pos : 0x7fffffff;
 #pragma unroll
@@ -958,9 +1093,66 @@ __global__ __launch_bounds__(1024) void k_panel_tall(const int32_t* __restrict__
   gdbl* P = f.L + (int64_t)kb * M + kb;
   int flag = 0, err = -1;
   double lmax = 0.0;
+  int second = 0;   // pair rule: position of the current pair's other row
   for (int k = 0; k < w; ++k) {
     gdbl* col = P + (int64_t)k * M;
     const double akk = col[k];
+    if (s.cpair) {   // ComplexF64 real-equivalent: pair-preserving pivots (oracle/mf.c rule)
+      int p;
+      if ((k & 1) == 0) {
+        double am = -1.0;
+        int ai = 0x7fffffff;
+        for (int e = k + 2 * tid; e < R; e += 2 * NT) {
+          const double v = fma(col[e], col[e], col[e + 1] * col[e + 1]);
+          if (v > am) { am = v; ai = e; }
+        }
+        am = wave_max_idx(am, ai);
+        if (lane == 0) { s_val[wv] = am; s_idx[wv] = ai; }
+        __syncthreads();
+        am = s_val[0];
+        ai = s_idx[0];
+        for (int v = 1; v < NWV; ++v)
+          if (s_val[v] > am || (s_val[v] == am && s_idx[v] < ai)) { am = s_val[v]; ai = s_idx[v]; }
+        const double d2 = fma(col[k], col[k], col[k + 1] * col[k + 1]);
+        int pc = k;
+        if (am <= 0.0) {
+          flag |= 1;
+          if (err < 0) err = kb + k;
+        } else if (!(d2 >= diag_tol * diag_tol * am && d2 != 0.0)) {
+          pc = ai;
+        }
+        const int r1 = fabs(col[pc + 1]) > fabs(col[pc]) ? pc + 1 : pc;
+        const int r2 = 2 * pc + 1 - r1;
+        second = r2 == k ? r1 : r2;
+        p = r1;
+      } else {
+        p = second;
+        if (col[p] == 0.0) {
+          flag |= 1;
+          if (err < 0) err = kb + k;
+        }
+      }
+      __syncthreads();   // every thread has read the column before the interchange
+      if (tid == 0) s_tp[k] = p;
+      if (p != k) {
+        for (int j = tid; j < w; j += NT) {
+          const double a = P[(int64_t)j * M + k];
+          P[(int64_t)j * M + k] = P[(int64_t)j * M + p];
+          P[(int64_t)j * M + p] = a;
+        }
+      }
+      __syncthreads();
+      const double pinv = recip(col[k]);
+      for (int r = k + 1 + tid; r < R; r += NT) {
+        const double l = col[r] * pinv;
+        col[r] = l;
+        lmax = fmax(lmax, fabs(l));
+        if (l != 0.0)
+          for (int j = k + 1; j < w; ++j) P[(int64_t)j * M + r] = fma(-l, P[(int64_t)j * M + k], P[(int64_t)j * M + r]);
+      }
+      __syncthreads();
+      continue;
+    }
     bool beats = false;
     for (int r = k + 1 + tid; r < R; r += NT) beats |= fabs(col[r]) * diag_tol > fabs(akk);
     const bool any_w = __ballot(beats) != 0ull;

@@ -435,6 +435,7 @@ struct smlu_handle {
   std::vector<GemmTask> hgt;  // host copy of the GEMM tasks (rocBLAS calls read their operands from it)
   // ComplexF64 handle (smlu_create_z): the plan and factors are those of the real-equivalent K
   bool zc = false;
+  bool cpair = false;                // pair-preserving pivots (complex handle, no row transversal)
   int64_t zn = 0, znnz = 0;          // complex n and nnz(A)
   std::vector<int64_t> zdst;         // per complex entry: K position of its (re, im) in column 2j
   std::vector<int32_t> zoff;         // ... and the distance to its (-im, re) in column 2j+1
@@ -598,7 +599,9 @@ static int build_schedule(smlu_handle* h) {
   // dominant), so there the mid-size fronts take the faster diagonal-tile path too; its growth
   // check still flags weak pivots if a refactor's new values lose dominance (refinement then
   // runs in the solves).  SMLU_FULLPIV_NS overrides (dev).
-  const int64_t full_piv_ns = h->pivmode == 1 ? std::numeric_limits<int64_t>::max()
+  // a complex handle's pair-preserving pivots search every fully-summed row (mode 1): the
+  // diagonal-tile panels have no pair rule
+  const int64_t full_piv_ns = (h->pivmode == 1 || h->cpair) ? std::numeric_limits<int64_t>::max()
                               : std::getenv("SMLU_FULLPIV_NS") ? std::atoll(std::getenv("SMLU_FULLPIV_NS"))
                               : h->dominant ? (int64_t)kSmallM : (int64_t)kFullPivNs;
   for (int64_t s = 0; s < nsup; ++s) {
@@ -621,6 +624,7 @@ static int build_schedule(smlu_handle* h) {
     r.chbeg = (int32_t)P.ch_ptr[s];
     r.chend = (int32_t)P.ch_ptr[s + 1];
     r.level = P.s_level[s];
+    r.cpair = h->cpair ? 1 : 0;
     if (h->nranks > 1 && P.dist(s)) { r.mode = 2; r.nb = kNbTile; }   // shared fronts: diagonal-tile pivoting
     h->hsn[s] = r;
   }
@@ -3002,6 +3006,7 @@ static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, 
   if (!e.empty()) return fail(nullptr, SMLU_ERR_ARG, e);
   h->rank = rank;
   h->nranks = nranks;
+  h->cpair = preorder != nullptr && !h->plan.matched;
   if (!p && !h->plan.matched) h->dominant = diagonally_dominant(n, colptr, rowval, nzval, h->opts.index_base);
   if (nranks > 1) {
     if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
@@ -3190,6 +3195,7 @@ static int refactor_csc_impl(smlu_handle* h, int64_t n, const int64_t* colptr, c
   if (!e.empty()) return fail(h, SMLU_ERR_ARG, e);
   h->dominant = !h->plan.matched && diagonally_dominant(n, colptr, rowval, nzval, base);
   h->pivmode = 0;
+  h->cpair = preorder != nullptr && !h->plan.matched;
   int rc = setup_device(h);
   if (rc != SMLU_OK) return rc;
   HIPCHK(hipMemcpyAsync(h->A.p, nzval, sizeof(double) * h->plan.nnzA, hipMemcpyHostToDevice, h->stream));
@@ -3850,15 +3856,24 @@ static int export_complex(smlu_handle* h, ExportedZ& Z, bool values) {
   const int64_t n = h->zn;
   Z.p.resize(n);
   Z.q.resize(n);
+  // A pair kept in reverse order (rows 2i+1, 2i: the pair rule swapped inside the pair) is the
+  // real equivalent of the complex row times -i with its second row negated (N): with
+  // K_rot = N P K Q, the factors of K_rot are N L N and N U, which fold as usual to complex
+  // L_c U_c = (D Rs.*A)[p, q], D = diag(-i on swapped rows); then (Rs.*A)[p, q] = L' U' with
+  // L' = D^-1 L_c D (still unit lower) and U' = D^-1 U_c.
+  std::vector<char> sw(n, 0);
   for (int64_t k = 0; k < n; ++k) {
-    if (X.p[2 * k] % 2 != 0 || X.p[2 * k + 1] != X.p[2 * k] + 1)
+    const int64_t a = X.p[2 * k], b = X.p[2 * k + 1];
+    if (std::min(a, b) % 2 != 0 || std::max(a, b) != std::min(a, b) + 1)
       return fail(h, SMLU_ERR_STATE, "complex factors: the row pivots split complex row pair " + std::to_string(k) +
                                          " (only the real-equivalent factors exist; smlu_get_factors)");
     if (X.q[2 * k] % 2 != 0 || X.q[2 * k + 1] != X.q[2 * k] + 1)
       return fail(h, SMLU_ERR_STATE, "internal: complex column pair split");
-    Z.p[k] = X.p[2 * k] / 2;
+    sw[k] = a > b;
+    Z.p[k] = std::min(a, b) / 2;
     Z.q[k] = X.q[2 * k] / 2;
   }
+  auto nsign = [&](int64_t r) { return ((r & 1) && sw[r / 2]) ? -1.0 : 1.0; };   // N's entry of K row r
   // L: complex column k from K's column 2k+1 (rows >= 2k+1); pairs (2i, 2i+1) are adjacent
   Z.Lp.assign(n + 1, 0);
   Z.Li.clear();
@@ -3872,12 +3887,24 @@ static int export_complex(smlu_handle* h, ExportedZ& Z, bool values) {
         Z.Lx.push_back(0.0);
         Z.Lx.push_back(0.0);
       }
-      const double v = values ? X.Lx[e] : 0.0;
+      const double v = values ? X.Lx[e] * nsign(r) * nsign(c) : 0.0;
       if (r & 1) Z.Lx[Z.Lx.size() - 2] = v;    // real part: row 2i+1 of the odd column
       else Z.Lx[Z.Lx.size() - 1] = -v;         // imaginary part: minus row 2i
     }
     Z.Lp[k + 1] = (int64_t)Z.Li.size();
   }
+  // D^-1 L_c D: entry (i, k) times d_k / d_i, d = -i on swapped rows (x i: (re, im) -> (-im, re))
+  if (values)
+    for (int64_t k = 0; k < n; ++k)
+      for (int64_t e = Z.Lp[k]; e < Z.Lp[k + 1]; ++e) {
+        const int64_t i = Z.Li[e];
+        if (sw[i] == sw[k]) continue;
+        double& re = Z.Lx[2 * e];
+        double& im = Z.Lx[2 * e + 1];
+        const double r0 = re, i0 = im;
+        if (sw[k]) { re = i0; im = -r0; }     // d_k / d_i = -i
+        else { re = -i0; im = r0; }           // d_k / d_i = i
+      }
   // U: complex column j from the even rows of K's columns 2j (real part) and 2j+1 (minus imaginary)
   Z.Up.assign(n + 1, 0);
   Z.Ui.clear();
@@ -3898,6 +3925,14 @@ static int export_complex(smlu_handle* h, ExportedZ& Z, bool values) {
     }
     Z.Up[j + 1] = (int64_t)Z.Ui.size();
   }
+  // D^-1 U_c: row i times 1/d_i = i on swapped rows (U's even rows are not touched by N)
+  if (values)
+    for (size_t e = 0; e < Z.Ui.size(); ++e)
+      if (sw[Z.Ui[e]]) {
+        const double r0 = Z.Ux[2 * e], i0 = Z.Ux[2 * e + 1];
+        Z.Ux[2 * e] = -i0;
+        Z.Ux[2 * e + 1] = r0;
+      }
   return SMLU_OK;
 }
 
@@ -4102,6 +4137,7 @@ double smlu_stat(const smlu_handle* h, const char* key) {
   if (!h || !key) return std::numeric_limits<double>::quiet_NaN();
   std::string k(key);
   if (k == "complex") return h->zc ? 1.0 : 0.0;
+  if (k == "cpair") return h->cpair ? 1.0 : 0.0;
   if (k == "launches") return (double)h->nlaunch;
   if (k == "refactor_ms_last") return h->refactor_ms;
   if (k == "solve_ms_last") return h->solve_ms;

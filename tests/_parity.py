@@ -37,7 +37,8 @@ def pivot_parity(A, F, prev_pivmode=0, full_piv_ns=None, given=False):
     fx = _real(F)
     p_or, pm, modes, _ = O.gpu_pivot_choice(A, fx["q"], fr, pivmode=prev_pivmode, full_piv_ns=full_piv_ns,
                                             given=given, pivot_tol=F.stat("pivot_tol"),
-                                            diag_tol=F.stat("diag_pivot_tol") if not given else 0.1)
+                                            diag_tol=F.stat("diag_pivot_tol") if not given else 0.1,
+                                            pairs=F.stat("cpair") == 1)
     assert np.array_equal(modes, fr["mode"]), "per-front pivot candidate modes differ from the restated rule"
     assert int(F.stat("pivmode")) == pm, (F.stat("pivmode"), pm)
     bad = np.flatnonzero(np.asarray(fx["p"]) != p_or)

@@ -161,3 +161,54 @@ def test_repivot_restatement():
     D2 = D + np.diag(D.sum(axis=1) + 1)
     p2, pm2, modes2, _ = O.gpu_pivot_choice(sp.csc_matrix(D2), q, fr)
     assert pm2 == 0 and (modes2 == 2).any() and np.array_equal(p2, q)
+
+
+def fold_complex(L, U, p, q, n):
+    """Python restatement of smlu.cpp: export_complex -- the complex n x n factors from the scalar
+    LU of the real-equivalent K under pair-preserving pivots, pairs kept in either order."""
+    sw = p[0::2] > p[1::2]
+    pc, qc = np.minimum(p[0::2], p[1::2]) // 2, q[0::2] // 2
+    nsign = np.ones(2 * n)
+    nsign[1::2][sw] = -1.0
+    Ld, Ud = L.toarray(), U.toarray()
+    Lr = nsign[:, None] * Ld * nsign[None, :]          # N L N
+    Lc = Lr[1::2, 1::2] - 1j * Lr[0::2, 1::2]           # real: row 2i+1, imag: -row 2i (odd columns)
+    Uc = Ud[0::2, 0::2] - 1j * Ud[0::2, 1::2]           # even rows of columns 2j, 2j+1
+    d = np.where(sw, -1j, 1.0)
+    return (Lc * d[None, :] / d[:, None]), Uc / d[:, None], pc, qc
+
+
+@pytest.mark.parametrize("case", ["imaginary_diagonal", "random", "fe"])
+def test_pair_rule_keeps_complex_pairs(case):
+    # ComplexF64 handles pivot the real-equivalent K pair by pair (mf.c: factor_front, pairs):
+    # the row order keeps every (2i, 2i+1) pair adjacent, and the folded complex factors satisfy
+    # L U == (Rs.*A)[p, q] with L unit lower (a swap inside a pair folds back as a row rotation)
+    rng = np.random.default_rng(3)
+    n = 40
+    if case == "imaginary_diagonal":
+        A = sp.random(n, n, density=0.15, random_state=np.random.RandomState(1), format="csc") * (1 + 0.5j)
+        A = sp.csc_matrix(A + sp.diags(1j * (3 + rng.random(n))))
+    elif case == "random":
+        D = rng.random((n, n)) + 1j * rng.random((n, n))
+        A = sp.csc_matrix(D)
+    else:
+        F = O.test_matrix(np.random.default_rng(47), 9)
+        A = sp.csc_matrix(F + 1j * (F != 0).multiply(np.random.default_rng(5).random(F.shape)))
+    n = A.shape[0]
+    K = O.real_equivalent(A)
+    m = K.shape[0]
+    q = np.arange(m)
+    mf = O.MultifrontalOracle(K, q, one_front(m), [1], pairs=True)
+    assert mf.factor(K.data) == 0
+    p = mf.p
+    mf.close()
+    assert np.array_equal(np.sort(np.minimum(p[0::2], p[1::2]) // 2), np.arange(n))
+    assert np.all(np.abs(p[0::2] - p[1::2]) == 1) and np.all(np.minimum(p[0::2], p[1::2]) % 2 == 0)
+    if case == "imaginary_diagonal":
+        assert (p[0::2] > p[1::2]).any()    # some pairs were swapped inside
+    ref = O.OracleLU(K, p, q)
+    Lc, Uc, pc, qc = fold_complex(ref.L, ref.U, p, q, n)
+    Rs = ref.Rs[0::2]   # rows 2i, 2i+1 sum the same magnitudes (in another order: equal to rounding)
+    B = (sp.diags(Rs) @ A).toarray()[pc][:, qc]
+    assert np.allclose(np.diag(Lc), 1.0) and np.allclose(np.triu(Lc, 1), 0) and np.allclose(np.tril(Uc, -1), 0)
+    assert np.abs(Lc @ Uc - B).max() <= 1e-12 * np.abs(B).max()
