@@ -260,7 +260,7 @@ def gpu_pivot_choice(A, q, fronts, *, pivmode=0, dominant_values=None, given=Fal
     if dominant_values:
         pivmode = 0
     if pairs:   # a ComplexF64 handle pivots pairs over every fully-summed row of every front
-        pivmode = 1
+        full_piv_ns = np.iinfo(np.int64).max
     dt = 0.0 if given else diag_tol
 
     def run(pm):
