@@ -818,49 +818,23 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
       if (UPPER) tri64_scale_upper(drow, dinv, bw);
     }
   }
-  // my row of the column block being applied (d) and of the next one (dn): every tile is loaded
-  // one apply step ahead, so its HBM latency overlaps the current step's wait and products
-  double d[64], dn[64];
-  auto load_into = [&](double (&dst)[64], int64_t c, int bw) {
+  double d[64];   // my row of the column block being applied, loaded before its x is available
+  auto load_tile = [&](int64_t c, int bw) {
 #pragma unroll
-    for (int j = 0; j < 64; ++j) dst[j] = j < bw ? Lp[(64 * c + j) * M + row] : 0.0;
+    for (int j = 0; j < 64; ++j) d[j] = j < bw ? Lp[(64 * c + j) * M + row] : 0.0;
   };
   auto fma_tile = [&](int bw) {   // o -= L[row, block] * x_block (x in xs), k_tri_block's dot64_split
 #pragma unroll
     for (int r = 0; r < NR; ++r)
       if (r < nr) o[r] -= dot64_split(d, bw, [&](int j) { return xs[j][r]; });
   };
-  // apply steps: the external blocks (solved by earlier chunks: forward 0 .. min(4q, nblk)-1,
-  // backward nblk-1 down to nblk-4q; every row of this chunk lies beyond them), then the
-  // internal blocks t = 0..3 of this chunk (applied by the waves beyond t)
+  // external blocks (solved by earlier chunks): forward 0 .. min(4q, nblk)-1, backward nblk-1
+  // down to nblk-4q; every row of this chunk lies beyond them
   const int64_t next = min<int64_t>(4 * q, nblk);
-  auto step_block = [&](int64_t e) -> int64_t {   // block of apply step e (< 0 or >= nblk: none)
-    const int64_t k = e < next ? e : 4 * q + (e - next);
-    return UPPER ? nblk - 1 - k : k;
-  };
-  auto step_applies = [&](int64_t e) -> bool {
-    const int64_t b = step_block(e);
-    if (b < 0 || b >= nblk || e >= next + 4) return false;
-    if (e < next) return has;
-    const int t = (int)(e - next);
-    return has && (wv > t || (wv == t && myblk >= nblk));
-  };
-  auto prefetch = [&](int64_t e) {
-    if (step_applies(e)) {
-      const int64_t c = step_block(e);
-      load_into(dn, c, (int)min<int64_t>(64, ns - 64 * c));
-    }
-  };
-  auto take = [&]() {
-#pragma unroll
-    for (int j = 0; j < 64; ++j) d[j] = dn[j];
-  };
-  prefetch(0);
   for (int64_t e = 0; e < next; ++e) {
     const int64_t c = UPPER ? nblk - 1 - e : e;
     const int bw = (int)min<int64_t>(64, ns - 64 * c);
-    if (has) take();
-    prefetch(e + 1);
+    if (has) load_tile(c, bw);
     sweep_wait(flags + c, epoch, status, spin);
     if (wv == 0)
       for (int r = 0; r < min(nr, NR); ++r) xs[lane][r] = atomic_read_f64(xhf + (c * kMultiRhs + r) * 64 + lane);
@@ -877,8 +851,7 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
     // rows that apply block b: the waves beyond t, and the update rows of wave t when block b is
     // the last, partial one (forward): same per-block arithmetic as every other row
     const bool applies = has && (wv > t || (wv == t && myblk >= nblk));
-    if (applies) take();
-    prefetch(next + t + 1);
+    if (applies) load_tile(b, bw);
     if (wv == t) {
       sweep_mark(UPPER, item, wv, 2);
 #pragma unroll
