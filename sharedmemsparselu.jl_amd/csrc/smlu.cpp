@@ -2196,8 +2196,10 @@ static int build_schedule(smlu_handle* h) {
   }
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
   h->ninv = (int64_t)invfront.size();
-  if (h->ninv > 0 && !std::getenv("SMLU_NO_DIAG_INV")) {   // dev knob: substitution on the diagonal blocks
-    // (finish_factor launches k_diag_inv after every factorization: inverses of the current factors)
+  // SMLU_DIAG_INV=1: the solves apply the large fronts' diagonal blocks as products with their
+  // inverses (finish_factor launches k_diag_inv after every factorization).  Off by default: the
+  // sweeps are hand-off bound, the product saved nothing (13.89 ms vs 13.77 ms substituting, 128^3)
+  if (h->ninv > 0 && std::getenv("SMLU_DIAG_INV") && std::atoi(std::getenv("SMLU_DIAG_INV")) == 1) {
     HIPCHK(h->invbase.upload(invbase.data(), invbase.size(), st));
     HIPCHK(h->invfront.upload(invfront.data(), invfront.size(), st));
     HIPCHK(h->dinvbuf.alloc((size_t)h->ninv * 2 * 4096));
