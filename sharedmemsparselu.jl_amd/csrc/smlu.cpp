@@ -2241,6 +2241,26 @@ static int build_schedule(smlu_handle* h) {
   }
   HIPCHK(h->gtasks.upload(gt.data(), gt.size(), st));
   h->hgt = gt;
+  if (const char* path = std::getenv("SMLU_DUMP_LAUNCHES")) {   // dev: tools/gemm_launch_report.py
+    if (FILE* fp = std::fopen(path, "w")) {
+      std::fprintf(fp, "idx,kind,step,cnt,nwg,tile,flops,m_max,n_max,k_max\n");
+      for (size_t i = 0; i < h->fac.size(); ++i) {
+        const Launch& L = h->fac[i];
+        int mm = 0, nn = 0, kk = 0;
+        const bool gemm = L.kind == K_GEMM || L.kind == K_GEMMO || L.kind == K_GEMM22 || L.kind == K_GEMMU ||
+                          L.kind == K_TRSML;
+        if (gemm)
+          for (int64_t t = L.off; t < L.off + L.cnt; ++t) {
+            mm = std::max(mm, gt[t].m);
+            nn = std::max(nn, gt[t].n);
+            kk = std::max(kk, gt[t].k);
+          }
+        std::fprintf(fp, "%zu,%d,%d,%lld,%lld,%lld,%.6e,%d,%d,%d\n", i, L.kind, L.step, (long long)L.cnt,
+                     (long long)L.nwg, gemm ? (long long)L.aux : -1LL, L.flops, mm, nn, kk);
+      }
+      std::fclose(fp);
+    }
+  }
   HIPCHK(h->stasks.upload(st_tasks.data(), st_tasks.size(), st));
   HIPCHK(h->urtasks.upload(ur_tasks.data(), ur_tasks.size(), st));
   HIPCHK(h->xcols.upload(xc.data(), xc.size(), st));
