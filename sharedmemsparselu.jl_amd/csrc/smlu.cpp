@@ -2439,6 +2439,8 @@ struct Timer {
       float ms = 0;
       if (hipEventElapsedTime(&ms, h->ev_pool[i].first, h->ev_pool[i].second) == hipSuccess)
         h->kind_ms[h->ev_kind[i]] += ms;
+      else
+        (void)hipGetLastError();   // a pair not recorded this time: no sticky error for the caller's next API call
     }
   }
 };
