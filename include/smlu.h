@@ -103,6 +103,14 @@ int smlu_refactor(smlu_handle* h, const double* nzval);
  * on a partitioned handle the ranks agree on it through the transport's allreduce). */
 int smlu_refactor_device(smlu_handle* h, const double* d_nzval);
 
+/* The caller's stream (a hipStream_t; NULL = the null stream, the default): every *_device
+ * entry point orders its reads of caller memory after the work enqueued on that stream so far
+ * (an event wait on the handle's stream, no host synchronisation), and returns with its outputs
+ * complete.  Set it to the stream that produces the values / right-hand sides (the Python mirror
+ * passes torch's current stream on every device call).  No reference counterpart: Julia's
+ * arrays are host memory. */
+int smlu_set_stream(smlu_handle* h, void* stream);
+
 /* lu!(F, A) where A's pattern may differ: re-analyses when it does (the reference's
  * `reallocate` branch, src/SharedMemSparseLU.jl:252-273). */
 int smlu_refactor_csc(smlu_handle* h, int64_t n, const int64_t* colptr, const int64_t* rowval,

@@ -99,6 +99,7 @@ struct Rhs {
 };
 constexpr int kMultiRhs = 16;   // right-hand sides per solve launch
 constexpr int kSweepWK = 4;     // k_tri_sweep: 64-row blocks (worker waves) per work item
+constexpr int kSweepXB = 64;    // k_tri_sweep: external blocks x right-hand sides per run (LDS 32 KB)
 // Inverses of the large fronts' 64x64 diagonal blocks for the solves (k_diag_inv): block b of front s
 // (base[s] >= 0) at inv + ((base[s] + b) * 2 + upper) * 4096, column-major; base == nullptr or
 // base[s] < 0: substitution.

@@ -1,5 +1,7 @@
 // kernels_solve.hip — level-scheduled forward/backward solves (lsolve!/rsolve!, src/SharedMemSparseLU.jl:349-392)
 // and ldiv!'s scale/permute steps (:318-339).
+#include <climits>
+
 #include "kernels_common.hpp"
 
 namespace smlu {
@@ -694,7 +696,10 @@ void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step, const SNod
 //  * block b is published by writing its 64 x NR solved values into its hand-off slot (atomic swaps)
 //    and then setting flag[b] to the epoch (atomic max) behind the wave's vmcnt drain and a barrier;
 //  * a consumer polls flag[b] (atomic compare-and-swap that never matches) until it reaches the epoch
-//    and reads the slot the same way on the raw bits.
+//    and reads the slot the same way on the raw bits.  The waits are bounded: a wait that gives up
+//    raises *status, which the host reads after every solve and then re-runs the solve on the
+//    per-block schedule (smlu.cpp: run_solve_dev), so a timed-out chunk's values are never returned;
+//    spin <= 0 reports every wait as timed out (the tests' forced-fallback knob SMLU_SWEEP_SPIN=0).
 // Deadlock-free: items are taken in ticket order and an item only waits on items of lower tickets
 // (earlier chunks of the same front), which are running.  Per right-hand side the arithmetic does
 // not depend on the batch width (a batched column is bitwise the single solve).
@@ -719,28 +724,6 @@ __device__ __forceinline__ void atomic_write_f64(double* p, double v) {
   (void)__hip_atomic_exchange(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// Bounded wait for flag f to reach the epoch.  A wait that gives up raises *status; the host reads
-// it after every solve and re-runs the solve on the per-block schedule (smlu.cpp: run_solve_dev), so
-// a timed-out chunk's values are never returned.  spin <= 0 reports every wait as timed out (the
-// tests' forced-fallback knob SMLU_SWEEP_SPIN=0).
-__device__ __forceinline__ void sweep_wait(int32_t* f, int32_t epoch, int32_t* status, int spin) {
-  if (threadIdx.x == 0) {
-    if (spin <= 0) {
-      (void)__hip_atomic_fetch_max(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      int n = 0;
-      while (atomic_read_i32(f) < epoch) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++n > spin) {
-          (void)__hip_atomic_fetch_max(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          break;
-        }
-      }
-    }
-  }
-  __syncthreads();
-}
-
 // Dev instrumentation (tools/sweep_trace.py): one launch shape (grid, direction) records per work item
 // and wave the 100 MHz real-time clock at its start, after its external blocks, before and after its
 // own substitution, after publishing, and at its end.  Compiled in with -DSMLU_SWEEP_TRACE only
@@ -767,7 +750,9 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
                  const SNode* __restrict__ sn, const double* __restrict__ store, double* __restrict__ x,
                  double* __restrict__ vbuf, Rhs rh, int spin, DiagInv di) {
   __shared__ double xs[64][NR];
+  __shared__ double xb[kSweepXB * 64];   // x of a run of external blocks, [block][row][rhs]
   __shared__ unsigned long long s_ticket;
+  __shared__ int s_run;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) s_ticket = __hip_atomic_fetch_add(tick, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
@@ -829,25 +814,76 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
       if (r < nr) o[r] -= dot64_split(d, bw, [&](int j) { return xs[j][r]; });
   };
   // external blocks (solved by earlier chunks): forward 0 .. min(4q, nblk)-1, backward nblk-1
-  // down to nblk-4q; every row of this chunk lies beyond them
+  // down to nblk-4q; every row of this chunk lies beyond them.  Taken in runs: wave 0 polls the
+  // flags of up to kSweepXB / NR blocks at once (one lane per flag) and takes the published prefix,
+  // the workgroup reads the run's hand-off slots together, then applies the run's blocks in order
+  // (tile loads only) -- two memory-side round trips per run instead of two per block, so a chunk
+  // that fell behind the chain catches up at the tile-load rate; at the chain's front a run is one
+  // block.  The next run's first tile is loaded before its poll.
   const int64_t next = min<int64_t>(4 * q, nblk);
-  for (int64_t e = 0; e < next; ++e) {
-    const int64_t c = UPPER ? nblk - 1 - e : e;
-    const int bw = (int)min<int64_t>(64, ns - 64 * c);
-    if (has) load_tile(c, bw);
-    sweep_wait(flags + c, epoch, status, spin);
-    if (wv == 0)
-      for (int r = 0; r < min(nr, NR); ++r) xs[lane][r] = atomic_read_f64(xhf + (c * kMultiRhs + r) * 64 + lane);
+  auto ext_blk = [&](int64_t e) { return UPPER ? nblk - 1 - e : e; };
+  auto ext_bw = [&](int64_t e) { return (int)min<int64_t>(64, ns - 64 * ext_blk(e)); };
+  if (has && next > 0) load_tile(ext_blk(0), ext_bw(0));
+  for (int64_t e = 0; e < next;) {
+    if (wv == 0) {
+      const int cand = (int)min<int64_t>(kSweepXB / NR, next - e);
+      int run = cand;
+      if (spin <= 0) {   // forced timeout (tests): report, take the run as it is
+        if (lane == 0) (void)__hip_atomic_fetch_max(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        for (int n = 0;; ++n) {
+          const bool ok = lane >= cand || atomic_read_i32(flags + ext_blk(e + lane)) >= epoch;
+          const unsigned long long late = __ballot(!ok);
+          run = late ? __builtin_ctzll(late) : cand;
+          if (run > 0) break;
+          if (n >= spin) {   // give up: the host re-runs the solve on the per-block schedule
+            if (lane == 0) (void)__hip_atomic_fetch_max(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            run = cand;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (lane == 0) s_run = run;
+    }
     __syncthreads();
-    if (has) fma_tile(bw);
+    const int run = s_run;
+    for (int k = tid; k < run * NR * 64; k += 256) {
+      const int u = k / (NR * 64), r = (k / 64) % NR, l = k % 64;
+      if (r < nr) xb[(u * 64 + l) * NR + r] = atomic_read_f64(xhf + (ext_blk(e + u) * kMultiRhs + r) * 64 + l);
+    }
     __syncthreads();
+    for (int u = 0; u < run; ++u) {
+      const int bw = ext_bw(e + u);
+      if (u > 0 && has) load_tile(ext_blk(e + u), bw);
+      if (has) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+          if (r < nr) o[r] -= dot64_split(d, bw, [&](int j) { return xb[(u * 64 + j) * NR + r]; });
+      }
+    }
+    e += run;
+    if (has && e < next) load_tile(ext_blk(e), ext_bw(e));
+    __syncthreads();   // the run's slots are read before the next run overwrites them
   }
   sweep_mark(UPPER, item, wv, 1);
-  // internal blocks: wave t solves block b and publishes it, the waves beyond apply it
-  for (int t = 0; t < 4; ++t) {
+  // internal blocks: wave t solves block b and publishes it, the waves beyond apply it.  Publishing
+  // = raising flag[b] once the wave's slot writes have completed (s_waitcnt vmcnt(0): every lane's
+  // atomics).  The chunk's last block is raised at once (the next chunk waits on it); an earlier
+  // block by its wave at the top of the next step, while the next wave substitutes -- the write
+  // round trip then holds no workgroup barrier (waiting right after the solve made the barrier
+  // behind the other waves' apply wait for it, ~3 us per block).
+  const int nint = (int)max<int64_t>(0, min<int64_t>(4, nblk - 4 * q));
+  auto publish = [&](int t) {
     const int64_t b = UPPER ? nblk - 1 - 4 * q - t : 4 * q + t;
-    if (b < 0 || b >= nblk) break;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) (void)__hip_atomic_fetch_max(flags + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) sweep_mark(UPPER, item, t, 4);
+  };
+  for (int t = 0; t < nint; ++t) {
+    const int64_t b = UPPER ? nblk - 1 - 4 * q - t : 4 * q + t;
     const int bw = (int)min<int64_t>(64, ns - 64 * b);
+    if (t > 0 && wv == t - 1) publish(t - 1);
     // rows that apply block b: the waves beyond t, and the update rows of wave t when block b is
     // the last, partial one (forward): same per-block arithmetic as every other row
     const bool applies = has && (wv > t || (wv == t && myblk >= nblk));
@@ -871,14 +907,7 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
       sweep_mark(UPPER, item, wv, 3);
     }
     __syncthreads();   // xs (LDS) visible to the waves that apply block b
-    if (wv == t) {
-      // publish: raise the flag once this wave's slot writes have completed (vmcnt counts every
-      // lane's atomics of the wave); the other waves apply the block meanwhile, so the write
-      // round trip is off the chunk's own chain
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) (void)__hip_atomic_fetch_max(flags + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (lane == 0) sweep_mark(UPPER, item, t, 4);
-    }
+    if (t == nint - 1 && wv == t) publish(t);
     if (applies) fma_tile(bw);
     __syncthreads();
   }
@@ -1073,6 +1102,85 @@ __global__ __launch_bounds__(256) void k_dominance(int64_t n, const int64_t* __r
   }
   if (!(d > 0.0 && d >= off)) flags[1] = 0;
 }
+// Status record of a factorization / dominance test / solve for the host (smlu.cpp: read_status):
+// out[0] = out[7] = seq (the host accepts a copy only when both match its own sequence number);
+// with info: out[1] = weak-pivot nodes, out[2], out[3] = first zero-pivot node and its info word
+// (-1, 0: none), out[4], out[5] = first flagged node and its word; out[6] = words[0] | words[1] << 32.
+// One workgroup of 1024 threads.
+__global__ __launch_bounds__(1024) void k_status(const int32_t* __restrict__ info, int64_t nnodes,
+                                                 const int32_t* __restrict__ words, int nwords,
+                                                 long long* __restrict__ out, long long seq) {
+  __shared__ long long s_weak[1024];
+  __shared__ long long s_sing[1024], s_flag[1024];
+  const int tid = threadIdx.x;
+  long long weak = 0, sing = LLONG_MAX, flag = LLONG_MAX;
+  if (info)
+    for (int64_t i = tid; i < nnodes; i += 1024) {
+      const int32_t v = info[i];
+      weak += (v >> 1) & 1;
+      if ((v & 1) && i < sing) sing = i;
+      if ((v & 3) && i < flag) flag = i;
+    }
+  s_weak[tid] = weak;
+  s_sing[tid] = sing;
+  s_flag[tid] = flag;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if (tid < w) {
+      s_weak[tid] += s_weak[tid + w];
+      s_sing[tid] = min(s_sing[tid], s_sing[tid + w]);
+      s_flag[tid] = min(s_flag[tid], s_flag[tid + w]);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const long long sg = s_sing[0], fl = s_flag[0];
+    out[1] = s_weak[0];
+    out[2] = sg == LLONG_MAX ? -1 : sg;
+    out[3] = sg == LLONG_MAX ? 0 : info[sg];
+    out[4] = fl == LLONG_MAX ? -1 : fl;
+    out[5] = fl == LLONG_MAX ? 0 : info[fl];
+    const long long w0 = nwords > 0 ? (long long)(uint32_t)words[0] : 0;
+    const long long w1 = nwords > 1 ? (long long)(uint32_t)words[1] : 0;
+    out[6] = w0 | (w1 << 32);
+    out[0] = seq;
+    out[7] = seq;
+  }
+}
+// Dev (tools/determinism.py): an order-independent 64-bit hash per front of its factor values
+// (L panel + U12, bit patterns) and of its row permutation, to localise a factorization that
+// differs between two runs on the same values.  One workgroup per front.
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  return x ^ (x >> 33);
+}
+__global__ __launch_bounds__(256) void k_front_hash(const SNode* __restrict__ sn, const double* __restrict__ store,
+                                                    const int32_t* __restrict__ rowperm,
+                                                    unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long hv, hp;
+  const SNode r = sn[blockIdx.x];
+  const int64_t M = (int64_t)r.ns + r.nu;
+  if (threadIdx.x == 0) hv = hp = 0;
+  __syncthreads();
+  unsigned long long a = 0, b = 0;
+  const int64_t nl = M * r.ns, nu12 = (int64_t)r.ns * r.nu;
+  for (int64_t i = threadIdx.x; i < nl + nu12; i += 256) {
+    const double v = i < nl ? store[r.Loff + i] : store[r.Uoff + (i - nl)];
+    a += mix64((unsigned long long)__double_as_longlong(v) + 0x9e3779b97f4a7c15ull * (unsigned long long)(i + 1));
+  }
+  for (int64_t i = threadIdx.x; i < r.ns; i += 256)
+    b += mix64((unsigned long long)(uint32_t)rowperm[r.first + i] * 0x9e3779b97f4a7c15ull + (unsigned long long)i);
+  atomicAdd(&hv, a);
+  atomicAdd(&hp, b);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = hv;
+    out[2 * blockIdx.x + 1] = hp;
+  }
+}
 __global__ void k_axpy1(int64_t n, const double* __restrict__ d, double* __restrict__ x) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) x[i] += d[i];
@@ -1223,14 +1331,23 @@ hipError_t launch_residual(hipStream_t st, int64_t n, const int64_t* rowptr, con
 }
 hipError_t launch_dominance(hipStream_t st, int64_t n, const int64_t* colptr, const int32_t* arow,
                             const int64_t* rowptr, const int32_t* ent, const int32_t* acol, const double* a,
-                            int32_t* dflags, int32_t* hflags) {
+                            int32_t* dflags) {
   static const int32_t ones[2] = {1, 1};
   hipError_t e = hipMemcpyAsync(dflags, ones, sizeof(ones), hipMemcpyHostToDevice, st);
   if (e != hipSuccess) return e;
   if (n > 0) k_dominance<<<nblk(n, 256), 256, 0, st>>>(n, colptr, arow, rowptr, ent, acol, a, dflags);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  return hipMemcpyAsync(hflags, dflags, sizeof(ones), hipMemcpyDeviceToHost, st);
+  return hipGetLastError();
+}
+hipError_t launch_front_hash(hipStream_t st, int64_t nsup, const SNode* sn, const double* store, const int32_t* rowperm,
+                             unsigned long long* out) {
+  if (nsup <= 0) return hipSuccess;
+  k_front_hash<<<(unsigned)nsup, 256, 0, st>>>(sn, store, rowperm, out);
+  return hipGetLastError();
+}
+hipError_t launch_status(hipStream_t st, const int32_t* info, int64_t nnodes, const int32_t* words, int nwords,
+                         long long* out, long long seq) {
+  k_status<<<1, 1024, 0, st>>>(info, nnodes, words, nwords, out, seq);
+  return hipGetLastError();
 }
 hipError_t launch_axpy1(hipStream_t st, int64_t n, const double* d, double* x) {
   if (n <= 0) return hipSuccess;

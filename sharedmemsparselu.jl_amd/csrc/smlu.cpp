@@ -74,7 +74,9 @@ hipError_t launch_residual(hipStream_t, int64_t, const int64_t*, const int32_t*,
                            const double*, const double*, const double*, double*, double*);
 hipError_t launch_axpy1(hipStream_t, int64_t, const double*, double*);
 hipError_t launch_dominance(hipStream_t, int64_t, const int64_t*, const int32_t*, const int64_t*, const int32_t*,
-                            const int32_t*, const double*, int32_t*, int32_t*);
+                            const int32_t*, const double*, int32_t*);
+hipError_t launch_status(hipStream_t, const int32_t*, int64_t, const int32_t*, int, long long*, long long);
+hipError_t launch_front_hash(hipStream_t, int64_t, const SNode*, const double*, const int32_t*, unsigned long long*);
 hipError_t launch_expand_z(hipStream_t, int64_t, const double*, const int64_t*, const int32_t*, double*);
 hipError_t launch_perm_in(hipStream_t, int64_t, const int64_t*, const double*, const double*, double*, int,
                           int64_t, int64_t);
@@ -386,8 +388,10 @@ struct smlu_handle {
   double kind_ms[K_NKIND] = {0};
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pool;
   std::vector<int> ev_kind;
-  int32_t* hinfo = nullptr;  // pinned
-  int32_t* hsstat = nullptr; // pinned copy of sstatus, read after every solve that ran sweeps
+  hipStream_t caller = nullptr;   // caller's stream (smlu_set_stream; nullptr = the null stream)
+  hipEvent_t ev_caller = nullptr;
+  DBuf<long long> rb;         // status record for the host (k_status; read_status)
+  long long rb_seq = 0;       // sequence number of the last status record
   int64_t sweep_timeouts = 0;   // solves re-run on the per-block schedule after a sweep wait timed out
   int sweep_spin = 1 << 22;     // polls before a sweep wait gives up (SMLU_SWEEP_SPIN; 0 = always, tests)
   DBuf<double> bstash;          // the solve's input when the final step overwrites it (x === b, lsolve!/rsolve!)
@@ -425,6 +429,12 @@ struct smlu_handle {
                               //    fronts; 1: full-candidate pivoting in every blocked front (the
                               //    re-pivoting refactor after a zero or weak tile pivot)
   int64_t repivots = 0;       // re-pivoting refactors run so far
+  int64_t flag_node = -1;     // first flagged node of the last factorization and its info word
+  int32_t flag_info = 0;
+  int64_t repivot_node = -1;  // what triggered the last re-pivot: the first flagged node, its info
+  int32_t repivot_info = 0;   //   word (bit 0 zero pivot, bit 1 weak pivot) and the growth seen
+  double repivot_growth = 0;
+  SNode repivot_sn{};         //   and that node's record (mode, ns, nu) in the schedule that flagged it
   bool trsm_gemm = true;      // GEMM-form triangular solves of the blocked fronts
   bool trsm_gemm64_only = false;   // SMLU_TRSM_GEMM=2: only for diagonal-tile (nb = 64) fronts
   int64_t side_wg = 0;        // grid cap of look-ahead GEMMs (SMLU_SIDE_WG; 0 = uncapped)
@@ -511,10 +521,8 @@ struct smlu_handle {
     }
     ev_pool.clear();
     ev_kind.clear();
-    if (hinfo) (void)hipHostFree(hinfo);
-    hinfo = nullptr;
-    if (hsstat) (void)hipHostFree(hsstat);
-    hsstat = nullptr;
+    rb.free();
+    if (ev_caller) (void)hipEventDestroy(ev_caller);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
     if (ev_join) (void)hipEventDestroy(ev_join);
     ev_fork = ev_join = nullptr;
@@ -2227,8 +2235,6 @@ static int build_schedule(smlu_handle* h) {
     HIPCHK(h->sstatus.alloc(1));
     HIPCHK(hipMemsetAsync(h->sstatus.p, 0, sizeof(int32_t), st));
   }
-  if (!h->hsstat) HIPCHK(hipHostMalloc((void**)&h->hsstat, sizeof(int32_t), 0));
-  *h->hsstat = 0;
   if (const char* e = std::getenv("SMLU_SWEEP_SPIN")) h->sweep_spin = std::atoi(e);
   if (h->nranks > 1) max_list = std::max<int64_t>(max_list, dist_slots);
   if (!tinv_patch.empty() || h->nranks > 1) {   // operands in the tile-inverse slots: patch in the buffer address
@@ -2403,9 +2409,7 @@ static int setup_device(smlu_handle* h) {
   const int64_t nnodes = P.nsup + (int64_t)h->lay.blocks.size();
   HIPCHK(h->info.alloc((size_t)std::max<int64_t>(nnodes, 1)));
   HIPCHK(init_kernel_attributes());
-  if (h->hinfo) HIPCHK(hipHostFree(h->hinfo));
-  h->hinfo = nullptr;
-  HIPCHK(hipHostMalloc((void**)&h->hinfo, sizeof(int32_t) * std::max<int64_t>(nnodes, 2), 0));   // >= 2: dominance flags
+  if (!h->rb.p) HIPCHK(h->rb.alloc(8));
   return build_schedule(h);
 }
 
@@ -2592,6 +2596,26 @@ static int factor_segment(smlu_handle* h, Timer& tm, int seg) {
   return enqueue_factor(h, tm, dbg, seg);
 }
 
+// Status words for the host (factor pivot status, dominance flags, sweep timeouts) travel as one
+// 64-byte record written by k_status behind the work on the stream and stamped at both ends with a
+// per-read sequence number; the host takes a copy only when both stamps match and copies again
+// otherwise.  (Observed on the MI355X box: a 1.4 MB device-to-host copy of the per-front info words
+// into pinned memory, issued right after a graph replay, once delivered foreign data -- an array of
+// device pointers -- which read as a weak pivot in every front and forced a re-pivoting refactor;
+// nothing in a factorization's status is taken on trust since.)
+static int read_status(smlu_handle* h, const int32_t* info, int64_t nnodes, const int32_t* words, int nwords,
+                       long long out[8]) {
+  hipStream_t st = h->stream;
+  const long long seq = ++h->rb_seq;
+  HIPCHK(launch_status(st, info, nnodes, words, nwords, h->rb.p, seq));
+  HIPCHK(hipStreamSynchronize(st));
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    HIPCHK(hipMemcpy(out, h->rb.p, 8 * sizeof(long long), hipMemcpyDeviceToHost));
+    if (out[0] == seq && out[7] == seq) return SMLU_OK;
+  }
+  return fail(h, SMLU_ERR_HIP, "status record read back with a wrong sequence stamp (device-to-host copy)");
+}
+
 // After the last segment: pivot status of this rank's fronts.
 static int finish_factor(smlu_handle* h, Timer& tm, std::chrono::steady_clock::time_point t0) {
   Plan& P = h->plan;
@@ -2600,25 +2624,25 @@ static int finish_factor(smlu_handle* h, Timer& tm, std::chrono::steady_clock::t
     HIPCHK(launch_diag_inv(st, false, h->ninv, h->invfront.p, h->invbase.p, h->sn.p, h->store.p, h->dinvbuf.p));
     HIPCHK(launch_diag_inv(st, true, h->ninv, h->invfront.p, h->invbase.p, h->sn.p, h->store.p, h->dinvbuf.p));
   }
-  HIPCHK(hipMemcpyAsync(h->hinfo, h->info.p, sizeof(int32_t) * h->nnodes, hipMemcpyDeviceToHost, st));
-  double g = 0;
-  HIPCHK(hipMemcpyAsync(&g, h->growth.p, sizeof(double), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  long long rec[8];
+  int rs = read_status(h, h->info.p, h->nnodes, reinterpret_cast<const int32_t*>(h->growth.p), 2, rec);
+  if (rs != SMLU_OK) return rs;
   tm.collect();
   h->refactor_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  double g;
+  std::memcpy(&g, &rec[6], sizeof g);
   h->growth_max = g;
   h->have_numeric = true;
   ++h->nfactor;
-  h->weak = 0;
+  h->weak = rec[1];
   h->errcol = -1;
+  h->flag_node = rec[4];
+  h->flag_info = (int32_t)rec[5];
   int rc = SMLU_OK;
-  for (int64_t s = 0; s < h->nnodes; ++s) {
-    int32_t v = h->hinfo[s];
-    if (v & 2) h->weak++;
-    if ((v & 1) && rc != SMLU_SINGULAR) {
-      rc = SMLU_SINGULAR;
-      h->errcol = P.s_first[h->node_front[s]] + ((v >> 2) > 0 ? (v >> 2) - 1 : 0);
-    }
+  if (rec[2] >= 0) {
+    const int32_t v = (int32_t)rec[3];
+    rc = SMLU_SINGULAR;
+    h->errcol = P.s_first[h->node_front[rec[2]]] + ((v >> 2) > 0 ? (v >> 2) - 1 : 0);
   }
   if (h->nranks > 1) {   // the pivot status of the whole partition, on every rank
     double red[3] = {rc == SMLU_SINGULAR ? 1.0 : 0.0, (double)h->errcol, (double)h->weak};
@@ -2762,6 +2786,10 @@ static int run_factor(smlu_handle* h) {
   const bool off = std::getenv("SMLU_NO_REPIVOT") != nullptr;   // dev/test knob
   if ((rc == SMLU_SINGULAR || h->weak > 0) && h->pivmode == 0 && !off && has_tile_fronts(h) &&
       h->opts.pivot_tol > 0 && !h->plan.given_order && h->nranks == 1) {
+    h->repivot_node = h->flag_node;
+    h->repivot_info = h->flag_info;
+    h->repivot_sn = h->flag_node >= 0 && h->flag_node < (int64_t)h->hsn.size() ? h->hsn[h->flag_node] : SNode{};
+    h->repivot_growth = h->growth_max;
     h->pivmode = 1;
     int r2 = rebuild_schedule(h);
     if (r2 != SMLU_OK) return r2;
@@ -2924,18 +2952,19 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
     int rc = sweeps(steps);
     if (rc != SMLU_OK) return rc;
   }
-  if (check) HIPCHK(hipMemcpyAsync(h->hsstat, h->sstatus.p, sizeof(int32_t), hipMemcpyDeviceToHost, st));
   HIPCHK(finish());
   HIPCHK(tm.end(stop));
   HIPCHK(hipStreamSynchronize(st));
   tm.collect();
   if (check) {
-    double bad = *h->hsstat != 0 ? 1.0 : 0.0;
+    long long rec[8];
+    int rs = read_status(h, nullptr, 0, h->sstatus.p, 1, rec);
+    if (rs != SMLU_OK) return rs;
+    double bad = (rec[6] & 0xffffffffll) != 0 ? 1.0 : 0.0;
     if (h->nranks > 1 && h->tr.allreduce_max(h->tr.ctx, &bad, 1) != 0)
       return fail(h, SMLU_ERR_HIP, "transport allreduce failed (sweep status)");
     if (bad != 0) {
       ++h->sweep_timeouts;
-      *h->hsstat = 0;
       HIPCHK(hipMemsetAsync(h->sstatus.p, 0, sizeof(int32_t), st));
       HIPCHK(load_input(rerun_src, rerun_ld));
       int rc = sweeps(true);
@@ -3141,9 +3170,11 @@ static int device_dominant(smlu_handle* h, bool* dom) {
   int rc = ensure_residual(h);   // the column of every A entry
   if (rc != SMLU_OK) return rc;
   HIPCHK(launch_dominance(st, P.n, h->Acolp.p, h->Arow.p, h->Arowptr.p, h->Arow_ent.p, h->Acol.p, h->A.p,
-                          h->domflag.p, h->hinfo));
-  HIPCHK(hipStreamSynchronize(st));
-  *dom = h->hinfo[0] != 0 || h->hinfo[1] != 0;
+                          h->domflag.p));
+  long long rec[8];
+  rc = read_status(h, nullptr, 0, h->domflag.p, 2, rec);
+  if (rc != SMLU_OK) return rc;
+  *dom = (rec[6] & 0xffffffffll) != 0 || (rec[6] >> 32) != 0;
   return SMLU_OK;
 }
 
@@ -3171,9 +3202,44 @@ int smlu_refactor(smlu_handle* h, const double* nzval) {
   return run_factor(h);   // collective on a partitioned handle
 }
 
+// Device entry points read caller memory (values, right-hand sides) on the handle's own stream:
+// order that stream after the work the caller has enqueued on its stream so far (an event, no
+// host wait).  Outputs are complete when an entry point returns (it synchronises its stream).
+static hipError_t after_caller(smlu_handle* h) {
+  if (!h->ev_caller) {
+    hipError_t e = hipEventCreateWithFlags(&h->ev_caller, hipEventDisableTiming);
+    if (e != hipSuccess) return e;
+  }
+  hipError_t e = hipEventRecord(h->ev_caller, h->caller);
+  return e != hipSuccess ? e : hipStreamWaitEvent(h->stream, h->ev_caller, 0);
+}
+
+// Dev (tools/determinism.py, not in smlu.h): per supernode of a one-GPU handle, a hash of its
+// factor values and one of its row permutation, out[2s], out[2s+1] (2 * nsuper entries).
+int smlu_dev_front_hash(smlu_handle* h, unsigned long long* out) {
+  if (!h || !out) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  if (h->nranks > 1) return fail(h, SMLU_ERR_STATE, "one-GPU handles only");
+  const int64_t ns = h->plan.nsup;
+  DBuf<unsigned long long> d;
+  HIPCHK(d.alloc((size_t)std::max<int64_t>(2 * ns, 1)));
+  HIPCHK(launch_front_hash(h->stream, ns, h->sn.p, h->store.p, h->rowperm.p, d.p));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  hipError_t e = hipMemcpy(out, d.p, sizeof(unsigned long long) * 2 * ns, hipMemcpyDeviceToHost);
+  d.free();
+  HIPCHK(e);
+  return SMLU_OK;
+}
+
+int smlu_set_stream(smlu_handle* h, void* stream) {
+  if (!h) return fail(h, SMLU_ERR_ARG, "NULL handle");
+  h->caller = reinterpret_cast<hipStream_t>(stream);
+  return SMLU_OK;
+}
+
 int smlu_refactor_device(smlu_handle* h, const double* d_nzval) {
   if (!h || !d_nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
   HIPCHK(hipSetDevice(h->device));
+  HIPCHK(after_caller(h));
   if (d_nzval != h->A.p)
     HIPCHK(hipMemcpyAsync(h->A.p, d_nzval, sizeof(double) * h->plan.nnzA, hipMemcpyDeviceToDevice, h->stream));
   return refactor_resident(h);
@@ -3365,6 +3431,7 @@ int smlu_refactor_z_device(smlu_handle* h, const double* d_nzval) {
   if (!h->zc) return fail(h, SMLU_ERR_ARG, "not a complex handle (smlu_create_z)");
   if (reinterpret_cast<uintptr_t>(d_nzval) % 16) return fail(h, SMLU_ERR_ARG, "complex values must be 16-byte aligned");
   HIPCHK(hipSetDevice(h->device));
+  HIPCHK(after_caller(h));
   if (!h->d_zdst.p) {
     HIPCHK(h->d_zdst.upload(h->zdst.data(), h->zdst.size(), h->stream));
     HIPCHK(h->d_zoff.upload(h->zoff.data(), h->zoff.size(), h->stream));
@@ -3454,9 +3521,11 @@ static int solve_refined(smlu_handle* h, const double* db, double* dx) {
     HIPCHK(hipMemsetAsync(h->ref_nrm.p, 0, sizeof(double), st));
     HIPCHK(launch_residual(st, n, h->Arowptr.p, h->Arow_ent.p, h->Acol.p, h->A.p, dx, h->ref_b.p, h->ref_r.p,
                            h->ref_nrm.p));
-    double nrm = 0;
-    HIPCHK(hipMemcpyAsync(&nrm, h->ref_nrm.p, sizeof(double), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    long long rec[8];
+    rc = read_status(h, nullptr, 0, reinterpret_cast<const int32_t*>(h->ref_nrm.p), 2, rec);
+    if (rc != SMLU_OK) return rc;
+    double nrm;
+    std::memcpy(&nrm, &rec[6], sizeof nrm);
     h->refine_resid = nrm;
     if (nrm == 0.0 || nrm > 0.5 * prev) break;
     prev = nrm;
@@ -3473,15 +3542,18 @@ static int solve_refined(smlu_handle* h, const double* db, double* dx) {
 int smlu_residual_device(smlu_handle* h, const double* d_x, const double* d_b, double* d_r, double* nrm) {
   if (!h || !d_x || !d_b || !d_r) return fail(h, SMLU_ERR_ARG, "NULL argument");
   HIPCHK(hipSetDevice(h->device));
+  HIPCHK(after_caller(h));
   int rc = ensure_residual(h);
   if (rc != SMLU_OK) return rc;
   hipStream_t st = h->stream;
   HIPCHK(hipMemsetAsync(h->ref_nrm.p, 0, sizeof(double), st));
   HIPCHK(launch_residual(st, h->plan.n, h->Arowptr.p, h->Arow_ent.p, h->Acol.p, h->A.p, d_x, d_b, d_r,
                          h->ref_nrm.p));
-  double v = 0;
-  HIPCHK(hipMemcpyAsync(&v, h->ref_nrm.p, sizeof(double), hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  long long rec[8];
+  rc = read_status(h, nullptr, 0, reinterpret_cast<const int32_t*>(h->ref_nrm.p), 2, rec);
+  if (rc != SMLU_OK) return rc;
+  double v;
+  std::memcpy(&v, &rec[6], sizeof v);
   if (nrm) *nrm = v;
   return SMLU_OK;
 }
@@ -3490,6 +3562,7 @@ int smlu_solve_device(smlu_handle* h, const double* d_b, double* d_x) {
   if (!h || !d_b || !d_x) return fail(h, SMLU_ERR_ARG, "NULL argument");
   if (!h->have_numeric) return fail(h, SMLU_ERR_STATE, "no numeric factorization");
   HIPCHK(hipSetDevice(h->device));
+  HIPCHK(after_caller(h));
   return solve_refined(h, d_b, d_x);
 }
 
@@ -3541,6 +3614,7 @@ int smlu_solve_multi_device(smlu_handle* h, int64_t nrhs, const double* d_B, int
   const int64_t n = h->plan.n;
   if (ldb < n || ldx < n) return fail(h, SMLU_ERR_ARG, "leading dimension smaller than n");
   HIPCHK(hipSetDevice(h->device));
+  HIPCHK(after_caller(h));
   return solve_multi_dev(h, nrhs, d_B, ldb, d_X, ldx);
 }
 
@@ -4094,6 +4168,7 @@ int smlu_chunked_ldiv_device(smlu_handle* h, const double* d_b, double* d_x) {
     if (rc != SMLU_OK) return rc;
   }
   HIPCHK(hipSetDevice(h->device));
+  HIPCHK(after_caller(h));
   hipStream_t st = h->stream;
   const int64_t n = h->plan.n;
   double* w = h->wrk.p;
@@ -4182,6 +4257,14 @@ double smlu_stat(const smlu_handle* h, const char* key) {
     return c;
   }
   if (k == "repivots") return (double)h->repivots;
+  if (k == "repivot_node") return (double)h->repivot_node;
+  if (k == "repivot_info") return (double)h->repivot_info;
+  if (k == "repivot_growth") return h->repivot_growth;
+  if (k == "repivot_node_mode" || k == "repivot_node_ns" || k == "repivot_node_nu") {
+    if (h->repivot_node < 0) return -1;
+    const SNode& r = h->repivot_sn;
+    return k == "repivot_node_mode" ? r.mode : k == "repivot_node_ns" ? r.ns : r.nu;
+  }
   if (k == "pivot_tol") return h->opts.pivot_tol;
   if (k == "diag_pivot_tol") return h->plan.given_order ? 0.0 : h->opts.diag_pivot_tol;
   if (k == "sweep_timeouts") {   // solves re-run on the per-block schedule after a sweep wait timed out

@@ -61,6 +61,7 @@ SIGNATURES = {
                                       ctypes.POINTER(vp)]),
     "smlu_refactor": (i32, [vp, vp]),
     "smlu_refactor_device": (i32, [vp, vp]),
+    "smlu_set_stream": (i32, [vp, vp]),
     "smlu_refactor_csc": (i32, [vp, i64, vp, vp, vp]),
     "smlu_solve": (i32, [vp, vp, vp]),
     "smlu_solve_device": (i32, [vp, vp, vp]),
@@ -163,6 +164,17 @@ def ptr(a):
     if a is None:
         return None
     return ctypes.c_void_p(a.ctypes.data)
+
+
+def order_after_caller(h, t):
+    """Point the handle's device entry points at the stream that produced tensor `t` (torch's
+    current stream on t's device), so the library's reads of t wait for that work
+    (smlu_set_stream).  Raw pointers keep the previous setting (the null stream by default)."""
+    if h is None or not hasattr(t, "is_cuda") or not t.is_cuda:
+        return
+    import torch
+    s = torch.cuda.current_stream(t.device).cuda_stream
+    lib().smlu_set_stream(h, ctypes.c_void_p(s))
 
 
 def last_error(h=None) -> str:

@@ -32,6 +32,7 @@ def main():
     base = torch.from_numpy(np.ascontiguousarray(A.data)).to(dev)
     vals = torch.empty_like(base)
     g = torch.Generator(device=dev)
+    print("pointers: vals", hex(vals.data_ptr()), "base", hex(base.data_ptr()), "dpos", hex(dpos.data_ptr()), flush=True)
     for r in range(12):
         g.manual_seed(47 + r)
         vals.copy_(base)
@@ -40,6 +41,8 @@ def main():
         rp0 = F.stat("repivots")
         F.refactor_device(vals)
         print(f"r={r} repivots {F.stat('repivots')} pivmode {F.stat('pivmode')} weak {F.stat('weak')} "
+              f"trigger node {F.stat('repivot_node')} info {F.stat('repivot_info')} mode {F.stat('repivot_node_mode')} "
+              f"ns {F.stat('repivot_node_ns')} nu {F.stat('repivot_node_nu')} g {F.stat('repivot_growth'):.3g} "
               f"growth {F.stat('growth_max'):.3g}", flush=True)
         if F.stat("repivots") > rp0:
             vh = vals.cpu().numpy()
