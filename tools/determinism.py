@@ -14,8 +14,10 @@ import numpy as np  # noqa: E402
 
 
 def main():
+    import ctypes
     import torch
     import smlu
+    import smlu._lib as C
     from smlu import matrices as mats
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 128
     A = mats.poisson3d(N)
@@ -26,6 +28,55 @@ def main():
     base = torch.from_numpy(np.ascontiguousarray(A.data)).to(dev)
     b = torch.from_numpy(np.random.default_rng(5).random(n)).to(dev)
     x = torch.empty_like(b)
+    fn = C.lib().smlu_dev_front_hash
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    nsup = int(F.stat("nsuper"))
+
+    def hashes():
+        out = np.zeros(2 * nsup, np.uint64)
+        assert fn(F._h, out.ctypes.data) == 0
+        return out.reshape(nsup, 2)
+
+    fr = F.fronts()
+    first, parent, rowptr, fmode = fr["first"], fr["parent"], fr["rowptr"], fr["mode"]
+    ns_, nu_ = np.diff(first), np.diff(rowptr)
+    height = np.zeros(nsup, np.int64)
+    for s in range(nsup):
+        if parent[s] >= 0:
+            height[parent[s]] = max(height[parent[s]], height[s] + 1)
+    fv = C.lib().smlu_dev_front_values
+    fv.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    fv.restype = ctypes.c_int
+
+    def values(s):
+        M = ns_[s] + nu_[s]
+        out = np.empty(M * ns_[s] + ns_[s] * nu_[s])
+        assert fv(F._h, int(s), out.ctypes.data) == 0
+        return out
+
+    def diff_front(s0, va, vb):
+        """Values of front s0 after refactoring va twice in a row vs after vb then va."""
+        F.refactor_device(va)
+        F.refactor_device(va)
+        a1 = values(s0)
+        F.refactor_device(vb)
+        F.refactor_device(va)
+        a2 = values(s0)
+        M, ns, nu = int(ns_[s0] + nu_[s0]), int(ns_[s0]), int(nu_[s0])
+        d = np.nonzero(a1 != a2)[0]
+        print(f"   front {s0} (M {M}, ns {ns}, nu {nu}): {d.size} of {a1.size} entries depend on the previous values", flush=True)
+        if d.size == 0:
+            return
+        lp = d[d < M * ns]
+        up = d[d >= M * ns] - M * ns
+        rows, cols = lp % M, lp // M
+        reg = {"L11/U11": int(((rows < ns)).sum()), "L21": int((rows >= ns).sum()), "U12": int(up.size)}
+        rel = np.abs(a1[d] - a2[d]) / np.maximum(np.abs(a1[d]), 1e-300)
+        print(f"   regions {reg}; max rel diff {rel.max():.3g}; L-panel cols {np.unique(cols)[:12]} rows {np.unique(rows)[:12]}; "
+              f"U12 rows {np.unique(up % max(ns, 1))[:12]} cols {np.unique(up // max(ns, 1))[:12]}", flush=True)
+
+    hs = {}
     xs = []
     # first graph launch (the refactor right after create captures the graph) vs the second
     v = base.clone()
@@ -42,6 +93,7 @@ def main():
         v[dpos] += torch.from_numpy(np.random.default_rng(47 + r).random(n)).to(dev)
         F.refactor_device(v)
         F.solve_device(x, b)
+        hs[r] = hashes()
         x1 = x.clone()
         F.solve_device(x, b)
         d = (x - x1).abs().max().item()
@@ -53,8 +105,15 @@ def main():
         F.refactor_device(v0)
         F.solve_device(x, b)
         d = (x - x0).abs()
+        h = hashes()
         print(f"refactor v{r} again: max diff {d.max().item():.3g} differing {(d > 0).sum().item()} "
-              f"bitwise {torch.equal(x, x0)}", flush=True)
+              f"bitwise {torch.equal(x, x0)}; fronts with other factor values {(h[:, 0] != hs[r][:, 0]).sum()}, "
+              f"other row perms {(h[:, 1] != hs[r][:, 1]).sum()}", flush=True)
+        dv = np.nonzero(h[:, 0] != hs[r][:, 0])[0]
+        if dv.size:
+            order = dv[np.lexsort((dv, height[dv]))]
+            print("   lowest differing fronts (s, height, mode, ns, nu):",
+                  [(int(s), int(height[s]), int(fmode[s]), int(ns_[s]), int(nu_[s])) for s in order[:6]], flush=True)
     F.close()
 
 

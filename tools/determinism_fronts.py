@@ -52,12 +52,30 @@ def main():
         v = base.clone()
         v[dpos] += torch.from_numpy(np.random.default_rng(seed).random(n)).to(dev)
         vs.append(v)
-    F.refactor_device(vs[0])
+    b = torch.from_numpy(np.random.default_rng(5).random(n)).to(dev)
+    x = torch.empty_like(b)
+    solve = len(sys.argv) > 3 and sys.argv[3] == "solve"   # a solve after every refactor
+
+    def refactor(v):
+        F.refactor_device(v)
+        if solve:
+            h1 = hashes()
+            F.solve_device(x, b)
+            h2 = hashes()
+            if not np.array_equal(h1, h2):
+                print("   the solve changed factor values of", int((h1[:, 0] != h2[:, 0]).sum()), "fronts", flush=True)
+            return x.clone()
+        return None
+
+    x0 = refactor(vs[0])
     H0 = hashes()
     for t in range(trials):
-        F.refactor_device(vs[1])
-        F.refactor_device(vs[0])
+        refactor(vs[1])
+        xt = refactor(vs[0])
         H = hashes()
+        if solve:
+            d = (xt - x0).abs()
+            print(f"trial {t}: solution differs in {(d > 0).sum().item()} entries (max {d.max().item():.3g})", flush=True)
         dv = np.nonzero(H[:, 0] != H0[:, 0])[0]
         dp = np.nonzero(H[:, 1] != H0[:, 1])[0]
         print(f"trial {t}: fronts with different values {dv.size}, different row permutations {dp.size}", flush=True)

@@ -1,6 +1,6 @@
 # Round profile (via gpurun from the repo root): rocprofv3 kernel stats of the bench, then the
 # PMC passes (FETCH_SIZE, WRITE_SIZE, one counter per pass) over the k_gemm* dispatches and over
-# every kernel of one eager factorization.  bash tools/profile_r3.sh N
+# every kernel of one eager factorization.  bash tools/profile_round.sh N
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 N=${1:-128}
