@@ -696,10 +696,7 @@ void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step, const SNod
 //  * block b is published by writing its 64 x NR solved values into its hand-off slot (atomic swaps)
 //    and then setting flag[b] to the epoch (atomic max) behind the wave's vmcnt drain and a barrier;
 //  * a consumer polls flag[b] (atomic compare-and-swap that never matches) until it reaches the epoch
-//    and reads the slot the same way on the raw bits.  The waits are bounded: a wait that gives up
-//    raises *status, which the host reads after every solve and then re-runs the solve on the
-//    per-block schedule (smlu.cpp: run_solve_dev), so a timed-out chunk's values are never returned;
-//    spin <= 0 reports every wait as timed out (the tests' forced-fallback knob SMLU_SWEEP_SPIN=0).
+//    and reads the slot the same way on the raw bits.
 // Deadlock-free: items are taken in ticket order and an item only waits on items of lower tickets
 // (earlier chunks of the same front), which are running.  Per right-hand side the arithmetic does
 // not depend on the batch width (a batched column is bitwise the single solve).
@@ -724,6 +721,28 @@ __device__ __forceinline__ void atomic_write_f64(double* p, double v) {
   (void)__hip_atomic_exchange(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v),
                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Bounded wait for flag f to reach the epoch.  A wait that gives up raises *status; the host reads
+// it after every solve and re-runs the solve on the per-block schedule (smlu.cpp: run_solve_dev), so
+// a timed-out chunk's values are never returned.  spin <= 0 reports every wait as timed out (the
+// tests' forced-fallback knob SMLU_SWEEP_SPIN=0).
+__device__ __forceinline__ void sweep_wait(int32_t* f, int32_t epoch, int32_t* status, int spin) {
+  if (threadIdx.x == 0) {
+    if (spin <= 0) {
+      (void)__hip_atomic_fetch_max(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      int n = 0;
+      while (atomic_read_i32(f) < epoch) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++n > spin) {
+          (void)__hip_atomic_fetch_max(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // Dev instrumentation (tools/sweep_trace.py): one launch shape (grid, direction) records per work item
 // and wave the 100 MHz real-time clock at its start, after its external blocks, before and after its
 // own substitution, after publishing, and at its end.  Compiled in with -DSMLU_SWEEP_TRACE only
@@ -750,9 +769,7 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
                  const SNode* __restrict__ sn, const double* __restrict__ store, double* __restrict__ x,
                  double* __restrict__ vbuf, Rhs rh, int spin, DiagInv di) {
   __shared__ double xs[64][NR];
-  __shared__ double xb[kSweepXB * 64];   // x of a run of external blocks, [block][row][rhs]
   __shared__ unsigned long long s_ticket;
-  __shared__ int s_run;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid == 0) s_ticket = __hip_atomic_fetch_add(tick, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
@@ -814,76 +831,25 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
       if (r < nr) o[r] -= dot64_split(d, bw, [&](int j) { return xs[j][r]; });
   };
   // external blocks (solved by earlier chunks): forward 0 .. min(4q, nblk)-1, backward nblk-1
-  // down to nblk-4q; every row of this chunk lies beyond them.  Taken in runs: wave 0 polls the
-  // flags of up to kSweepXB / NR blocks at once (one lane per flag) and takes the published prefix,
-  // the workgroup reads the run's hand-off slots together, then applies the run's blocks in order
-  // (tile loads only) -- two memory-side round trips per run instead of two per block, so a chunk
-  // that fell behind the chain catches up at the tile-load rate; at the chain's front a run is one
-  // block.  The next run's first tile is loaded before its poll.
+  // down to nblk-4q; every row of this chunk lies beyond them
   const int64_t next = min<int64_t>(4 * q, nblk);
-  auto ext_blk = [&](int64_t e) { return UPPER ? nblk - 1 - e : e; };
-  auto ext_bw = [&](int64_t e) { return (int)min<int64_t>(64, ns - 64 * ext_blk(e)); };
-  if (has && next > 0) load_tile(ext_blk(0), ext_bw(0));
-  for (int64_t e = 0; e < next;) {
-    if (wv == 0) {
-      const int cand = (int)min<int64_t>(kSweepXB / NR, next - e);
-      int run = cand;
-      if (spin <= 0) {   // forced timeout (tests): report, take the run as it is
-        if (lane == 0) (void)__hip_atomic_fetch_max(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        for (int n = 0;; ++n) {
-          const bool ok = lane >= cand || atomic_read_i32(flags + ext_blk(e + lane)) >= epoch;
-          const unsigned long long late = __ballot(!ok);
-          run = late ? __builtin_ctzll(late) : cand;
-          if (run > 0) break;
-          if (n >= spin) {   // give up: the host re-runs the solve on the per-block schedule
-            if (lane == 0) (void)__hip_atomic_fetch_max(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            run = cand;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      if (lane == 0) s_run = run;
-    }
+  for (int64_t e = 0; e < next; ++e) {
+    const int64_t c = UPPER ? nblk - 1 - e : e;
+    const int bw = (int)min<int64_t>(64, ns - 64 * c);
+    if (has) load_tile(c, bw);
+    sweep_wait(flags + c, epoch, status, spin);
+    if (wv == 0)
+      for (int r = 0; r < min(nr, NR); ++r) xs[lane][r] = atomic_read_f64(xhf + (c * kMultiRhs + r) * 64 + lane);
     __syncthreads();
-    const int run = s_run;
-    for (int k = tid; k < run * NR * 64; k += 256) {
-      const int u = k / (NR * 64), r = (k / 64) % NR, l = k % 64;
-      if (r < nr) xb[(u * 64 + l) * NR + r] = atomic_read_f64(xhf + (ext_blk(e + u) * kMultiRhs + r) * 64 + l);
-    }
+    if (has) fma_tile(bw);
     __syncthreads();
-    for (int u = 0; u < run; ++u) {
-      const int bw = ext_bw(e + u);
-      if (u > 0 && has) load_tile(ext_blk(e + u), bw);
-      if (has) {
-#pragma unroll
-        for (int r = 0; r < NR; ++r)
-          if (r < nr) o[r] -= dot64_split(d, bw, [&](int j) { return xb[(u * 64 + j) * NR + r]; });
-      }
-    }
-    e += run;
-    if (has && e < next) load_tile(ext_blk(e), ext_bw(e));
-    __syncthreads();   // the run's slots are read before the next run overwrites them
   }
   sweep_mark(UPPER, item, wv, 1);
-  // internal blocks: wave t solves block b and publishes it, the waves beyond apply it.  Publishing
-  // = raising flag[b] once the wave's slot writes have completed (s_waitcnt vmcnt(0): every lane's
-  // atomics).  The chunk's last block is raised at once (the next chunk waits on it); an earlier
-  // block by its wave at the top of the next step, while the next wave substitutes -- the write
-  // round trip then holds no workgroup barrier (waiting right after the solve made the barrier
-  // behind the other waves' apply wait for it, ~3 us per block).
-  const int nint = (int)max<int64_t>(0, min<int64_t>(4, nblk - 4 * q));
-  auto publish = [&](int t) {
+  // internal blocks: wave t solves block b and publishes it, the waves beyond apply it
+  for (int t = 0; t < 4; ++t) {
     const int64_t b = UPPER ? nblk - 1 - 4 * q - t : 4 * q + t;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) (void)__hip_atomic_fetch_max(flags + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lane == 0) sweep_mark(UPPER, item, t, 4);
-  };
-  for (int t = 0; t < nint; ++t) {
-    const int64_t b = UPPER ? nblk - 1 - 4 * q - t : 4 * q + t;
+    if (b < 0 || b >= nblk) break;
     const int bw = (int)min<int64_t>(64, ns - 64 * b);
-    if (t > 0 && wv == t - 1) publish(t - 1);
     // rows that apply block b: the waves beyond t, and the update rows of wave t when block b is
     // the last, partial one (forward): same per-block arithmetic as every other row
     const bool applies = has && (wv > t || (wv == t && myblk >= nblk));
@@ -907,7 +873,14 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
       sweep_mark(UPPER, item, wv, 3);
     }
     __syncthreads();   // xs (LDS) visible to the waves that apply block b
-    if (t == nint - 1 && wv == t) publish(t);
+    if (wv == t) {
+      // publish: raise the flag once this wave's slot writes have completed (vmcnt counts every
+      // lane's atomics of the wave); the other waves apply the block meanwhile, so the write
+      // round trip is off the chunk's own chain
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) (void)__hip_atomic_fetch_max(flags + b, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) sweep_mark(UPPER, item, t, 4);
+    }
     if (applies) fma_tile(bw);
     __syncthreads();
   }

@@ -3230,6 +3230,48 @@ int smlu_dev_front_hash(smlu_handle* h, unsigned long long* out) {
   return SMLU_OK;
 }
 
+// Dev (tools/determinism.py, not in smlu.h): the factor values of supernode s as stored, L panel
+// (M x ns, ld M) then U12 (ns x nu, ld ns); out holds M*ns + ns*nu doubles.
+int smlu_dev_front_values(smlu_handle* h, int64_t s, double* out) {
+  if (!h || !out || s < 0 || s >= h->plan.nsup) return fail(h, SMLU_ERR_ARG, "invalid arguments");
+  if (h->nranks > 1) return fail(h, SMLU_ERR_STATE, "one-GPU handles only");
+  const SNode& r = h->hsn[s];
+  const int64_t M = (int64_t)r.ns + r.nu;
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(out, h->store.p + r.Loff, sizeof(double) * M * r.ns, hipMemcpyDeviceToHost));
+  if (r.nu > 0)
+    HIPCHK(hipMemcpy(out + M * r.ns, h->store.p + r.Uoff, sizeof(double) * r.ns * r.nu, hipMemcpyDeviceToHost));
+  return SMLU_OK;
+}
+
+// Dev (tools/determinism.py, not in smlu.h): doubles [off, off+cnt) of the factor store (which 0)
+// or of the front scratch (which 1) to host memory; cnt < 0 returns the buffer's length in *len.
+int smlu_dev_copy(smlu_handle* h, int which, int64_t off, int64_t cnt, double* out, int64_t* len) {
+  if (!h || which < 0 || which > 1) return fail(h, SMLU_ERR_ARG, "invalid arguments");
+  const DBuf<double>& b = which == 0 ? h->store : h->scratch;
+  if (cnt < 0) {
+    if (len) *len = (int64_t)b.n;
+    return SMLU_OK;
+  }
+  if (!out || off < 0 || off + cnt > (int64_t)b.n) return fail(h, SMLU_ERR_ARG, "range outside the buffer");
+  HIPCHK(hipStreamSynchronize(h->stream));
+  HIPCHK(hipMemcpy(out, b.p + off, sizeof(double) * cnt, hipMemcpyDeviceToHost));
+  return SMLU_OK;
+}
+
+// Dev (not in smlu.h): per supernode Loff, Uoff, Foff (-1: no F22) and M, 4 * nsuper entries.
+int smlu_dev_front_offsets(smlu_handle* h, int64_t* out) {
+  if (!h || !out) return fail(h, SMLU_ERR_ARG, "NULL argument");
+  for (int64_t s = 0; s < h->plan.nsup; ++s) {
+    const SNode& r = h->hsn[s];
+    out[4 * s] = r.Loff;
+    out[4 * s + 1] = r.Uoff;
+    out[4 * s + 2] = r.Foff;
+    out[4 * s + 3] = (int64_t)r.ns + r.nu;
+  }
+  return SMLU_OK;
+}
+
 int smlu_set_stream(smlu_handle* h, void* stream) {
   if (!h) return fail(h, SMLU_ERR_ARG, "NULL handle");
   h->caller = reinterpret_cast<hipStream_t>(stream);

@@ -44,18 +44,23 @@ def main():
     off = off.reshape(nsup, 4)
     watch = [s for s in range(nsup) if hmin <= height[s] <= hmax]
 
-    def grab(which, o, cnt):
-        out = np.empty(cnt)
-        if cnt:
-            assert L.smlu_dev_copy(F._h, which, int(o), int(cnt), out.ctypes.data, None) == 0
+    def whole(which):
+        n = ctypes.c_int64()
+        assert L.smlu_dev_copy(F._h, which, 0, -1, None, ctypes.byref(n)) == 0
+        out = np.empty(n.value)
+        step = 1 << 27
+        for o in range(0, n.value, step):
+            c = min(step, n.value - o)
+            assert L.smlu_dev_copy(F._h, which, o, c, out[o:].ctypes.data, None) == 0
         return out
 
     def snapshot():
+        st, sc = whole(0), whole(1)
         snap = {}
         for s in watch:
             M, ns, nu = int(off[s, 3]), int(ns_[s]), int(nu_[s])
-            lu = np.concatenate([grab(0, off[s, 0], M * ns), grab(0, off[s, 1], ns * nu) if nu else np.empty(0)])
-            f22 = grab(1, off[s, 2], nu * nu) if off[s, 2] >= 0 and nu else np.empty(0)
+            lu = np.concatenate([st[off[s, 0]:off[s, 0] + M * ns], st[off[s, 1]:off[s, 1] + ns * nu] if nu else np.empty(0)])
+            f22 = sc[off[s, 2]:off[s, 2] + nu * nu] if off[s, 2] >= 0 and nu else np.empty(0)
             snap[s] = (lu, f22)
         return snap
 
