@@ -35,6 +35,16 @@ __global__ void k_fill(int64_t n, double* __restrict__ x, double v) {
   if (i < n) x[i] = v;
 }
 
+// Start of a factorization: info words and the growth maximum cleared, the local row permutation
+// reset to the identity (rowperm = rowperm0) -- one kernel instead of memset / memcpy graph nodes.
+__global__ void k_factor_reset(int64_t nnodes, int32_t* __restrict__ info, double* __restrict__ growth, int64_t n,
+                               int32_t* __restrict__ rowperm, const int32_t* __restrict__ rowperm0) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nnodes) info[i] = 0;
+  if (i < n) rowperm[i] = rowperm0[i];
+  if (i == 0) growth[0] = 0.0;
+}
+
 // ------------------------------------------------------------------------------------
 // Front assembly (one wave per front column, one launch per level): the column is built in
 // 256-row chunks in LDS -- zeros, then the scaled A entries (plain stores: every entry owns
@@ -1494,6 +1504,12 @@ hipError_t launch_rowscale(hipStream_t st, int64_t n, const int64_t* rowptr, con
                            const double* a, double* Rs) {
   if (n <= 0) return hipSuccess;
   k_rowscale<<<nblk(n, 256), 256, 0, st>>>(n, rowptr, ent, a, Rs);
+  return hipGetLastError();
+}
+hipError_t launch_factor_reset(hipStream_t st, int64_t nnodes, int32_t* info, double* growth, int64_t n,
+                               int32_t* rowperm, const int32_t* rowperm0) {
+  const int64_t m = nnodes > n ? nnodes : (n > 1 ? n : 1);
+  k_factor_reset<<<nblk(m, 256), 256, 0, st>>>(nnodes, info, growth, n, rowperm, rowperm0);
   return hipGetLastError();
 }
 hipError_t launch_fill(hipStream_t st, int64_t n, double* x, double v) {

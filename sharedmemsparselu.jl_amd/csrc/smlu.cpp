@@ -32,6 +32,7 @@
 namespace smlu {
 hipError_t launch_rowscale(hipStream_t, int64_t, const int64_t*, const int32_t*, const double*, double*);
 hipError_t launch_fill(hipStream_t, int64_t, double*, double);
+hipError_t launch_factor_reset(hipStream_t, int64_t, int32_t*, double*, int64_t, int32_t*, const int32_t*);
 hipError_t launch_assemble(hipStream_t, int64_t, const XCol*, const XContrib*, const int2*, const SNode*,
                            const int32_t*, const double*, const int32_t*, const double*, double*, double*);
 hipError_t launch_front_small(hipStream_t, int, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
@@ -2525,10 +2526,9 @@ static int enqueue_factor(smlu_handle* h, Timer& tm, bool dbg, int seg) {
   double diag_tol = P.given_order ? 0.0 : h->opts.diag_pivot_tol;
   double piv_tol = h->opts.pivot_tol;
   if (seg > 0) goto launches;
-  HIPCHK(hipMemsetAsync(h->info.p, 0, sizeof(int32_t) * std::max<int64_t>(h->nnodes, 1), st));
-  HIPCHK(hipMemsetAsync(h->growth.p, 0, sizeof(double), st));
-  // identity (local) row permutation; fronts overwrite their part
-  HIPCHK(hipMemcpyAsync(h->rowperm.p, h->rowperm0.p, sizeof(int32_t) * P.n, hipMemcpyDeviceToDevice, st));
+  // info words and growth cleared, identity (local) row permutation (fronts overwrite their part):
+  // one kernel, so that the captured graph holds kernel nodes only
+  HIPCHK(launch_factor_reset(st, h->nnodes, h->info.p, h->growth.p, P.n, h->rowperm.p, h->rowperm0.p));
   if (!h->given_Rs) {
     if (h->opts.scale) HIPCHK(launch_rowscale(st, P.n, h->Arowptr.p, h->Arow_ent.p, h->A.p, h->Rs.p));
     else HIPCHK(launch_fill(st, P.n, h->Rs.p, 1.0));

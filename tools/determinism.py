@@ -99,7 +99,9 @@ def main():
         (None if nosolve else F.solve_device(x, b))
         d = (x - x1).abs().max().item()
         print(f"r={r} solve twice: max diff {d:.3g} bitwise {torch.equal(x, x1)} weak {F.stat('weak')} "
-              f"timeouts {F.stat('sweep_timeouts')} refine_steps {F.stat('refine_steps')}", flush=True)
+              f"timeouts {F.stat('sweep_timeouts')} refine_steps {F.stat('refine_steps')} repivots {F.stat('repivots')} "
+              f"(last trigger node {F.stat('repivot_node')} info {F.stat('repivot_info')} mode {F.stat('repivot_node_mode')})",
+              flush=True)
         xs.append((v, x.clone()))
     for r in (0, 1):
         v0, x0 = xs[r]
@@ -108,7 +110,7 @@ def main():
         d = (x - x0).abs()
         h = hashes()
         print(f"refactor v{r} again: max diff {d.max().item():.3g} differing {(d > 0).sum().item()} "
-              f"bitwise {torch.equal(x, x0)}; fronts with other factor values {(h[:, 0] != hs[r][:, 0]).sum()}, "
+              f"bitwise {torch.equal(x, x0)}; repivots {F.stat('repivots')}; fronts with other factor values {(h[:, 0] != hs[r][:, 0]).sum()}, "
               f"other row perms {(h[:, 1] != hs[r][:, 1]).sum()}", flush=True)
         dv = np.nonzero(h[:, 0] != hs[r][:, 0])[0]
         if dv.size:
