@@ -314,6 +314,18 @@ int     smlu_plan_rank_memory(const smlu_plan* plan, int32_t nparts, int32_t ran
 double  smlu_plan_project(const smlu_plan* plan, int32_t nparts, double tflops, double gbs, double lat_us,
                           double* t1);
 
+/* ---- diagnostics (no reference counterpart; tools/determinism*.py) ----------------------
+ * Reads of a one-GPU handle's factorization, for reproducibility checks: per supernode s a hash
+ * of its factor values (L panel + U12 bit patterns) and one of its row permutation,
+ * out[2s], out[2s+1] (2 * nsuper entries); its values as stored (L panel M x ns, ld M, then U12
+ * ns x nu, ld ns); its offsets (Loff, Uoff, Foff (-1: no F22), M; 4 * nsuper entries); and
+ * doubles [off, off+cnt) of the factor store (which 0) or the front scratch (which 1) -- cnt < 0
+ * returns the buffer's length in *len.  Each synchronises the handle's stream first. */
+int smlu_dev_front_hash(smlu_handle* h, unsigned long long* out);
+int smlu_dev_front_values(smlu_handle* h, int64_t s, double* out);
+int smlu_dev_front_offsets(smlu_handle* h, int64_t* out);
+int smlu_dev_copy(smlu_handle* h, int which, int64_t off, int64_t cnt, double* out, int64_t* len);
+
 /* Library version string. */
 const char* smlu_version(void);
 

@@ -62,6 +62,10 @@ SIGNATURES = {
     "smlu_refactor": (i32, [vp, vp]),
     "smlu_refactor_device": (i32, [vp, vp]),
     "smlu_set_stream": (i32, [vp, vp]),
+    "smlu_dev_front_hash": (i32, [vp, vp]),
+    "smlu_dev_front_values": (i32, [vp, i64, vp]),
+    "smlu_dev_front_offsets": (i32, [vp, vp]),
+    "smlu_dev_copy": (i32, [vp, i32, i64, i64, vp, vp]),
     "smlu_refactor_csc": (i32, [vp, i64, vp, vp, vp]),
     "smlu_solve": (i32, [vp, vp, vp]),
     "smlu_solve_device": (i32, [vp, vp, vp]),
