@@ -259,6 +259,59 @@ def timed_region(step, steps, warmup, sync, device=None):
     return max_over_ranks(time.perf_counter() - t0, device)
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def self_launch(n):
+    """`python bench.py --gpus N` (N > 1, no WORLD_SIZE in the environment): run this script under
+    torch.distributed.run with N ranks on this node (127.0.0.1 rendezvous) and return their exit
+    status.  The child launcher is a subprocess; this process never initialises the GPU."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"--gpus {n} without a launcher: starting {n} ranks: {' '.join(cmd[1:6])} ...")
+    return subprocess.call(cmd)
+
+
+def init_gloo():
+    """Control-plane process group (barriers, max-over-ranks timing, the RCCL unique id).  gloo
+    prints its connection banner on the C-level stdout: keep stdout for the JSON line."""
+    import torch.distributed as dist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo")
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+def launch_check(rank, world, local):
+    """The launcher path alone: every rank joins a gloo group and reports itself; rank 0 prints
+    {"launch_check": true, "world": W, "ranks": [...]} (no GPU call)."""
+    import torch.distributed as dist
+    if world > 1:
+        init_gloo()
+    me = {"rank": rank, "local_rank": local, "pid": os.getpid()}
+    allr = [None] * world
+    if world > 1:
+        dist.all_gather_object(allr, me)
+    else:
+        allr = [me]
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "world": world, "ranks": allr}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -274,31 +327,32 @@ def main():
                     help="rehearsal: all ranks on cuda:0, gloo transport (never for measurements)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: independent replicas instead of the partitioned factorization")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher check only: every rank reports (rank, world) over gloo, rank 0 prints "
+                         "one JSON line; no GPU call (tests/test_bench_launch.py)")
     args = ap.parse_args()
 
+    # --gpus N without a launcher: start the N ranks here, before anything touches the GPU, as
+    # child processes of torch.distributed.run (never an exec), and exit with their status.
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     import torch
     import torch.distributed as dist
+    if args.launch_check:
+        sys.exit(launch_check(rank, world, local))
     if args.test_one_gpu:
         local = 0
     if world > 1:
         # control plane (barriers, the max-over-ranks timing, the RCCL unique id) over gloo; the
         # data path is the library's own RCCL communicator (xGMI point-to-point), so a process
         # holds exactly one RCCL instance
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        # gloo prints its connection banner on the C-level stdout: keep stdout for the JSON line
-        sys.stdout.flush()
-        saved = os.dup(1)
-        os.dup2(2, 1)
-        try:
-            dist.init_process_group("gloo")
-        finally:
-            sys.stdout.flush()
-            os.dup2(saved, 1)
-            os.close(saved)
+        init_gloo()
     else:
         torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
@@ -374,6 +428,20 @@ def main():
     xh, bh = x.cpu().numpy(), b.cpu().numpy()
     solve_residual = float(np.abs(Al @ xh - bh).max() / np.abs(bh).max())
     ms_per_step = dt / args.steps * 1e3
+    # per-rank evidence of the partitioned run: the communicator's own rank count and what this rank
+    # moved in its last refactor (gathered to rank 0 over the gloo control plane)
+    me = {"rank": rank, "device": local, "create_s": round(t_create, 3),
+          "refactor_ms_last": F.stat("refactor_ms_last")}
+    if partitioned:
+        me.update({"rccl_nranks": int(F.stat("rccl_nranks")), "comm_steps": int(F.stat("comm_steps")),
+                   "comm_bytes_sent_refactor": F.stat("comm_bytes_sent_refactor"),
+                   "comm_bytes_recv_refactor": F.stat("comm_bytes_recv_refactor"),
+                   "shared_fronts": int(F.stat("shared_fronts")),
+                   "store_bytes_rank": F.stat("store_bytes_rank")})
+    per_rank = [me]
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, me)
 
     if rank == 0:
         K = args.steps
@@ -451,7 +519,10 @@ def main():
             "solve_8rhs_ms": solve8_ms,
             "solve_residual": solve_residual,
             "create_s": t_create,
+            "ranks": per_rank,
         }
+        if partitioned:
+            res["rccl_nranks"] = min(r.get("rccl_nranks", 0) for r in per_rank)
         if not args.no_cpu and world == 1:
             log("ordering comparison (host symbolic analysis) ...")
             res["config"]["ordering_compare"] = ordering_compare(N)

@@ -107,8 +107,10 @@ int smlu_refactor_device(smlu_handle* h, const double* d_nzval);
  * entry point orders its reads of caller memory after the work enqueued on that stream so far
  * (an event wait on the handle's stream, no host synchronisation), and returns with its outputs
  * complete.  Set it to the stream that produces the values / right-hand sides (the Python mirror
- * passes torch's current stream on every device call).  No reference counterpart: Julia's
- * arrays are host memory. */
+ * passes torch's current stream on every device call and resets it to NULL afterwards).
+ * Lifetime: the handle keeps the raw stream until the next smlu_set_stream; the caller must
+ * reset it (NULL) before destroying that stream.  No reference counterpart: Julia's arrays are
+ * host memory. */
 int smlu_set_stream(smlu_handle* h, void* stream);
 
 /* lu!(F, A) where A's pattern may differ: re-analyses when it does (the reference's

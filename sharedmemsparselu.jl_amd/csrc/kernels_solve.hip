@@ -1023,7 +1023,9 @@ __global__ void k_unswap(int64_t n, const int64_t* __restrict__ pos_first,
 
 // ------------------------------------------------------------------------------------
 // Iterative refinement (pivot-failure fallback): r = b - A x by rows of A (entries of a row in
-// column order, deterministic), max |r_i| into *nrm; x += d.
+// column order, deterministic), max |r_i| into nrm[0] and the componentwise backward error
+// max_i |r_i| / (|A| |x| + |b|)_i (Oettli-Prager; LAPACK dgerfs' BERR, a row with a zero
+// denominator and r_i = 0 counts 0) into nrm[1]; x += d.
 // ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_residual(int64_t n, const int64_t* __restrict__ rowptr,
                                                   const int32_t* __restrict__ ent,
@@ -1033,18 +1035,24 @@ __global__ __launch_bounds__(256) void k_residual(int64_t n, const int64_t* __re
                                                   const double* __restrict__ b, double* __restrict__ r,
                                                   double* __restrict__ nrm) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  double ri = 0.0;
+  double ri = 0.0, wi = 0.0;
   if (i < n) {
-    double acc = 0.0;
+    double acc = 0.0, den = 0.0;
     for (int64_t e = rowptr[i]; e < rowptr[i + 1]; ++e) {
       const int32_t k = ent[e];
-      acc = fma(a[k], x[acol[k]], acc);
+      const double xk = x[acol[k]];
+      acc = fma(a[k], xk, acc);
+      den = fma(fabs(a[k]), fabs(xk), den);
     }
     ri = b[i] - acc;
     r[i] = ri;
+    den += fabs(b[i]);
+    wi = ri == 0.0 ? 0.0 : den > 0.0 ? fabs(ri) / den : HUGE_VAL;
   }
   const double m = wave_max(fabs(ri));
+  const double w = wave_max(wi);
   if ((threadIdx.x & 63) == 0 && m > 0.0) atomic_max_pos(nrm, m);
+  if ((threadIdx.x & 63) == 0 && w > 0.0) atomic_max_pos(nrm + 1, w);
 }
 // Diagonal dominance of A's current values in HBM (the device twin of smlu.cpp's host
 // diagonally_dominant(), for smlu_refactor_device): thread i sums |column i| in CSC order and
@@ -1076,38 +1084,54 @@ __global__ __launch_bounds__(256) void k_dominance(int64_t n, const int64_t* __r
   if (!(d > 0.0 && d >= off)) flags[1] = 0;
 }
 // Status record of a factorization / dominance test / solve for the host (smlu.cpp: read_status):
-// out[0] = out[7] = seq (the host accepts a copy only when both match its own sequence number);
+// out[0] = out[15] = seq (the host accepts a copy only when both match its own sequence number);
 // with info: out[1] = weak-pivot nodes, out[2], out[3] = first zero-pivot node and its info word
-// (-1, 0: none), out[4], out[5] = first flagged node and its word; out[6] = words[0] | words[1] << 32.
-// One workgroup of 1024 threads.
+// (-1, 0: none), out[4], out[5] = first flagged node and its word; out[6] = words[0] | words[1] << 32,
+// out[7] = words[2] | words[3] << 32 (up to 4 status words);
+// out[8], out[9] = first node whose info word is outside the legal code set and that word (-1, 0:
+// none), out[10] = how many such nodes.  Legal words are the ones publish_info / the growth epilogues
+// write: bit 0 zero pivot, bit 1 weak pivot, bits 2.. = 1 + the front-local column of the first zero
+// pivot, at most ns (0 <= v < (ns + 1) << 2).  Any other word is not a pivot status and is never
+// read as one (the host fails with SMLU_ERR_STATE).  One workgroup of 1024 threads.
 __global__ __launch_bounds__(1024) void k_status(const int32_t* __restrict__ info, int64_t nnodes,
+                                                 const SNode* __restrict__ sn,
                                                  const int32_t* __restrict__ words, int nwords,
                                                  long long* __restrict__ out, long long seq) {
-  __shared__ long long s_weak[1024];
-  __shared__ long long s_sing[1024], s_flag[1024];
+  __shared__ long long s_weak[1024], s_nbad[1024];
+  __shared__ long long s_sing[1024], s_flag[1024], s_bad[1024];
   const int tid = threadIdx.x;
-  long long weak = 0, sing = LLONG_MAX, flag = LLONG_MAX;
+  long long weak = 0, nbad = 0, sing = LLONG_MAX, flag = LLONG_MAX, bad = LLONG_MAX;
   if (info)
     for (int64_t i = tid; i < nnodes; i += 1024) {
       const int32_t v = info[i];
+      const bool legal = v >= 0 && (!sn || (int64_t)v < (((int64_t)sn[i].ns + 1) << 2));
+      if (!legal) {
+        ++nbad;
+        if (i < bad) bad = i;
+        continue;
+      }
       weak += (v >> 1) & 1;
       if ((v & 1) && i < sing) sing = i;
       if ((v & 3) && i < flag) flag = i;
     }
   s_weak[tid] = weak;
+  s_nbad[tid] = nbad;
   s_sing[tid] = sing;
   s_flag[tid] = flag;
+  s_bad[tid] = bad;
   __syncthreads();
   for (int w = 512; w > 0; w >>= 1) {
     if (tid < w) {
       s_weak[tid] += s_weak[tid + w];
+      s_nbad[tid] += s_nbad[tid + w];
       s_sing[tid] = min(s_sing[tid], s_sing[tid + w]);
       s_flag[tid] = min(s_flag[tid], s_flag[tid + w]);
+      s_bad[tid] = min(s_bad[tid], s_bad[tid + w]);
     }
     __syncthreads();
   }
   if (tid == 0) {
-    const long long sg = s_sing[0], fl = s_flag[0];
+    const long long sg = s_sing[0], fl = s_flag[0], bd = s_bad[0];
     out[1] = s_weak[0];
     out[2] = sg == LLONG_MAX ? -1 : sg;
     out[3] = sg == LLONG_MAX ? 0 : info[sg];
@@ -1115,9 +1139,16 @@ __global__ __launch_bounds__(1024) void k_status(const int32_t* __restrict__ inf
     out[5] = fl == LLONG_MAX ? 0 : info[fl];
     const long long w0 = nwords > 0 ? (long long)(uint32_t)words[0] : 0;
     const long long w1 = nwords > 1 ? (long long)(uint32_t)words[1] : 0;
+    const long long w2 = nwords > 2 ? (long long)(uint32_t)words[2] : 0;
+    const long long w3 = nwords > 3 ? (long long)(uint32_t)words[3] : 0;
     out[6] = w0 | (w1 << 32);
+    out[7] = w2 | (w3 << 32);
+    out[8] = bd == LLONG_MAX ? -1 : bd;
+    out[9] = bd == LLONG_MAX ? 0 : info[bd];
+    out[10] = s_nbad[0];
+    for (int i = 11; i < 15; ++i) out[i] = 0;
     out[0] = seq;
-    out[7] = seq;
+    out[15] = seq;
   }
 }
 // Dev (tools/determinism.py): an order-independent 64-bit hash per front of its factor values
@@ -1317,9 +1348,9 @@ hipError_t launch_front_hash(hipStream_t st, int64_t nsup, const SNode* sn, cons
   k_front_hash<<<(unsigned)nsup, 256, 0, st>>>(sn, store, rowperm, out);
   return hipGetLastError();
 }
-hipError_t launch_status(hipStream_t st, const int32_t* info, int64_t nnodes, const int32_t* words, int nwords,
-                         long long* out, long long seq) {
-  k_status<<<1, 1024, 0, st>>>(info, nnodes, words, nwords, out, seq);
+hipError_t launch_status(hipStream_t st, const int32_t* info, int64_t nnodes, const SNode* sn, const int32_t* words,
+                         int nwords, long long* out, long long seq) {
+  k_status<<<1, 1024, 0, st>>>(info, nnodes, sn, words, nwords, out, seq);
   return hipGetLastError();
 }
 hipError_t launch_axpy1(hipStream_t st, int64_t n, const double* d, double* x) {

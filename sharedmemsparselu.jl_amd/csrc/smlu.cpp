@@ -76,7 +76,7 @@ hipError_t launch_residual(hipStream_t, int64_t, const int64_t*, const int32_t*,
 hipError_t launch_axpy1(hipStream_t, int64_t, const double*, double*);
 hipError_t launch_dominance(hipStream_t, int64_t, const int64_t*, const int32_t*, const int64_t*, const int32_t*,
                             const int32_t*, const double*, int32_t*);
-hipError_t launch_status(hipStream_t, const int32_t*, int64_t, const int32_t*, int, long long*, long long);
+hipError_t launch_status(hipStream_t, const int32_t*, int64_t, const SNode*, const int32_t*, int, long long*, long long);
 hipError_t launch_front_hash(hipStream_t, int64_t, const SNode*, const double*, const int32_t*, unsigned long long*);
 hipError_t launch_expand_z(hipStream_t, int64_t, const double*, const int64_t*, const int32_t*, double*);
 hipError_t launch_perm_in(hipStream_t, int64_t, const int64_t*, const double*, const double*, double*, int,
@@ -202,6 +202,7 @@ struct RcclApi {
   ncclResult_t (*GroupStart)();
   ncclResult_t (*GroupEnd)();
   ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+  ncclResult_t (*CommCount)(const ncclComm_t, int*);
 };
 
 RcclApi* rccl_api() {
@@ -226,6 +227,7 @@ RcclApi* rccl_api() {
   api.GroupStart = (decltype(api.GroupStart))sym("ncclGroupStart");
   api.GroupEnd = (decltype(api.GroupEnd))sym("ncclGroupEnd");
   api.AllReduce = (decltype(api.AllReduce))sym("ncclAllReduce");
+  api.CommCount = (decltype(api.CommCount))sym("ncclCommCount");
   if (!ok) return nullptr;
   api.lib = l;
   return &api;
@@ -273,6 +275,7 @@ constexpr int kRbAtomicsNotAllowed = 0; // rocblas_atomics_not_allowed
 struct RcclState {
   ncclComm_t comm = nullptr;
   int rank = 0;
+  int comm_count = 0;             // ranks in the communicator (ncclCommCount after init)
   hipStream_t stream = nullptr;   // the handle's stream (allreduce)
   double* dbuf = nullptr;         // device scratch for the allreduce
 };
@@ -353,6 +356,7 @@ struct smlu_handle {
   DBuf<int64_t> Acolp;                         // A's colptr (device dominance check)
   DBuf<int32_t> domflag;
   int refine_steps = 0;
+  double refine_berr = -1;   // componentwise backward error at the last refinement check
   double refine_resid = -1;
   DBuf<int64_t> Arowptr, p0, q, posfirst;
   DBuf<int32_t> Arow_ent, Arow, rows, relmap, chlist, ilist, rowperm, rowperm0, info, swaps;
@@ -393,6 +397,9 @@ struct smlu_handle {
   hipEvent_t ev_caller = nullptr;
   DBuf<long long> rb;         // status record for the host (k_status; read_status)
   long long rb_seq = 0;       // sequence number of the last status record
+  int64_t status_copy_retries = 0;   // status records re-read after a stamp mismatch
+  int64_t bad_info_node = -1, bad_info_count = 0;   // illegal info words seen by k_status
+  int32_t bad_info_word = 0;
   int64_t sweep_timeouts = 0;   // solves re-run on the per-block schedule after a sweep wait timed out
   int sweep_spin = 1 << 22;     // polls before a sweep wait gives up (SMLU_SWEEP_SPIN; 0 = always, tests)
   DBuf<double> bstash;          // the solve's input when the final step overwrites it (x === b, lsolve!/rsolve!)
@@ -416,6 +423,9 @@ struct smlu_handle {
   char* hstage_s = nullptr;                        // pinned host staging (host-memory transports)
   char* hstage_r = nullptr;
   int64_t stage_bytes_s = 0, stage_bytes_r = 0;
+  // bytes this rank sent / received through the transport (cumulative, and in the last refactor)
+  double comm_sent = 0, comm_recv = 0, comm_sent_fac = 0, comm_recv_fac = 0;
+  int64_t comm_calls = 0;
   size_t fac_graph_events = 0;
   bool graph_failed = false;
   bool lookahead = false;     // SMLU_LOOKAHEAD=1: trailing updates beyond the next block on a side stream
@@ -2410,7 +2420,7 @@ static int setup_device(smlu_handle* h) {
   const int64_t nnodes = P.nsup + (int64_t)h->lay.blocks.size();
   HIPCHK(h->info.alloc((size_t)std::max<int64_t>(nnodes, 1)));
   HIPCHK(init_kernel_attributes());
-  if (!h->rb.p) HIPCHK(h->rb.alloc(8));
+  if (!h->rb.p) HIPCHK(h->rb.alloc(16));
   return build_schedule(h);
 }
 
@@ -2604,14 +2614,15 @@ static int factor_segment(smlu_handle* h, Timer& tm, int seg) {
 // device pointers -- which read as a weak pivot in every front and forced a re-pivoting refactor;
 // nothing in a factorization's status is taken on trust since.)
 static int read_status(smlu_handle* h, const int32_t* info, int64_t nnodes, const int32_t* words, int nwords,
-                       long long out[8]) {
+                       long long out[16]) {
   hipStream_t st = h->stream;
   const long long seq = ++h->rb_seq;
-  HIPCHK(launch_status(st, info, nnodes, words, nwords, h->rb.p, seq));
+  HIPCHK(launch_status(st, info, nnodes, info ? h->sn.p : nullptr, words, nwords, h->rb.p, seq));
   HIPCHK(hipStreamSynchronize(st));
   for (int attempt = 0; attempt < 4; ++attempt) {
-    HIPCHK(hipMemcpy(out, h->rb.p, 8 * sizeof(long long), hipMemcpyDeviceToHost));
-    if (out[0] == seq && out[7] == seq) return SMLU_OK;
+    HIPCHK(hipMemcpy(out, h->rb.p, 16 * sizeof(long long), hipMemcpyDeviceToHost));
+    if (out[0] == seq && out[15] == seq) return SMLU_OK;
+    ++h->status_copy_retries;   // counted (smlu_stat "status_copy_retries"): the tests require 0
   }
   return fail(h, SMLU_ERR_HIP, "status record read back with a wrong sequence stamp (device-to-host copy)");
 }
@@ -2624,9 +2635,17 @@ static int finish_factor(smlu_handle* h, Timer& tm, std::chrono::steady_clock::t
     HIPCHK(launch_diag_inv(st, false, h->ninv, h->invfront.p, h->invbase.p, h->sn.p, h->store.p, h->dinvbuf.p));
     HIPCHK(launch_diag_inv(st, true, h->ninv, h->invfront.p, h->invbase.p, h->sn.p, h->store.p, h->dinvbuf.p));
   }
-  long long rec[8];
+  long long rec[16];
   int rs = read_status(h, h->info.p, h->nnodes, reinterpret_cast<const int32_t*>(h->growth.p), 2, rec);
   if (rs != SMLU_OK) return rs;
+  if (rec[10] > 0) {   // an info word no factor kernel writes: never read as a pivot status
+    h->bad_info_node = rec[8];
+    h->bad_info_word = (int32_t)rec[9];
+    h->bad_info_count += rec[10];
+    return fail(h, SMLU_ERR_STATE, "factorization status: " + std::to_string(rec[10]) +
+                " front info words outside the legal code set (first: node " + std::to_string(rec[8]) +
+                ", word " + std::to_string(rec[9]) + ")");
+  }
   tm.collect();
   h->refactor_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   double g;
@@ -2708,6 +2727,23 @@ static int exec_comm(smlu_handle* h, int id) {
     }
   }
   if (e != 0) return fail(h, SMLU_ERR_HIP, "transport error " + std::to_string(e) + " in communication step");
+  {   // bytes moved by this rank (bench.py: comm_bytes per rank)
+    double sent = 0, recv = 0;
+    if (op.type == 1) {
+      if (h->rank == op.root) sent = (double)op.bytes * (double)(op.grp.size() - 1);
+      else recv = (double)op.bytes;
+    } else {
+      for (size_t i = 0; i < op.peer.size(); ++i) {
+        sent += (double)op.sbytes[i];
+        recv += (double)op.rbytes[i];
+      }
+    }
+    h->comm_sent += sent;
+    h->comm_recv += recv;
+    h->comm_sent_fac += sent;
+    h->comm_recv_fac += recv;
+    ++h->comm_calls;
+  }
   HIPCHK(launch_segcopy(st, h->segdesc.p + op.unpack0, (int64_t)op.unpack.size()));
   return SMLU_OK;
 }
@@ -2716,6 +2752,7 @@ static int run_factor_once(smlu_handle* h) {
   HIPCHK(hipSetDevice(h->device));
   auto t0 = std::chrono::steady_clock::now();
   for (auto& v : h->kind_ms) v = 0;
+  h->comm_sent_fac = h->comm_recv_fac = 0;
   Timer tm(h);
   for (size_t seg = 0; seg < h->fac_seg.size(); ++seg) {
     if (seg > 0) {
@@ -2957,7 +2994,7 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
   HIPCHK(hipStreamSynchronize(st));
   tm.collect();
   if (check) {
-    long long rec[8];
+    long long rec[16];
     int rs = read_status(h, nullptr, 0, h->sstatus.p, 1, rec);
     if (rs != SMLU_OK) return rs;
     double bad = (rec[6] & 0xffffffffll) != 0 ? 1.0 : 0.0;
@@ -3171,7 +3208,7 @@ static int device_dominant(smlu_handle* h, bool* dom) {
   if (rc != SMLU_OK) return rc;
   HIPCHK(launch_dominance(st, P.n, h->Acolp.p, h->Arow.p, h->Arowptr.p, h->Arow_ent.p, h->Acol.p, h->A.p,
                           h->domflag.p));
-  long long rec[8];
+  long long rec[16];
   rc = read_status(h, nullptr, 0, h->domflag.p, 2, rec);
   if (rc != SMLU_OK) return rc;
   *dom = (rec[6] & 0xffffffffll) != 0 || (rec[6] >> 32) != 0;
@@ -3516,8 +3553,11 @@ extern "C" {
 // failure fallback).  So it does for non-dominant values factored under a diagonal
 // tolerance below the pivot tolerance (UMFPACK's symmetric default 0.001 < 0.1): a diagonal kept
 // at 0.001 of its column lets the factors grow up to 1000x per step, and UMFPACK's own solve
-// refines by default (IRSTEP 2) for the same reason.  Stops when the residual max-norm stops
-// halving (at once for an accurate solve: one residual, no extra solve).
+// refines by default (IRSTEP 2) for the same reason.  Stopping rule of LAPACK's dgerfs with a
+// rounding floor: a correction is solved only while the componentwise backward error
+// max |r|/(|A||x|+|b|) exceeds 4 unit roundoffs (2^-51; dgerfs uses 1, which a residual summed in
+// fp64 rarely reaches, so it spends two extra solves to gain nothing) and at most halves the
+// previous one -- an accurate solve costs one residual and no extra solve.
 // Residual buffers and the column of every A entry (allocated on first use).
 static int ensure_residual(smlu_handle* h) {
   Plan& P = h->plan;
@@ -3527,7 +3567,7 @@ static int ensure_residual(smlu_handle* h) {
     HIPCHK(h->ref_b.alloc((size_t)n));
     HIPCHK(h->ref_r.alloc((size_t)n));
     HIPCHK(h->ref_d.alloc((size_t)n));
-    HIPCHK(h->ref_nrm.alloc(1));
+    HIPCHK(h->ref_nrm.alloc(2));
   }
   if (!h->Acol.p) {
     std::vector<int32_t> ac((size_t)std::max<int64_t>(P.nnzA, 1));
@@ -3548,6 +3588,7 @@ static int solve_refined(smlu_handle* h, const double* db, double* dx) {
   const int steps = auto_refine_steps(h);
   h->refine_steps = 0;
   h->refine_resid = -1;
+  h->refine_berr = -1;
   if (steps == 0) return run_solve_dev(h, db, dx, 0);
   Plan& P = h->plan;
   const int64_t n = P.n;
@@ -3558,19 +3599,22 @@ static int solve_refined(smlu_handle* h, const double* db, double* dx) {
   int rc = run_solve_dev(h, h->ref_b.p, dx, 0);
   if (rc != SMLU_OK) return rc;
   const double ms = h->solve_ms;
+  const double eps = std::ldexp(1.0, -51);   // 4 unit roundoffs
   double prev = HUGE_VAL;
   for (int it = 0; it < steps; ++it) {
-    HIPCHK(hipMemsetAsync(h->ref_nrm.p, 0, sizeof(double), st));
+    HIPCHK(hipMemsetAsync(h->ref_nrm.p, 0, 2 * sizeof(double), st));
     HIPCHK(launch_residual(st, n, h->Arowptr.p, h->Arow_ent.p, h->Acol.p, h->A.p, dx, h->ref_b.p, h->ref_r.p,
                            h->ref_nrm.p));
-    long long rec[8];
-    rc = read_status(h, nullptr, 0, reinterpret_cast<const int32_t*>(h->ref_nrm.p), 2, rec);
+    long long rec[16];
+    rc = read_status(h, nullptr, 0, reinterpret_cast<const int32_t*>(h->ref_nrm.p), 4, rec);
     if (rc != SMLU_OK) return rc;
-    double nrm;
+    double nrm, berr;
     std::memcpy(&nrm, &rec[6], sizeof nrm);
+    std::memcpy(&berr, &rec[7], sizeof berr);
     h->refine_resid = nrm;
-    if (nrm == 0.0 || nrm > 0.5 * prev) break;
-    prev = nrm;
+    h->refine_berr = berr;
+    if (berr <= eps || berr > 0.5 * prev) break;
+    prev = berr;
     rc = run_solve_dev(h, h->ref_r.p, h->ref_d.p, 0);
     if (rc != SMLU_OK) return rc;
     HIPCHK(launch_axpy1(st, n, h->ref_d.p, dx));
@@ -3588,10 +3632,10 @@ int smlu_residual_device(smlu_handle* h, const double* d_x, const double* d_b, d
   int rc = ensure_residual(h);
   if (rc != SMLU_OK) return rc;
   hipStream_t st = h->stream;
-  HIPCHK(hipMemsetAsync(h->ref_nrm.p, 0, sizeof(double), st));
+  HIPCHK(hipMemsetAsync(h->ref_nrm.p, 0, 2 * sizeof(double), st));
   HIPCHK(launch_residual(st, h->plan.n, h->Arowptr.p, h->Arow_ent.p, h->Acol.p, h->A.p, d_x, d_b, d_r,
                          h->ref_nrm.p));
-  long long rec[8];
+  long long rec[16];
   rc = read_status(h, nullptr, 0, reinterpret_cast<const int32_t*>(h->ref_nrm.p), 2, rec);
   if (rc != SMLU_OK) return rc;
   double v;
@@ -4290,6 +4334,12 @@ double smlu_stat(const smlu_handle* h, const char* key) {
   if (k == "nranks") return (double)h->nranks;
   if (k == "owned_blocks") return (double)h->lay.blocks.size();
   if (k == "comm_steps") return (double)h->comm.size();
+  if (k == "comm_calls") return (double)h->comm_calls;
+  if (k == "comm_bytes_sent") return h->comm_sent;
+  if (k == "comm_bytes_recv") return h->comm_recv;
+  if (k == "comm_bytes_sent_refactor") return h->comm_sent_fac;
+  if (k == "comm_bytes_recv_refactor") return h->comm_recv_fac;
+  if (k == "rccl_nranks") return h->rccl ? (double)static_cast<const RcclState*>(h->rccl)->comm_count : 0.0;
   if (k == "store_bytes_rank") return 8.0 * (double)h->lay.store_size;
   if (k == "scratch_bytes_rank") return 8.0 * (double)h->lay.scratch_size;
   if (k == "shared_fronts") {
@@ -4347,8 +4397,13 @@ double smlu_stat(const smlu_handle* h, const char* key) {
     for (const SNode& r : h->hsn) c += r.mode == m ? 1 : 0;
     return c;
   }
+  if (k == "status_copy_retries") return (double)h->status_copy_retries;
+  if (k == "bad_info_count") return (double)h->bad_info_count;
+  if (k == "bad_info_node") return (double)h->bad_info_node;
+  if (k == "bad_info_word") return (double)h->bad_info_word;
   if (k == "refine_steps") return (double)h->refine_steps;
   if (k == "refine_residual") return h->refine_resid;
+  if (k == "refine_berr") return h->refine_berr;
   if (k == "gemm_flops") return h->gemm_flops;
   if (k == "gemm22_flops") return h->gemm22_flops;
   if (k == "gemm_launches") return (double)h->gemm_launches;
@@ -4486,6 +4541,11 @@ int smlu_dist_create_rccl(int64_t n, const int64_t* colptr, const int64_t* rowva
     return fail(nullptr, SMLU_ERR_HIP, "ncclCommInitRank failed");
   }
   st->rank = rank;
+  if (R->CommCount(st->comm, &st->comm_count) != ncclSuccess || st->comm_count != nranks) {
+    (void)R->CommDestroy(st->comm);
+    delete st;
+    return fail(nullptr, SMLU_ERR_HIP, "ncclCommCount does not report the requested rank count");
+  }
   smlu_transport tr{};
   tr.ctx = st;
   tr.device_memory = 1;

@@ -173,12 +173,36 @@ def ptr(a):
 def order_after_caller(h, t):
     """Point the handle's device entry points at the stream that produced tensor `t` (torch's
     current stream on t's device), so the library's reads of t wait for that work
-    (smlu_set_stream).  Raw pointers keep the previous setting (the null stream by default)."""
-    if h is None or not hasattr(t, "is_cuda") or not t.is_cuda:
+    (smlu_set_stream).  Raw pointers get the null stream.  Pair every call with
+    release_caller() (try/finally): the handle never keeps a stream the caller may destroy."""
+    if h is None:
         return
-    import torch
-    s = torch.cuda.current_stream(t.device).cuda_stream
+    s = 0
+    if hasattr(t, "is_cuda") and t.is_cuda:
+        import torch
+        s = torch.cuda.current_stream(t.device).cuda_stream
     lib().smlu_set_stream(h, ctypes.c_void_p(s))
+
+
+def release_caller(h):
+    """Back to the null stream after a device call (smlu.h: smlu_set_stream lifetime)."""
+    if h is not None:
+        lib().smlu_set_stream(h, ctypes.c_void_p(0))
+
+
+class caller_stream:
+    """with caller_stream(h, t): ... -- order_after_caller on entry, release_caller on exit."""
+
+    def __init__(self, h, t):
+        self.h, self.t = h, t
+
+    def __enter__(self):
+        order_after_caller(self.h, self.t)
+        return self
+
+    def __exit__(self, *exc):
+        release_caller(self.h)
+        return False
 
 
 def last_error(h=None) -> str:

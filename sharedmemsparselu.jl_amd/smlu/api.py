@@ -219,9 +219,9 @@ class ParallelSparseLU:
         """lu! with values already on the device (torch tensor or raw pointer int; complex
         handles take interleaved complex values, e.g. a complex128 tensor)."""
         ptr = d_values.data_ptr() if hasattr(d_values, "data_ptr") else int(d_values)
-        C.order_after_caller(self._h, d_values)
         fn = C.lib().smlu_refactor_z_device if self.is_complex else C.lib().smlu_refactor_device
-        rc = _check(fn(self._h, ctypes.c_void_p(ptr)), self._h)
+        with C.caller_stream(self._h, d_values):
+            rc = _check(fn(self._h, ctypes.c_void_p(ptr)), self._h)
         self._factors = None
         self._zfactors = None
         if rc == C.SMLU_SINGULAR:
@@ -231,9 +231,9 @@ class ParallelSparseLU:
     def solve_device(self, d_x, d_b):
         px = d_x.data_ptr() if hasattr(d_x, "data_ptr") else int(d_x)
         pb = d_b.data_ptr() if hasattr(d_b, "data_ptr") else int(d_b)
-        C.order_after_caller(self._h, d_b)
-        return _check(C.lib().smlu_solve_device(self._h, ctypes.c_void_p(pb), ctypes.c_void_p(px)),
-                      self._h)
+        with C.caller_stream(self._h, d_b):
+            return _check(C.lib().smlu_solve_device(self._h, ctypes.c_void_p(pb), ctypes.c_void_p(px)),
+                          self._h)
 
     def solve_multi_device(self, d_X, d_B):
         """ldiv! for several right-hand sides on the device: d_B, d_X are (nrhs, n) contiguous
@@ -243,9 +243,9 @@ class ParallelSparseLU:
         if n != self.n or tuple(d_X.shape) != (nrhs, n):
             raise DimensionMismatch(f"B has shape {tuple(d_B.shape)}, X has shape {tuple(d_X.shape)}, n={self.n}")
         ld = 2 * n if self.is_complex else n     # leading dimension in doubles
-        C.order_after_caller(self._h, d_B)
-        return _check(C.lib().smlu_solve_multi_device(self._h, nrhs, ctypes.c_void_p(d_B.data_ptr()), ld,
-                                                      ctypes.c_void_p(d_X.data_ptr()), ld), self._h)
+        with C.caller_stream(self._h, d_B):
+            return _check(C.lib().smlu_solve_multi_device(self._h, nrhs, ctypes.c_void_p(d_B.data_ptr()), ld,
+                                                          ctypes.c_void_p(d_X.data_ptr()), ld), self._h)
 
     def close(self):
         h = getattr(self, "_h", None)

@@ -160,8 +160,8 @@ class DistributedSparseLU:
     def refactor_device(self, d_values):
         """lu!(F, A) with values already in HBM (A's CSC order); collective."""
         ptr = d_values.data_ptr() if hasattr(d_values, "data_ptr") else int(d_values)
-        C.order_after_caller(self._h, d_values)
-        rc = _check(C.lib().smlu_refactor_device(self._h, ctypes.c_void_p(ptr)), self._h)
+        with C.caller_stream(self._h, d_values):
+            rc = _check(C.lib().smlu_refactor_device(self._h, ctypes.c_void_p(ptr)), self._h)
         self.status = rc
         if rc == C.SMLU_SINGULAR:
             raise SingularException(C.lib().smlu_last_error_col(self._h))
@@ -172,8 +172,8 @@ class DistributedSparseLU:
         anywhere in the partition trigger the same iterative refinement as on one GPU."""
         px = d_x.data_ptr() if hasattr(d_x, "data_ptr") else int(d_x)
         pb = d_b.data_ptr() if hasattr(d_b, "data_ptr") else int(d_b)
-        C.order_after_caller(self._h, d_b)
-        _check(C.lib().smlu_solve_device(self._h, ctypes.c_void_p(pb), ctypes.c_void_p(px)), self._h)
+        with C.caller_stream(self._h, d_b):
+            _check(C.lib().smlu_solve_device(self._h, ctypes.c_void_p(pb), ctypes.c_void_p(px)), self._h)
         return d_x
 
     def stat(self, key):

@@ -268,3 +268,65 @@ def test_dist_rccl_two_ranks_two_gpus():
     for rank, x13, x2, info, _ in res:
         assert info["transport"] == "rccl" and info["shared_fronts"] > 0
         assert np.allclose(x13[0], xs, rtol=1e-11, atol=1e-13), rank
+
+
+def _spin_worker(rank, world, port, which, ob, q):
+    # two partitioned handles on the same matrix: the default bounded waits, and SMLU_SWEEP_SPIN=0
+    # (every sync-free sweep wait reports a timeout on every rank) -> the solve must be re-run on
+    # the per-block schedule with the remapped comm segments and give the same x bitwise
+    try:
+        import torch
+        import torch.distributed as dist
+        import smlu
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        if ob:
+            os.environ["SMLU_OB"] = str(ob)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        torch.cuda.set_device(0)
+        A = _matrix(which)
+        n = A.shape[0]
+        db = torch.from_numpy(np.random.default_rng(11).random(n)).cuda()
+        F = smlu.DistributedSparseLU(A, device=0)
+        dx = torch.empty_like(db)
+        F.solve_device(dx, db)
+        x_ref = dx.cpu().numpy()
+        t_ref = F.stat("sweep_timeouts")
+        sweeps = F.stat("solve_sweeps")
+        F.close()
+        os.environ["SMLU_SWEEP_SPIN"] = "0"
+        G = smlu.DistributedSparseLU(A, device=0)
+        dx2 = torch.empty_like(db)
+        G.solve_device(dx2, db)
+        x_spin = dx2.cpu().numpy()
+        t_spin = G.stat("sweep_timeouts")
+        sweeps_all = G.stat("solve_sweeps")
+        G.close()
+        q.put((rank, x_ref, x_spin, (t_ref, t_spin, sweeps, sweeps_all), None))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((rank, None, None, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world,which,ob", [(2, "poisson_big", 128), (4, "poisson40", 128)])
+def test_dist_forced_sweep_timeout_reruns_per_block(world, which, ob):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_spin_worker, args=(r, world, port, which, ob, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=300) for _ in ps]
+    for p in ps:
+        p.join(timeout=120)
+    errs = [r[4] for r in res if r[4]]
+    assert not errs, errs[0]
+    assert any(r[3][2] > 0 for r in res), "no rank runs a sync-free sweep: the test would prove nothing"
+    A = _matrix(which)
+    b = np.random.default_rng(11).random(A.shape[0])
+    for rank, x_ref, x_spin, (t_ref, t_spin, sweeps, _), _ in res:
+        assert t_ref == 0, rank
+        assert t_spin > 0, (rank, t_spin, sweeps)   # the allreduced flag: every rank re-ran
+        assert np.array_equal(x_ref, x_spin), (rank, np.abs(x_ref - x_spin).max())
+        assert np.abs(A @ x_spin - b).max() / np.abs(b).max() < 1e-12

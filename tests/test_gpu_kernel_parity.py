@@ -1,14 +1,15 @@
 """Every kernel variant of the numeric refactor against the oracle, and the error paths.
 
-* GEMM tile variants.  A launch normally takes the fp64 MFMA 128x128 tile
-  (`k_gemm128_mfma`) only when it has >= 512 output tiles, which the oracle-sized cases never
-  reach.  The schedule knobs force each variant on oracle-sized fronts, so the dominant kernel
-  of the 128^3 refactor (`k_gemm128_mfma<false>`) and its TRSM form (`<true>`, growth epilogue)
-  are compared with the oracle entry by entry:
-    mfma128  SMLU_T128MIN=1                   every GEMM launch on k_gemm128_mfma
+* GEMM tile variants.  A launch normally takes the fp64 MFMA 128x128 tile (`k_gemm128_mfma2`,
+  the v2 tile) only when it has >= 512 output tiles, which the oracle-sized cases never reach.
+  The schedule knobs force each variant on oracle-sized fronts, so the dominant kernel of the
+  128^3 refactor (`k_gemm128_mfma2<false>`) and its TRSM form (`<true>`, growth epilogue) are
+  compared with the oracle entry by entry:
+    mfma128  SMLU_T128MIN=1                   every GEMM launch on k_gemm128_mfma2
     valu64   SMLU_T128MIN=2^60, SMLU_SMALLK=0 every GEMM launch on the VALU 64x64 tile k_gemm
     valu128  SMLU_T128MIN=1, use_mfma=0       the VALU 128x128 tile k_gemm128
-    default  as shipped (k_gemm_k64 for k <= 64 launches, k_tri_inv, 64x64 tiles)
+    default  as shipped (k_gemm_k64 for k <= 64 launches, fused panels with tile inverses,
+             k_urows, 64x64 tiles below the MFMA threshold)
     rocblas  SMLU_ROCBLAS=1 SMLU_ROCBLAS_MIN=1 every F22 / trailing GEMM task through rocBLAS dgemm
              (deterministic mode; opt-in comparison path, the default runs our tiles only)
 * Error paths of the reference surface: SingularException from lu(A) (src/SharedMemSparseLU.jl:74)

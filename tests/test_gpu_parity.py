@@ -197,6 +197,33 @@ def test_weak_pivots_trigger_refinement(gpu, monkeypatch):
     assert isapprox(xb, spla.spsolve(P, np.ones(P.shape[0])), TOL, TOL)
 
 
+@pytest.mark.parametrize("nel", [50, 200])
+def test_nondominant_refinement_stops_on_backward_error(gpu, nel):
+    # The reference's sparse FE matrix (test/runtests.jl:12-21) is not diagonally dominant, so the
+    # default options (diag_pivot_tol 0.001 < pivot_tol 0.1) arm the automatic refinement.  It must
+    # stop on LAPACK dgerfs' rule with a rounding floor: no correction solve once the componentwise
+    # backward error max|r|/(|A||x|+|b|) is within 4 unit roundoffs (2^-51), at most one for a
+    # well-conditioned matrix.
+    rng = np.random.default_rng(100 + nel)
+    A = sp.csc_matrix(O.test_matrix(rng, nel, 5))
+    n = A.shape[0]
+    F = smlu.ParallelSparseLU(A)
+    assert F.stat("dominant") == 0
+    b = rng.random(n)
+    x = np.empty(n)
+    smlu.ldiv_(x, F, b)
+    steps, berr = F.stat("refine_steps"), F.stat("refine_berr")
+    assert 0 <= berr <= 2.0 ** -51, (steps, berr)
+    assert steps <= 1, (steps, berr)
+    if steps == 1:   # a correction was solved only because the first solve's berr exceeded eps
+        F0 = smlu.ParallelSparseLU(A, refine=0)
+        x0 = np.empty(n)
+        smlu.ldiv_(x0, F0, b)
+        r0 = np.abs(A @ x0 - b) / (abs(A) @ np.abs(x0) + np.abs(b))
+        assert r0.max() > 2.0 ** -51
+    assert isapprox(x, spla.spsolve(A, b), TOL, TOL)
+
+
 def test_solve_multiple_rhs(gpu):
     # ldiv! with a matrix of right-hand sides: equals column-by-column solves
     A = mats.poisson2d(40)
