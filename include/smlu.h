@@ -36,7 +36,8 @@ extern "C" {
 #define SMLU_ERR_ALLOC        (-3)  /* host or device allocation failed */
 #define SMLU_ERR_HIP          (-4)  /* HIP runtime error */
 #define SMLU_ERR_NODEVICE     (-5)  /* no gfx950 device visible: the library never falls back to the CPU */
-#define SMLU_ERR_STATE        (-6)  /* handle has no numeric factorization */
+#define SMLU_ERR_STATE        (-6)  /* handle has no numeric factorization / illegal device status */
+#define SMLU_ERR_PATTERN      (-7)  /* a given L/U pattern is not the structural fill of (Rs.*A)[p,q] */
 
 /* ---- ordering choices ------------------------------------------------------------- */
 #define SMLU_ORDER_AUTO         0   /* geometric ND if grid[] given, else graph nested dissection */
@@ -87,12 +88,20 @@ int smlu_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const d
                 const smlu_opts* opts, smlu_handle** out);
 
 /* As smlu_create, but with the caller's row order p and column order q (1-based or 0-based
- * per opts), and optionally Rs (NULL = compute).  Used by the Julia shim to hand over
- * UMFPACK's own (p, q, Rs) so that pivot order matches the reference by construction
- * (SURVEY §8f-1).  No pivoting is performed on top of the given order. */
+ * per opts), optionally Rs (NULL = compute) and optionally the L and U patterns (CSC colptr /
+ * rowval; L with its unit diagonal first in each column, U with its diagonal last, rows
+ * increasing; all four NULL = none).  Used by the Julia shim to hand over UMFPACK's own analysis
+ * -- lu(A) and F.p, F.q, F.Rs, F.L, F.U, src/SharedMemSparseLU.jl:74-77, :93-94 -- so that pivot
+ * order and L/U pattern match the reference by construction.  No pivoting
+ * is performed on top of the given order.  A given pattern must lie inside the structural fill of
+ * (Rs.*A)[p, q] (UMFPACK's may miss fill entries that came out exactly zero; smlu_stat
+ * "pattern_dropped" counts them), else SMLU_ERR_PATTERN and no handle; smlu_get_factors then
+ * exports exactly that pattern. */
 int smlu_create_with_pivots(int64_t n, const int64_t* colptr, const int64_t* rowval,
                             const double* nzval, const int64_t* p, const int64_t* q,
-                            const double* Rs, const smlu_opts* opts, smlu_handle** out);
+                            const double* Rs, const int64_t* Lcolptr, const int64_t* Lrowval,
+                            const int64_t* Ucolptr, const int64_t* Urowval, const smlu_opts* opts,
+                            smlu_handle** out);
 
 /* lu!(F, A) — src/SharedMemSparseLU.jl:245-279: numeric refactorization with the same
  * pattern, new values (nzval in A's original CSC order, host memory). */

@@ -523,6 +523,20 @@ void oracle_mf_result(const oracle_mf* h, int32_t* rowperm, int32_t* flags, doub
   if (Rs) memcpy(Rs, h->Rs, (size_t)h->n * sizeof(double));
 }
 
+/* Front s's factor values as stored after the last factorization: its L panel (M x ns, ld M: the
+ * unit-lower multipliers below the diagonal, U11 on and above it, rows in pivot order) followed by
+ * U12 (ns x nu, ld ns) -- the layout of the GPU's smlu_dev_front_values, so the two compare entry
+ * by entry on the same assembly tree.  Returns the number of doubles written (M ns + ns nu). */
+int64_t oracle_mf_front_values(const oracle_mf* h, int64_t s, double* out) {
+  if (s < 0 || s >= h->nsup) return -1;
+  const int64_t ns = ns_of(h, s), nu = nu_of(h, s), M = ns + nu;
+  if (out) {
+    memcpy(out, h->store + h->loff[s], (size_t)(M * ns) * sizeof(double));
+    if (nu > 0) memcpy(out + M * ns, h->store + h->uoff[s], (size_t)(ns * nu) * sizeof(double));
+  }
+  return M * ns + ns * nu;
+}
+
 /* Diagonal dominance by columns or by rows (|a_jj| >= sum of the other |a_ij| with a_jj != 0),
  * sequential sums in CSC order: the test the GPU path applies to every new set of values to pick
  * its pivoting mode.  Returns 1 / 0. */

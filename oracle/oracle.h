@@ -43,6 +43,9 @@ int oracle_mf_factor(oracle_mf* h, const double* nzval);
 void oracle_mf_set_pairs(oracle_mf* h, int pairs);
 void oracle_mf_result(const oracle_mf* h, int32_t* rowperm, int32_t* flags, double* Rs);
 void oracle_mf_destroy(oracle_mf* h);
+/* Front s after oracle_mf_factor: L panel (M x ns, ld M) then U12 (ns x nu, ld ns); returns the
+ * count of doubles (out may be NULL to query it), -1 for a bad s. */
+int64_t oracle_mf_front_values(const oracle_mf* h, int64_t s, double* out);
 int oracle_dominant(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* a);
 
 #ifdef __cplusplus

@@ -81,6 +81,8 @@ def lib():
         L.oracle_mf_factor.argtypes = [vp, vp]
         L.oracle_mf_result.argtypes = [vp, vp, vp, vp]
         L.oracle_mf_destroy.argtypes = [vp]
+        L.oracle_mf_front_values.restype = ctypes.c_int64
+        L.oracle_mf_front_values.argtypes = [vp, ctypes.c_int64, vp]
         L.oracle_dominant.restype = ctypes.c_int
         L.oracle_dominant.argtypes = [ctypes.c_int64, vp, vp, vp]
         _LIB = L
@@ -207,6 +209,16 @@ class MultifrontalOracle:
         lib().oracle_mf_result(self._h, _vp(self.rowperm), _vp(self.flags), _vp(self.Rs))
         return rc
 
+    def front_values(self, s):
+        """Front s's stored factor values after factor(): L panel (M x ns, ld M) then U12 (ns x nu,
+        ld ns), the layout of the GPU's smlu_dev_front_values."""
+        cnt = lib().oracle_mf_front_values(self._h, int(s), None)
+        if cnt < 0:
+            raise IndexError(s)
+        out = np.empty(cnt)
+        lib().oracle_mf_front_values(self._h, int(s), _vp(out))
+        return out
+
     @property
     def p(self):
         """Final row order: p[k] = p0[first_s + rowperm[k]] (new -> old)."""
@@ -243,13 +255,14 @@ def front_modes(fronts, pivmode, dominant_values, full_piv_ns=None):
 
 
 def gpu_pivot_choice(A, q, fronts, *, pivmode=0, dominant_values=None, given=False, pivot_tol=0.1,
-                     diag_tol=0.001, full_piv_ns=None, values=None, pairs=False):
+                     diag_tol=0.001, full_piv_ns=None, values=None, pairs=False, threads=1, keep=False):
     """Independent restatement of the GPU path's whole pivot decision for one factorization:
     the candidate modes, threshold partial pivoting inside every front (mf.c), and the
     re-pivoting refactor (a zero or weak pivot while diagonal-tile fronts exist -> every blocked
     front again with all fully-summed rows as candidates).  `pivmode`: the handle's mode before
     this factorization (dominant values reset it to 0).  A given (p, q) keeps the diagonal unless
-    it is exactly zero (diag_tol 0) and is never re-pivoted.  Returns (p, pivmode, modes, flags)."""
+    it is exactly zero (diag_tol 0) and is never re-pivoted.  Returns (p, pivmode, modes, flags),
+    and with keep=True also the factored MultifrontalOracle (its front_values; the caller closes it)."""
     A = sp.csc_matrix(A)
     A.sort_indices()
     vals = A.data if values is None else values
@@ -265,17 +278,20 @@ def gpu_pivot_choice(A, q, fronts, *, pivmode=0, dominant_values=None, given=Fal
 
     def run(pm):
         modes = front_modes(fronts, pm, dominant_values, full_piv_ns)
-        mf = MultifrontalOracle(A, q, fronts, modes, diag_tol=dt, pivot_tol=pivot_tol, pairs=pairs)
+        mf = MultifrontalOracle(A, q, fronts, modes, diag_tol=dt, pivot_tol=pivot_tol, pairs=pairs,
+                                threads=threads)
         st = mf.factor(vals)
-        out = (mf.p, modes, mf.flags.copy(), st)
-        mf.close()
-        return out
+        return mf.p, modes, mf.flags.copy(), st, mf
 
-    p, modes, flags, st = run(pivmode)
+    p, modes, flags, st, mf = run(pivmode)
     if ((st == 1 or (flags & 2).any()) and pivmode == 0 and (modes == 2).any() and pivot_tol > 0
             and not given and not pairs):
+        mf.close()
         pivmode = 1
-        p, modes, flags, st = run(1)
+        p, modes, flags, st, mf = run(1)
+    if keep:
+        return p, pivmode, modes, flags, mf
+    mf.close()
     return p, pivmode, modes, flags
 
 

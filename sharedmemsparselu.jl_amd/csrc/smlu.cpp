@@ -396,6 +396,12 @@ struct smlu_handle {
   hipStream_t caller = nullptr;   // caller's stream (smlu_set_stream; nullptr = the null stream)
   hipEvent_t ev_caller = nullptr;
   DBuf<long long> rb;         // status record for the host (k_status; read_status)
+  // the caller's L/U pattern (smlu_create_with_pivots, UMFPACK's F.L / F.U): when present, the
+  // factors are exported on exactly that pattern; pattern_dropped counts the structural entries of
+  // (Rs.*A)[p, q]'s fill it leaves out (UMFPACK drops entries that are exactly zero)
+  std::vector<int64_t> gLp, gLi, gUp, gUi;
+  bool given_pattern = false;
+  int64_t pattern_dropped = 0;
   long long rb_seq = 0;       // sequence number of the last status record
   int64_t status_copy_retries = 0;   // status records re-read after a stamp mismatch
   int64_t bad_info_node = -1, bad_info_count = 0;   // illegal info words seen by k_status
@@ -3163,13 +3169,6 @@ int smlu_create_i32(int64_t n, const int32_t* colptr, const int32_t* rowval, con
   return smlu_create(n, cp.data(), rv.data(), nzval, opts, out);
 }
 
-int smlu_create_with_pivots(int64_t n, const int64_t* colptr, const int64_t* rowval,
-                            const double* nzval, const int64_t* p, const int64_t* q,
-                            const double* Rs, const smlu_opts* opts, smlu_handle** out) {
-  if (!p || !q) return fail(nullptr, SMLU_ERR_ARG, "p and q are required");
-  return create_impl(n, colptr, rowval, nzval, p, q, Rs, opts, out);
-}
-
 static int ensure_residual(smlu_handle* h);
 
 // Pivoting mode per refactor: dominant values take the diagonal-tile path for
@@ -3984,10 +3983,115 @@ static int export_factors(smlu_handle* h, Exported& X, bool values) {
   return SMLU_OK;
 }
 
+// Exported factors restricted to the caller's L/U pattern (smlu_create_with_pivots with patterns):
+// every given entry must be an entry of the structural fill X holds (else SMLU_ERR_PATTERN); the
+// fill entries the caller's pattern leaves out are counted in h->pattern_dropped.
+static int project_to_given(smlu_handle* h, Exported& X) {
+  const int64_t n = h->plan.n;
+  int64_t dropped = 0;
+  auto one = [&](const std::vector<int64_t>& gp, const std::vector<int64_t>& gi, std::vector<int64_t>& xp,
+                 std::vector<int64_t>& xi, std::vector<double>& xv, const char* which) -> int {
+    std::vector<double> v(gi.size(), 0.0);
+    for (int64_t j = 0; j < n; ++j) {
+      int64_t t = xp[j];
+      const int64_t te = xp[j + 1];
+      for (int64_t e = gp[j]; e < gp[j + 1]; ++e) {
+        while (t < te && xi[t] < gi[e]) ++t;
+        if (t == te || xi[t] != gi[e])
+          return fail(h, SMLU_ERR_PATTERN, std::string("given ") + which + " entry (" + std::to_string(gi[e]) + ", " +
+                                               std::to_string(j) + ") is not in the structural fill of (Rs.*A)[p, q]");
+        if (!xv.empty()) v[e] = xv[t];
+        ++t;
+      }
+      dropped += (xp[j + 1] - xp[j]) - (gp[j + 1] - gp[j]);
+    }
+    xp = gp;
+    xi = gi;
+    if (!xv.empty()) xv.swap(v);
+    return SMLU_OK;
+  };
+  int rc = one(h->gLp, h->gLi, X.Lp, X.Li, X.Lx, "L");
+  if (rc != SMLU_OK) return rc;
+  rc = one(h->gUp, h->gUi, X.Up, X.Ui, X.Ux, "U");
+  if (rc != SMLU_OK) return rc;
+  h->pattern_dropped = dropped;
+  return SMLU_OK;
+}
+
+static int export_given(smlu_handle* h, Exported& X, bool values) {
+  int rc = export_factors(h, X, values);
+  if (rc != SMLU_OK || !h->given_pattern) return rc;
+  return project_to_given(h, X);
+}
+
+// A caller's CSC pattern of L (unit diagonal stored first in each column) or U (diagonal last),
+// rows strictly increasing, index base `base` -> 0-based arrays; "" or what is wrong.
+static std::string read_factor_pattern(int64_t n, const int64_t* cp, const int64_t* ri, int64_t base, bool lower,
+                                       std::vector<int64_t>& P, std::vector<int64_t>& I) {
+  if (!cp || !ri) return "pattern arrays missing";
+  if (cp[0] != base) return "colptr[0] must equal index_base";
+  P.assign(n + 1, 0);
+  for (int64_t j = 0; j <= n; ++j) P[j] = cp[j] - base;
+  for (int64_t j = 0; j < n; ++j)
+    if (P[j + 1] <= P[j]) return "every column must hold its diagonal entry";
+  I.resize(P[n]);
+  for (int64_t j = 0; j < n; ++j)
+    for (int64_t e = P[j]; e < P[j + 1]; ++e) {
+      const int64_t r = ri[e] - base;
+      if (r < 0 || r >= n || (e > P[j] && r <= I[e - 1])) return "row indices out of range or not increasing";
+      if (lower ? r < j : r > j) return lower ? "L entry above the diagonal" : "U entry below the diagonal";
+      I[e] = r;
+    }
+  for (int64_t j = 0; j < n; ++j)
+    if ((lower ? I[P[j]] : I[P[j + 1] - 1]) != j)
+      return lower ? "L: unit diagonal must be stored first" : "U: diagonal must be stored last";
+  return "";
+}
+
+int smlu_create_with_pivots(int64_t n, const int64_t* colptr, const int64_t* rowval,
+                            const double* nzval, const int64_t* p, const int64_t* q,
+                            const double* Rs, const int64_t* Lcolptr, const int64_t* Lrowval,
+                            const int64_t* Ucolptr, const int64_t* Urowval, const smlu_opts* opts,
+                            smlu_handle** out) {
+  if (!p || !q) return fail(nullptr, SMLU_ERR_ARG, "p and q are required");
+  const bool pat = Lcolptr || Lrowval || Ucolptr || Urowval;
+  std::vector<int64_t> Lp, Li, Up, Ui;
+  if (pat) {
+    if (n <= 0) return fail(nullptr, SMLU_ERR_ARG, "invalid matrix arguments");
+    const int64_t base = opts ? opts->index_base : 1;
+    std::string e;
+    try {
+      e = read_factor_pattern(n, Lcolptr, Lrowval, base, true, Lp, Li);
+      if (e.empty()) e = read_factor_pattern(n, Ucolptr, Urowval, base, false, Up, Ui);
+    } catch (const std::bad_alloc&) {
+      return fail(nullptr, SMLU_ERR_ALLOC, "host allocation failed");
+    }
+    if (!e.empty()) return fail(nullptr, SMLU_ERR_PATTERN, "given L/U pattern: " + e);
+  }
+  int rc = create_impl(n, colptr, rowval, nzval, p, q, Rs, opts, out);
+  if (rc < 0 || !pat || !*out) return rc;
+  smlu_handle* h = *out;
+  // the caller's pattern against the structural fill of (Rs.*A)[p, q] of the plan
+  h->gLp.swap(Lp);
+  h->gLi.swap(Li);
+  h->gUp.swap(Up);
+  h->gUi.swap(Ui);
+  h->given_pattern = true;
+  Exported X;
+  int r2 = export_given(h, X, false);
+  if (r2 != SMLU_OK) {
+    const std::string msg = h->err;
+    smlu_destroy(h);
+    *out = nullptr;
+    return fail(nullptr, r2, msg);
+  }
+  return rc;
+}
+
 int smlu_get_sizes(smlu_handle* h, int64_t* n, int64_t* nnzL, int64_t* nnzU) {
   if (!h) return fail(h, SMLU_ERR_ARG, "NULL handle");
   Exported X;
-  int rc = export_factors(h, X, false);
+  int rc = export_given(h, X, false);
   if (rc != SMLU_OK) return rc;
   if (n) *n = h->plan.n;
   if (nnzL) *nnzL = X.Lp[h->plan.n];
@@ -4003,7 +4107,7 @@ int smlu_get_factors(smlu_handle* h, int64_t* Lcolptr, int64_t* Lrowval, double*
   HIPCHK(hipSetDevice(h->device));
   HIPCHK(hipStreamSynchronize(h->stream));
   Exported X;
-  int rc = export_factors(h, X, true);
+  int rc = export_given(h, X, true);
   if (rc != SMLU_OK) return rc;
   const int64_t n = h->plan.n, b = h->opts.index_base;
   if (Lcolptr) for (int64_t j = 0; j <= n; ++j) Lcolptr[j] = X.Lp[j] + b;
@@ -4397,6 +4501,8 @@ double smlu_stat(const smlu_handle* h, const char* key) {
     for (const SNode& r : h->hsn) c += r.mode == m ? 1 : 0;
     return c;
   }
+  if (k == "pattern_dropped") return (double)h->pattern_dropped;
+  if (k == "given_pattern") return h->given_pattern ? 1.0 : 0.0;
   if (k == "status_copy_retries") return (double)h->status_copy_retries;
   if (k == "bad_info_count") return (double)h->bad_info_count;
   if (k == "bad_info_node") return (double)h->bad_info_node;

@@ -79,16 +79,21 @@ function ParallelSparseLU(A::SparseMatrixCSC{Tf,Ti}, chunk_size=nothing) where {
     return F
 end
 
-# Optional: hand UMFPACK's own analysis over so that pivot order matches it by construction
-# (SURVEY §8f-1): the reference's lu(A) (:74) and its p, q, Rs extraction (:75-77, :93-94).
+# Optional: hand UMFPACK's own analysis over so that pivot order and L/U pattern match it by
+# construction (SURVEY §8f-1, §8(b)): the reference's lu(A) (:74) and its L, U, p, q, Rs
+# extraction (:75-77, :93-94).  The library checks the pattern against the structural fill of
+# (Rs.*A)[p, q] and exports F.L / F.U on exactly that pattern.
 function ParallelSparseLU_umfpack(A::SparseMatrixCSC{Float64,Ti}, chunk_size=nothing) where {Ti<:SmluInt}
     U = lu(A)
+    FL = U.L; FU = U.U
     o = default_opts(); o.chunk_size = min(something(chunk_size, 8), A.n); h = Ref{Ptr{Cvoid}}(C_NULL)
     rc = ccall((:smlu_create_with_pivots, libsmlu), Int32,
                (Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Ptr{Int64}, Ptr{Int64},
-                Ptr{Float64}, Ref{SmluOpts}, Ref{Ptr{Cvoid}}),
+                Ptr{Float64}, Ptr{Int64}, Ptr{Int64}, Ptr{Int64}, Ptr{Int64}, Ref{SmluOpts}, Ref{Ptr{Cvoid}}),
                A.n, Vector{Int64}(A.colptr), Vector{Int64}(A.rowval), A.nzval,
-               Vector{Int64}(U.p), Vector{Int64}(U.q), U.Rs, o, h)
+               Vector{Int64}(U.p), Vector{Int64}(U.q), U.Rs,
+               Vector{Int64}(FL.colptr), Vector{Int64}(FL.rowval),
+               Vector{Int64}(FU.colptr), Vector{Int64}(FU.rowval), o, h)
     check(rc, h[])
     F = ParallelSparseLU{Float64,Ti}(A.m, A.n, h[], copy(A.colptr), copy(A.rowval), o.chunk_size)
     finalizer(cleanup_ParallelSparseLU!, F)

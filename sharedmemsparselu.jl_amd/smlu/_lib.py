@@ -29,6 +29,7 @@ SMLU_ERR_ALLOC = -3
 SMLU_ERR_HIP = -4
 SMLU_ERR_NODEVICE = -5
 SMLU_ERR_STATE = -6
+SMLU_ERR_PATTERN = -7
 
 ORDER_AUTO, ORDER_NATURAL, ORDER_GEOMETRIC_ND, ORDER_GRAPH_ND, ORDER_GIVEN, ORDER_AMD = range(6)
 
@@ -57,7 +58,7 @@ class SmluOpts(ctypes.Structure):
 SIGNATURES = {
     "smlu_default_opts": (None, [ctypes.POINTER(SmluOpts)]),
     "smlu_create": (i32, [i64, vp, vp, vp, ctypes.POINTER(SmluOpts), ctypes.POINTER(vp)]),
-    "smlu_create_with_pivots": (i32, [i64, vp, vp, vp, vp, vp, vp, ctypes.POINTER(SmluOpts),
+    "smlu_create_with_pivots": (i32, [i64, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, ctypes.POINTER(SmluOpts),
                                       ctypes.POINTER(vp)]),
     "smlu_refactor": (i32, [vp, vp]),
     "smlu_refactor_device": (i32, [vp, vp]),

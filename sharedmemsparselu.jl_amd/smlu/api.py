@@ -72,7 +72,7 @@ class ParallelSparseLU:
     def __init__(self, A, chunk_size=None, *, ordering="auto", grid=None, device=0,
                  profile=False, p=None, q=None, Rs=None, pivot_tol=None, diag_pivot_tol=None,
                  leaf_size=None, relax=True, use_mfma=None, refine=None,
-                 int32_indices=False):
+                 int32_indices=False, L_pattern=None, U_pattern=None):
         A = _csc(A)
         m, n = A.shape
         if m != n:
@@ -117,9 +117,19 @@ class ParallelSparseLU:
             pp = np.ascontiguousarray(p, dtype=np.int64)
             qq = np.ascontiguousarray(q, dtype=np.int64)
             rs = None if Rs is None else np.ascontiguousarray(Rs, dtype=np.float64)
+            # UMFPACK's F.L / F.U patterns: any sparse matrix, only the pattern is used
+            pat = []
+            for M in (L_pattern, U_pattern):
+                if M is None:
+                    pat += [None, None]
+                else:
+                    M = sp.csc_matrix(M)
+                    M.sort_indices()
+                    pat += [np.ascontiguousarray(M.indptr, dtype=np.int64),
+                            np.ascontiguousarray(M.indices, dtype=np.int64)]
             rc = L.smlu_create_with_pivots(n, C.ptr(self._colptr), C.ptr(self._rowval), C.ptr(vals),
-                                           C.ptr(pp), C.ptr(qq), C.ptr(rs), ctypes.byref(self._opts),
-                                           ctypes.byref(h))
+                                           C.ptr(pp), C.ptr(qq), C.ptr(rs), *[C.ptr(a) for a in pat],
+                                           ctypes.byref(self._opts), ctypes.byref(h))
         elif int32_indices:
             # SparseMatrixCSC{Float64,Int32}: the Int32 entry point
             cp32 = np.ascontiguousarray(A.indptr, dtype=np.int32)
@@ -196,6 +206,29 @@ class ParallelSparseLU:
 
     def stat(self, key):
         return C.lib().smlu_stat(self._h, key.encode())
+
+    def perm_scale(self):
+        """(F.p, F.q, F.Rs) without downloading L and U (smlu_get_factors with NULL factor
+        pointers); real-equivalent order on a complex handle."""
+        n = 2 * self.n if self.is_complex else self.n
+        p = np.empty(n, np.int64); q = np.empty(n, np.int64); Rs = np.empty(n)
+        _check(C.lib().smlu_get_factors(self._h, None, None, None, None, None, None, C.ptr(p), C.ptr(q),
+                                        C.ptr(Rs)), self._h)
+        return p, q, Rs
+
+    def front_store(self):
+        """Diagnostics (smlu_dev_front_offsets / smlu_dev_copy): the factor store as one host array
+        and per front (Loff, Uoff, Foff, M); front s is store[Loff:Loff+M*ns] (L panel, ld M) and
+        store[Uoff:Uoff+ns*nu] (U12, ld ns)."""
+        L = C.lib()
+        ns = int(self.stat("nsuper"))
+        off = np.empty(4 * ns, np.int64)
+        _check(L.smlu_dev_front_offsets(self._h, C.ptr(off)), self._h)
+        ln = ctypes.c_int64()
+        _check(L.smlu_dev_copy(self._h, 0, 0, -1, None, ctypes.byref(ln)), self._h)
+        store = np.empty(ln.value)
+        _check(L.smlu_dev_copy(self._h, 0, 0, ln.value, C.ptr(store), None), self._h)
+        return store, off.reshape(ns, 4)
 
     def fronts(self):
         """The analysis' assembly tree and the current schedule's pivot-candidate mode per front

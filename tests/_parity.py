@@ -88,3 +88,45 @@ def tile_pivoting_matrix(n, seed):
         D[b0:b1, b0:b1] += blk
     np.fill_diagonal(D, 1e-3 * rng.random(n))
     return D
+
+
+def front_parity(A, F, rtol=1e-12, threads=16, prev_pivmode=0):
+    """Factor parity at sizes the one-core fixed-pivot oracle cannot reach: the multifrontal oracle
+    (oracle/mf.c, OpenMP) chooses its own pivots on the handle's assembly tree (the candidate modes
+    and the re-pivoting decision restated as in pivot_parity: modes, pivmode and p bit-identical,
+    Rs bitwise), then EVERY front's stored factor values -- its L panel (M x ns: unit-lower
+    multipliers and U11) and U12 (ns x nu) -- are compared entry by entry with the GPU's factor
+    store (smlu_dev_front_offsets / smlu_dev_copy).  Tolerance per front: rtol * growth * max(1,
+    max |front|).  Returns (fronts compared, entries compared, worst scaled difference)."""
+    A = sp.csc_matrix(A)
+    A.sort_indices()
+    fr = F.fronts()
+    p, q, Rs = F.perm_scale()
+    assert np.array_equal(Rs, O.rowscale(A)), "row scaling must be bitwise identical"
+    p_or, pm, modes, _, mf = O.gpu_pivot_choice(A, q, fr, pivmode=prev_pivmode, pivot_tol=F.stat("pivot_tol"),
+                                                diag_tol=F.stat("diag_pivot_tol"), threads=threads, keep=True)
+    try:
+        assert np.array_equal(modes, fr["mode"]), "per-front pivot candidate modes differ from the restated rule"
+        assert int(F.stat("pivmode")) == pm, (F.stat("pivmode"), pm)
+        bad = np.flatnonzero(p != p_or)
+        assert bad.size == 0, f"pivot order differs from the oracle's at {bad.size} positions, first {bad[:8]}"
+        store, off = F.front_store()
+        nsz = np.diff(fr["first"])
+        nuz = np.diff(fr["rowptr"])
+        amax = max(abs(A.data).max() * abs(Rs).max(), 1e-300)
+        worst, entries = 0.0, 0
+        for s in range(nsz.size):
+            ns_, nu_ = int(nsz[s]), int(nuz[s])
+            M = ns_ + nu_
+            G = np.concatenate([store[off[s, 0]:off[s, 0] + M * ns_], store[off[s, 1]:off[s, 1] + ns_ * nu_]])
+            R = mf.front_values(s)
+            assert G.size == R.size
+            rmax = abs(R).max() if R.size else 0.0
+            rho = max(1.0, rmax / amax)
+            d = abs(G - R).max() / (rho * max(rmax, 1.0)) if R.size else 0.0
+            assert d <= rtol, f"front {s} (ns {ns_}, nu {nu_}, mode {fr['mode'][s]}): scaled difference {d:.3g}"
+            worst = max(worst, d)
+            entries += R.size
+        return nsz.size, entries, worst
+    finally:
+        mf.close()

@@ -55,6 +55,34 @@ def test_c2_poisson2d_512_factor_solve_refactor(gpu):
     F.close()
 
 
+def _fullsize_front_parity(A, label):
+    from _parity import front_parity
+    F = smlu.ParallelSparseLU(A)
+    nf, ne, worst = front_parity(A, F)
+    print(f"{label}: {nf} fronts, {ne} factor entries compared, worst scaled difference {worst:.2e}")
+    A2 = mats.perturb_diag(A, 47)   # C5-style new values: the refactor against the oracle as well
+    smlu.lu_(F, A2)
+    nf2, ne2, worst2 = front_parity(A2, F)
+    print(f"{label} refactor: worst scaled difference {worst2:.2e}")
+    F.close()
+    return ne
+
+
+def test_c2_poisson2d_512_front_parity(gpu):
+    # C2 at full size, every factor entry against the multifrontal oracle (p asserted first)
+    ne = _fullsize_front_parity(mats.poisson2d(512), "C2 512^2")
+    assert ne > 1.5e7
+
+
+def test_poisson3d_64_front_parity(gpu):
+    # 3D 64^3 ND: root front of ~4,600 pivots (12 outer blocks of 384, diagonal-tile pivoting, the
+    # GEMM-form triangular solves, k_urows and k = 384 trailing updates on the MFMA tiles) and
+    # the levels below it, every factor entry against the multifrontal oracle
+    A = mats.poisson3d(64)
+    ne = _fullsize_front_parity(A, "3D 64^3")
+    assert ne > 1.5e8
+
+
 def test_c3_poisson3d_128_refactor_steady_state(gpu):
     # C3/C5: 3D 7-point Poisson 128^3; five refactors with new values from HBM, each checked by
     # its solve residual; refactoring the same values twice gives bitwise-identical solutions

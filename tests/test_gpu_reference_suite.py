@@ -126,11 +126,13 @@ def test_golden_with_given_pivots(gpu, path):
     z = np.load(path, allow_pickle=False)
     n = int(z["n"])
     A = sp.csc_matrix((z["A_data"], z["A_indices"], z["A_indptr"]), shape=(n, n))
-    F = smlu.ParallelSparseLU(A, p=z["p"], q=z["q"])
-    assert np.array_equal(F.p, z["p"]) and np.array_equal(F.q, z["q"])
-    assert np.array_equal(F.Rs, z["Rs"])
     L = sp.csc_matrix((z["L_data"], z["L_indices"], z["L_indptr"]), shape=(n, n))
     U = sp.csc_matrix((z["U_data"], z["U_indices"], z["U_indptr"]), shape=(n, n))
+    # the whole §8(b) hand-over: (p, q) and the fixture's own L/U pattern
+    F = smlu.ParallelSparseLU(A, p=z["p"], q=z["q"], L_pattern=L, U_pattern=U)
+    assert F.stat("given_pattern") == 1 and F.stat("pattern_dropped") == 0
+    assert np.array_equal(F.p, z["p"]) and np.array_equal(F.q, z["q"])
+    assert np.array_equal(F.Rs, z["Rs"])
     for G, R in ((F.L, L), (F.U, U)):
         assert np.array_equal(G.indptr, R.indptr), "colptr differs from the fixture"
         assert np.array_equal(G.indices, R.indices), "rowval differs from the fixture"
@@ -155,3 +157,60 @@ def test_c1_fixture_default_analysis(gpu):
     smlu.ldiv_(x, F, z["b"])
     check_c1_digest(z, F.L, F.U, F.Rs, x, 1e-12)
     F.close()
+
+
+def _pattern_case():
+    z = np.load(os.path.join(HERE, "golden", "poisson2d_16.npz"), allow_pickle=False)
+    n = int(z["n"])
+    A = sp.csc_matrix((z["A_data"], z["A_indices"], z["A_indptr"]), shape=(n, n))
+    L = sp.csc_matrix((z["L_data"], z["L_indices"], z["L_indptr"]), shape=(n, n))
+    U = sp.csc_matrix((z["U_data"], z["U_indices"], z["U_indptr"]), shape=(n, n))
+    return z, n, A, L, U
+
+
+def test_given_pattern_with_dropped_fill(gpu):
+    # UMFPACK leaves out fill entries that came out exactly zero: a given pattern that is a strict
+    # subset of the structural fill is accepted, F.L / F.U come back on exactly that pattern with
+    # the factor values at its positions, and pattern_dropped counts what it left out
+    z, n, A, L, U = _pattern_case()
+    keepL = np.ones(L.nnz, bool)
+    Lc = L.tocoo()
+    off = np.flatnonzero(Lc.row != Lc.col)
+    keepL[off[::7]] = False          # every 7th strictly-lower entry of the fixture's L
+    L2 = sp.csc_matrix((Lc.data[keepL], (Lc.row[keepL], Lc.col[keepL])), shape=(n, n))
+    Uc = U.tocoo()
+    keepU = np.ones(U.nnz, bool)
+    offu = np.flatnonzero(Uc.row != Uc.col)
+    keepU[offu[::5]] = False
+    U2 = sp.csc_matrix((Uc.data[keepU], (Uc.row[keepU], Uc.col[keepU])), shape=(n, n))
+    F = smlu.ParallelSparseLU(A, p=z["p"], q=z["q"], L_pattern=L2, U_pattern=U2)
+    assert F.stat("pattern_dropped") == (L.nnz - L2.nnz) + (U.nnz - U2.nnz)
+    for G, R, P in ((F.L, L, L2), (F.U, U, U2)):
+        P = sp.csc_matrix(P)
+        P.sort_indices()
+        assert np.array_equal(G.indptr, P.indptr) and np.array_equal(G.indices, P.indices)
+        # values at the kept positions are the factor's own
+        Rk = R.multiply(P != 0).tocsc()
+        Rk.sort_indices()
+        assert abs(G - Rk).max() <= 1e-11 * max(1.0, abs(R).max())
+    F.close()
+
+
+@pytest.mark.parametrize("bad", ["outside_fill", "no_diagonal", "upper_in_L"])
+def test_given_pattern_rejected(gpu, bad):
+    z, n, A, L, U = _pattern_case()
+    L2 = L.tolil()
+    if bad == "outside_fill":
+        # an entry the structural fill of (Rs.*A)[p, q] does not have
+        Ld = L.toarray() != 0
+        i, j = np.argwhere(~Ld & np.tri(n, k=-1, dtype=bool))[0]
+        L2[i, j] = 1.0
+    elif bad == "no_diagonal":
+        L2[3, 3] = 0.0
+    else:
+        L2[0, 5] = 1.0
+    L2 = sp.csc_matrix(L2)
+    L2.eliminate_zeros()
+    with pytest.raises(smlu.SmluError) as ei:
+        smlu.ParallelSparseLU(A, p=z["p"], q=z["q"], L_pattern=L2, U_pattern=U)
+    assert "(-7)" in str(ei.value)
