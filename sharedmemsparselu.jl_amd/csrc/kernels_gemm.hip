@@ -666,7 +666,7 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_dst) {
 }
 
 
-template <bool TRSM, bool PRIO, bool EB>
+template <bool TRSM, bool EB>
 __device__ __forceinline__ void gemm128_mfma3_interior(const GemmTask& t, int m0, int n0, Mfma3Lds& S,
                                                        const GrowthArgs& ga) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -745,14 +745,12 @@ __device__ __forceinline__ void gemm128_mfma3_interior(const GemmTask& t, int m0
     double fb0[4], fb1[4];
     frags(cur, 0, fa0, fb0);
     frags(cur, 1, fa1, fb1);
-    if (PRIO) __builtin_amdgcn_s_setprio(1);
     quad(fa0, fb0);
     frags(cur, 2, fa0, fb0);
     quad(fa1, fb1);
     frags(cur, 3, fa1, fb1);
     quad(fa0, fb0);
     quad(fa1, fb1);
-    if (PRIO) __builtin_amdgcn_s_setprio(0);
   };
   const int nk = (K + HBK_ - 1) / HBK_;
   const int nfull = K / HBK_;
@@ -782,13 +780,11 @@ __device__ __forceinline__ void gemm128_mfma3_interior(const GemmTask& t, int m0
       if (next_full) issue((kt + 1) * HBK_, cur ^ 1);
       if (next && !next_full) stage_tail((kt + 1) * HBK_, cur ^ 1);
       frags(cur, 1, fa1, fb1);
-      if (PRIO) __builtin_amdgcn_s_setprio(1);
       quad(fa0, fb0);
       frags(cur, 2, fa0, fb0);
       quad(fa1, fb1);
       frags(cur, 3, fa1, fb1);
       quad(fa0, fb0);
-      if (PRIO) __builtin_amdgcn_s_setprio(0);
       if (next) {
         __syncthreads();
         frags(cur ^ 1, 0, fa0, fb0);
@@ -810,7 +806,7 @@ __device__ __forceinline__ void gemm128_mfma3_interior(const GemmTask& t, int m0
   if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
 }
 
-template <bool TRSM, bool PRIO = false, bool EB = false>
+template <bool TRSM, bool EB = false>
 __global__ __launch_bounds__(256, 2) void k_gemm128_mfma3(const GemmTask* __restrict__ tasks, int ntask,
                                                           GrowthArgs ga) {
   __shared__ __attribute__((aligned(16))) double lds[sizeof(Mfma3Lds) / sizeof(double)];
@@ -820,214 +816,11 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma3(const GemmTask* __rest
   tile_rc<HBM_>(t, b - t.tile0, tm, tn);
   const int m0 = tm * HBM_, n0 = tn * HBM_;
   if (m0 + HBM_ <= t.m && n0 + HBM_ <= t.n) {
-    gemm128_mfma3_interior<TRSM, PRIO, EB>(t, m0, n0, *reinterpret_cast<Mfma3Lds*>(lds), ga);
+    gemm128_mfma3_interior<TRSM, EB>(t, m0, n0, *reinterpret_cast<Mfma3Lds*>(lds), ga);
   } else {
     auto& As = *reinterpret_cast<double(*)[2][HBK_][HBM_]>(lds);
     auto& Bs = *reinterpret_cast<double(*)[2][HBK_][HLDB_]>(lds + 2 * HBK_ * HBM_);
     gemm128_mfma_body<TRSM, false>(t, m0, n0, As, Bs, ga);
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// MFMA tile v4 (tile code 132): 256 x 128 output tile per 256-thread workgroup, one workgroup per
-// CU.  Each wave owns a 128 x 64 quadrant (8 x 4 blocks of v_mfma_f64_16x16x4: 256 accumulator
-// registers, which the compiler places in the AGPRs), so a 16-deep K slice is 128 MFMAs per wave
-// against 12 fragment reads per 32 MFMAs.  Three LDS stages (48 KB each: A [k][256], B [col][k]
-// pair-swizzled as in v3) filled by LDS-DMA two slices ahead: the DMA of slice t + 2 is issued at
-// the top of slice t, and the end-of-slice wait is a counted vmcnt that leaves it in flight
-// across the barrier (raw s_barrier: __syncthreads would drain it).  Same per-element arithmetic
-// as v2 / v3 (acc = C, one MFMA-FMA per k ascending, B negated by the MFMA's neg modifier).
-// Interior tiles only; an edge tile runs as two 128 x 128 halves of gemm128_mfma_body<.., false>.
-// ------------------------------------------------------------------------------------
-#define V4M 256
-#define V4N 128
-struct Mfma4Lds {
-  double A[3][HBK_][V4M];   // [stage][k][row]
-  double B[3][V4N][HBK_];   // [stage][col][k, pair-swizzled]
-};
-static_assert(sizeof(Mfma4Lds) == 147456, "v4 tile LDS image");
-
-template <int TM, int TN>
-__device__ __forceinline__ void tile_rc2(const GemmTask& t, int64_t tl, int& tm, int& tn) {
-  constexpr int GM = 8;
-  const int64_t tiles_n = (t.n + TN - 1) / TN;
-  const int64_t g = tl / (GM * tiles_n);
-  const int first = (int)(g * GM);
-  const int gm = min(GM, t.tiles_m - first);
-  const int64_t in = tl - g * GM * tiles_n;
-  tm = first + (int)(in % gm);
-  tn = (int)(in / gm);
-}
-
-template <bool TRSM, bool EARLYBAR>
-__device__ __forceinline__ void gemm256_mfma4_interior(const GemmTask& t, int m0, int n0, Mfma4Lds& S,
-                                                       const GrowthArgs& ga) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = (wv & 1) * 128, wc = (wv >> 1) * 64;
-  const int li = lane & 15, lk = lane >> 4;
-  const int K = t.k;
-  const int64_t lda = t.lda, ldb = t.ldb, ldc = t.ldc;
-  const uint32_t c_lo = (uint32_t)(((int64_t)lk * ldc + 2 * li) * 8);
-  auto cbase = [&](int ip, int j, int r) {
-    return reinterpret_cast<char*>(t.C) + ((int64_t)(n0 + wc + 16 * j + 4 * r) * ldc + m0 + wr + 32 * ip) * 8;
-  };
-  // DMA sources.  A: wave wv stages k-rows wv + 4q, both 128-row halves (8 instructions);
-  // B: as v3 (columns 8 (wv + 4q) + (lane >> 3), pair (lane & 7) ^ ((4 wv + (lane >> 4)) & 7)).
-  const int bpair = (lane & 7) ^ ((4 * wv + (lane >> 4)) & 7);
-  const char* asrc = reinterpret_cast<const char*>(t.A) + ((int64_t)wv * lda + m0 + 2 * lane) * 8;
-  const char* bsrc = reinterpret_cast<const char*>(t.B) + ((int64_t)(n0 + 8 * wv + (lane >> 3)) * ldb + 2 * bpair) * 8;
-  auto issue = [&](int k0, int st) {   // 12 DMA per wave
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        glds16(asrc + ((int64_t)(k0 + 4 * q) * lda + 128 * h) * 8, &S.A[st][wv + 4 * q][128 * h]);
-      glds16(bsrc + ((int64_t)32 * q * ldb + k0) * 8, &S.B[st][8 * (wv + 4 * q)][0]);
-    }
-  };
-  auto stage_tail = [&](int k0, int st) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int ka = k0 + wv + 4 * q;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const v2d a = ka < K ? ldu2(asrc + ((int64_t)(k0 + 4 * q) * lda + 128 * h) * 8, 0) : v2d{0.0, 0.0};
-        *reinterpret_cast<v2d*>(&S.A[st][wv + 4 * q][128 * h + 2 * lane]) = a;
-      }
-      const gdbl* bp = gbl(reinterpret_cast<const double*>(bsrc + ((int64_t)32 * q * ldb + k0) * 8));
-      const int kb = k0 + 2 * bpair;
-      v2d b;
-      b.x = kb < K ? bp[0] : 0.0;
-      b.y = kb + 1 < K ? bp[1] : 0.0;
-      *reinterpret_cast<v2d*>(&S.B[st][8 * (wv + 4 * q)][2 * lane]) = b;
-    }
-  };
-  v4d acc[8][4];
-#pragma unroll
-  for (int ip = 0; ip < 4; ++ip)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const v2d c = ldu2(cbase(ip, j, r), c_lo);
-        acc[2 * ip][j][r] = c.x;
-        acc[2 * ip + 1][j][r] = c.y;
-      }
-  const int a_off = (lk * V4M + wr + 2 * li);
-  int b_off[4];
-#pragma unroll
-  for (int kq = 0; kq < 4; ++kq) b_off[kq] = (wc + li) * HBK_ + (((2 * kq + (lk >> 1)) ^ (li >> 1)) << 1) + (lk & 1);
-  auto frags = [&](int st, int kq, v2d (&fa)[4], double (&fb)[4]) {
-    const double* As = &S.A[st][0][0] + a_off + kq * 4 * V4M;
-    const double* Bs = &S.B[st][0][0] + b_off[kq];
-#pragma unroll
-    for (int ip = 0; ip < 4; ++ip) fa[ip] = *reinterpret_cast<const v2d*>(As + 32 * ip);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = Bs[16 * HBK_ * j];
-  };
-  auto quad = [&](const v2d (&fa)[4], const double (&fb)[4]) {
-#pragma unroll
-    for (int ip = 0; ip < 4; ++ip)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[2 * ip][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[j], fa[ip].x, acc[2 * ip][j], 0, 0, 1);
-        acc[2 * ip + 1][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[j], fa[ip].y, acc[2 * ip + 1][j], 0, 0, 1);
-      }
-  };
-  auto slice = [&](int st) {
-    v2d fa0[4], fa1[4];
-    double fb0[4], fb1[4];
-    frags(st, 0, fa0, fb0);
-    frags(st, 1, fa1, fb1);
-    quad(fa0, fb0);
-    frags(st, 2, fa0, fb0);
-    quad(fa1, fb1);
-    frags(st, 3, fa1, fb1);
-    quad(fa0, fb0);
-    quad(fa1, fb1);
-  };
-  const int nk = (K + HBK_ - 1) / HBK_;
-  const int nfull = K / HBK_;
-  auto stage = [&](int kt) {   // slice kt into stage kt % 3; returns the DMA count it left in flight
-    if (kt < nfull) { issue(kt * HBK_, kt % 3); return 12; }
-    stage_tail(kt * HBK_, kt % 3);
-    return 0;
-  };
-  auto wait_landed = [&](int inflight) {   // every DMA but the last `inflight` ones landed
-    if (inflight == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-  stage(0);
-  int fl = 0;
-  if (nk > 1) fl = stage(1);
-  wait_landed(fl);
-  if (!EARLYBAR) {
-    for (int kt = 0; kt < nk; ++kt) {
-      int f2 = 0;
-      if (kt + 2 < nk) f2 = stage(kt + 2);
-      slice(kt % 3);
-      if (kt + 1 < nk) wait_landed(f2);
-    }
-  } else {
-    // the barrier of slice kt + 1 sits between the MFMAs of k-quads 2 and 3 of slice kt (all of
-    // slice kt's fragment reads are in registers by then), and slice kt + 1's first fragments are
-    // read behind quad 3's MFMAs: no LDS latency and no barrier in front of an empty MFMA queue
-    v2d fa0[4], fa1[4];
-    double fb0[4], fb1[4];
-    frags(0, 0, fa0, fb0);
-    for (int kt = 0; kt < nk; ++kt) {
-      const int st = kt % 3;
-      int f2 = 0;
-      if (kt + 2 < nk) f2 = stage(kt + 2);
-      frags(st, 1, fa1, fb1);
-      quad(fa0, fb0);
-      frags(st, 2, fa0, fb0);
-      quad(fa1, fb1);
-      frags(st, 3, fa1, fb1);
-      quad(fa0, fb0);
-      if (kt + 1 < nk) {
-        wait_landed(f2);
-        frags((kt + 1) % 3, 0, fa0, fb0);
-      }
-      quad(fa1, fb1);
-    }
-  }
-  double gmax = 0.0;
-#pragma unroll
-  for (int ip = 0; ip < 4; ++ip)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const v2d c = v2d{acc[2 * ip][j][r], acc[2 * ip + 1][j][r]};
-        stu2(cbase(ip, j, r), c_lo, c);
-        if (TRSM) gmax = fmax(gmax, fmax(fabs(c.x), fabs(c.y)));
-      }
-  if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
-}
-
-template <bool TRSM, bool EARLYBAR>
-__global__ __launch_bounds__(256, 1) void k_gemm256_mfma4(const GemmTask* __restrict__ tasks, int ntask,
-                                                          GrowthArgs ga) {
-  __shared__ __attribute__((aligned(16))) double lds[sizeof(Mfma4Lds) / sizeof(double)];
-  const int64_t b = xcd_window_remap(blockIdx.x, gridDim.x);
-  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
-  int tm, tn;
-  tile_rc2<V4M, V4N>(t, b - t.tile0, tm, tn);
-  const int m0 = tm * V4M, n0 = tn * V4N;
-  if (m0 + V4M <= t.m && n0 + V4N <= t.n) {
-    gemm256_mfma4_interior<TRSM, EARLYBAR>(t, m0, n0, *reinterpret_cast<Mfma4Lds*>(lds), ga);
-  } else {
-    auto& As = *reinterpret_cast<double(*)[2][HBK_][HBM_]>(lds);
-    auto& Bs = *reinterpret_cast<double(*)[2][HBK_][HLDB_]>(lds + 2 * HBK_ * HBM_);
-    gemm128_mfma_body<TRSM, false>(t, m0, n0, As, Bs, ga);
-    if (m0 + HBM_ < t.m) {
-      __syncthreads();
-      gemm128_mfma_body<TRSM, false>(t, m0 + HBM_, n0, As, Bs, ga);
-    }
   }
 }
 
@@ -1310,13 +1103,8 @@ hipError_t launch_gemm_g(hipStream_t st, int64_t ntiles, const GemmTask* tasks, 
   if (ntiles <= 0) return hipSuccess;
   const GrowthArgs ga{info, growth, piv_tol};
   const bool trsm = info != nullptr;
-  if (tile == 132 && trsm) k_gemm256_mfma4<true, false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 132) k_gemm256_mfma4<false, false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 133 && trsm) k_gemm256_mfma4<true, true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 133) k_gemm256_mfma4<false, true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 134) k_gemm128_mfma3<false, true, false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 135) k_gemm128_mfma3<false, false, true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 136) k_gemm128_mfma3<false, true, true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  if (tile == 135 && trsm) k_gemm128_mfma3<true, true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  else if (tile == 135) k_gemm128_mfma3<false, true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 131 && trsm) k_gemm128_mfma3<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 131) k_gemm128_mfma3<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 130 && trsm) k_gemm128_mfma2<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);

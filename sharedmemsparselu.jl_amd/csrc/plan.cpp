@@ -16,6 +16,8 @@
 #include <cstring>
 #include <numeric>
 #include <stdexcept>
+#include <thread>
+#include <atomic>
 
 #include "plan.hpp"
 
@@ -34,6 +36,46 @@ int64_t Plan::local_index(int64_t s, int64_t g) const {
 }
 
 namespace {
+
+// Host threads for the analysis (bounded: the 256^3 plan is built on every rank of a node).
+int plan_threads() {
+  static const int t = (int)std::min(32u, std::max(1u, std::thread::hardware_concurrency()));
+  return t;
+}
+
+// f(lo, hi) over [0, n) in contiguous chunks on plan_threads() threads.
+template <class F>
+void parallel_for(int64_t n, F&& f, int64_t grain = 65536) {
+  const int T = (int)std::min<int64_t>(plan_threads(), std::max<int64_t>(1, n / grain));
+  if (T <= 1) { f((int64_t)0, n); return; }
+  std::vector<std::thread> th;
+  th.reserve(T - 1);
+  for (int t = 1; t < T; ++t) th.emplace_back([&f, n, T, t] { f(n * t / T, n * (t + 1) / T); });
+  f((int64_t)0, n / T);
+  for (auto& x : th) x.join();
+}
+
+// std::sort of [b, e) in parallel chunks merged pairwise (same result as std::sort for a strict
+// weak order whose equivalent elements are identical, e.g. distinct keys).
+template <class It, class Cmp>
+void parallel_sort(It b, It e, Cmp cmp) {
+  const int64_t n = e - b;
+  const int T = (int)std::min<int64_t>(plan_threads(), std::max<int64_t>(1, n / 262144));
+  if (T <= 1) { std::sort(b, e, cmp); return; }
+  std::vector<int64_t> cut(T + 1);
+  for (int t = 0; t <= T; ++t) cut[t] = n * t / T;
+  parallel_for(T, [&](int64_t lo, int64_t hi) {
+    for (int64_t t = lo; t < hi; ++t) std::sort(b + cut[t], b + cut[t + 1], cmp);
+  }, 1);
+  for (int w = 1; w < T; w *= 2) {
+    std::vector<std::thread> th;
+    for (int t = 0; t + w < T; t += 2 * w) {
+      const int64_t lo = cut[t], mid = cut[t + w], hi = cut[std::min(T, t + 2 * w)];
+      th.emplace_back([=] { std::inplace_merge(b + lo, b + mid, b + hi, cmp); });
+    }
+    for (auto& x : th) x.join();
+  }
+}
 
 // Elimination tree of the symmetric pattern in the new labels (Liu, path compression).
 std::vector<int64_t> etree_sym(const Graph& g, const std::vector<int64_t>& q,
@@ -116,6 +158,12 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
                         const PlanOptions& opt, const int64_t* pgiven, const int64_t* qgiven,
                         const int64_t* rowmatch) {
   auto t0 = std::chrono::steady_clock::now();
+  auto tp = t0;
+  auto phase = [&](int i) {
+    const auto t = std::chrono::steady_clock::now();
+    phase_ms[i] += std::chrono::duration<double, std::milli>(t - tp).count();
+    tp = t;
+  };
   n = n_;
   if (n <= 0) return "n must be positive";
   if (n >= (int64_t)INT32_MAX) return "n too large for int32 row indices";
@@ -150,6 +198,7 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
     for (int64_t j = 0; j <= n && sym_pattern; ++j) sym_pattern = cnt[j] == Acolptr[j];
     for (int64_t e = 0; e < nnzA && sym_pattern; ++e) sym_pattern = tr[e] == Arow[e];
   }
+  phase(0);
   Graph g = build_sym_graph(n, Acolptr.data(), Arow.data());
   // Row pre-permutation from a transversal (match[c] = row of A placed at column c's
   // diagonal): the fronts are built on pattern(B + B') with B = A[match, :], labelled by columns.
@@ -170,6 +219,7 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
     g = build_sym_graph(n, bptr.data(), brow.data());
   }
 
+  phase(1);
   // ---- ordering ----
   given_order = (pgiven != nullptr && qgiven != nullptr);
   std::vector<int64_t> ord;
@@ -220,6 +270,7 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
     p0 = pv;
   }
 
+  phase(2);
   q = ord;
   qinv.assign(n, 0);
   for (int64_t k = 0; k < n; ++k) qinv[q[k]] = k;
@@ -227,12 +278,15 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
   // ---- elimination tree + postorder ----
   std::vector<int64_t> parent = etree_sym(g, q, qinv);
   if (!given_order) {
+    // postorder: an equivalent order whose etree is the same tree relabelled (no second pass)
     std::vector<int64_t> post = postorder(parent);
-    std::vector<int64_t> q2(n);
+    std::vector<int64_t> q2(n), pinv(n), parent2(n);
     for (int64_t k = 0; k < n; ++k) q2[k] = q[post[k]];
+    for (int64_t k = 0; k < n; ++k) pinv[post[k]] = k;
+    for (int64_t k = 0; k < n; ++k) parent2[k] = parent[post[k]] < 0 ? -1 : pinv[parent[post[k]]];
     q.swap(q2);
+    parent.swap(parent2);
     for (int64_t k = 0; k < n; ++k) qinv[q[k]] = k;
-    parent = etree_sym(g, q, qinv);
   }
   if (!given_order) p0 = q;
   if (matched)
@@ -240,6 +294,7 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
   p0inv.assign(n, 0);
   for (int64_t k = 0; k < n; ++k) p0inv[p0[k]] = k;
 
+  phase(3);
   // ---- column counts (Gilbert-Ng-Peyton), labels are (post)ordered: parent > child ----
   std::vector<int64_t> cc(n, 0);
   {
@@ -300,6 +355,7 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
     }
   }
 
+  phase(4);
   // ---- exact supernodes: j, j+1 together iff parent[j]==j+1 && cc[j]==cc[j+1]+1 ----
   // For given non-postordered orders cc is unknown; compute exact structures column by
   // column with the symbolic "row structure" walk restricted to supernode detection.
@@ -335,7 +391,63 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
       if (t_parent[t] != -1) tch[pos[t_parent[t]]++] = (int32_t)t;
   }
   // row structures R_t = (union of A pattern of t's columns, rows > last) U (children R \ cols(t))
-  {
+  if (have_cc) {
+    // |R_t| = cc[last] - 1 is known: every t writes its own slice of t_rows, all t of one height
+    // in the t-supernode tree at once (children are lower), thread-local marks
+    t_rowptr.assign(ntsup + 1, 0);
+    for (int64_t t = 0; t < ntsup; ++t) t_rowptr[t + 1] = t_rowptr[t] + (cc[t_first[t + 1] - 1] - 1);
+    t_rows.assign(t_rowptr[ntsup], 0);
+    std::vector<int32_t> height(ntsup, 0);
+    int32_t hmax = 0;
+    for (int64_t t = 0; t < ntsup; ++t) {
+      for (int64_t k = tch_ptr[t]; k < tch_ptr[t + 1]; ++k) height[t] = std::max(height[t], height[tch[k]] + 1);
+      hmax = std::max(hmax, height[t]);
+    }
+    std::vector<int64_t> hptr(hmax + 2, 0), hlist(ntsup);
+    for (int64_t t = 0; t < ntsup; ++t) hptr[height[t] + 1]++;
+    for (int32_t h2 = 0; h2 <= hmax; ++h2) hptr[h2 + 1] += hptr[h2];
+    {
+      std::vector<int64_t> pos(hptr.begin(), hptr.end() - 1);
+      for (int64_t t = 0; t < ntsup; ++t) hlist[pos[height[t]]++] = t;
+    }
+    std::atomic<bool> bad{false};
+    const int T = plan_threads();
+    std::vector<std::vector<int32_t>> marks(T);
+    std::atomic<int> slot{0};
+    for (int32_t h2 = 0; h2 <= hmax; ++h2) {
+      const int64_t lo0 = hptr[h2], cnt = hptr[h2 + 1] - hptr[h2];
+      slot = 0;
+      parallel_for(cnt, [&](int64_t lo, int64_t hi) {
+        const int me = slot++;
+        std::vector<int32_t>& mark = marks[me];
+        if (mark.empty()) mark.assign(n, -1);
+        std::vector<int32_t> buf;
+        for (int64_t x = lo; x < hi; ++x) {
+          const int64_t t = hlist[lo0 + x];
+          const int64_t f = t_first[t], l = t_first[t + 1] - 1;
+          buf.clear();
+          for (int64_t j = f; j <= l; ++j) {
+            int64_t u = q[j];
+            for (int64_t e = g.ptr[u]; e < g.ptr[u + 1]; ++e) {
+              int64_t i = qinv[g.adj[e]];
+              if (i > l && mark[i] != (int32_t)t) { mark[i] = (int32_t)t; buf.push_back((int32_t)i); }
+            }
+          }
+          for (int64_t k = tch_ptr[t]; k < tch_ptr[t + 1]; ++k) {
+            int64_t c = tch[k];
+            for (int64_t e = t_rowptr[c]; e < t_rowptr[c + 1]; ++e) {
+              int64_t i = t_rows[e];
+              if (i > l && mark[i] != (int32_t)t) { mark[i] = (int32_t)t; buf.push_back((int32_t)i); }
+            }
+          }
+          if ((int64_t)buf.size() != t_rowptr[t + 1] - t_rowptr[t]) { bad = true; continue; }
+          std::sort(buf.begin(), buf.end());
+          std::copy(buf.begin(), buf.end(), t_rows.begin() + t_rowptr[t]);
+        }
+      }, 2048);
+    }
+    if (bad) return "internal: column count mismatch";
+  } else {
     t_rowptr.assign(ntsup + 1, 0);
     t_rows.clear();
     std::vector<int64_t> mark(n, -1);
@@ -365,6 +477,7 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
     }
   }
 
+  phase(5);
   // exact structural counts + update count
   nnzL = 0;
   upd = 0;
@@ -442,6 +555,7 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
     r_first.swap(rf);
     r_parent_t.swap(rt);   // top t-supernode of each relaxed supernode
   }
+  phase(6);
   nsup = (int64_t)r_first.size();
   s_first.assign(nsup + 1, 0);
   for (int64_t s = 0; s < nsup; ++s) s_first[s] = r_first[s];
@@ -520,6 +634,7 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
     }
   }
 
+  phase(7);
   // ---- HBM layout ----
   auto align = [](int64_t x) { return (x + 15) & ~int64_t(15); };
   Loff.assign(nsup, 0);
@@ -598,31 +713,38 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
       if (Foff[s] >= 0) Foff[s] += lev_soff[s_level[s]];
   }
 
+  phase(8);
   // ---- A map ----
   Adest.assign(nnzA, 0);
   A_s.assign(nnzA, 0);
   A_li.assign(nnzA, 0);
   A_lj.assign(nnzA, 0);
   std::vector<int> ent_level(nnzA, 0);
-  for (int64_t c = 0; c < n; ++c) {
-    int64_t pc = qinv[c];
-    for (int64_t e = Acolptr[c]; e < Acolptr[c + 1]; ++e) {
-      int64_t pr = p0inv[Arow[e]];
-      int64_t k = std::min(pr, pc);
-      int64_t s = col2s[k];
-      int64_t li = local_index(s, pr), lj = local_index(s, pc);
-      if (li < 0 || lj < 0) return "internal: A entry outside its front";
-      int64_t a = ns(s), m = M(s);
-      int64_t dest;
-      if (lj < a) dest = Loff[s] + lj * m + li;
-      else if (li < a) dest = Uoff[s] + (lj - a) * a + li;
-      else dest = -1 - (Foff[s] + (lj - a) * (m - a) + (li - a));
-      Adest[e] = dest;
-      A_s[e] = (int32_t)s;
-      A_li[e] = (int32_t)li;
-      A_lj[e] = (int32_t)lj;
-      ent_level[e] = s_level[s];
-    }
+  {
+    std::atomic<bool> outside{false};
+    parallel_for(n, [&](int64_t c0, int64_t c1) {
+      for (int64_t c = c0; c < c1; ++c) {
+        int64_t pc = qinv[c];
+        for (int64_t e = Acolptr[c]; e < Acolptr[c + 1]; ++e) {
+          int64_t pr = p0inv[Arow[e]];
+          int64_t k = std::min(pr, pc);
+          int64_t s = col2s[k];
+          int64_t li = local_index(s, pr), lj = local_index(s, pc);
+          if (li < 0 || lj < 0) { outside = true; continue; }
+          int64_t a = ns(s), m = M(s);
+          int64_t dest;
+          if (lj < a) dest = Loff[s] + lj * m + li;
+          else if (li < a) dest = Uoff[s] + (lj - a) * a + li;
+          else dest = -1 - (Foff[s] + (lj - a) * (m - a) + (li - a));
+          Adest[e] = dest;
+          A_s[e] = (int32_t)s;
+          A_li[e] = (int32_t)li;
+          A_lj[e] = (int32_t)lj;
+          ent_level[e] = s_level[s];
+        }
+      }
+    }, 4096);
+    if (outside) return "internal: A entry outside its front";
   }
   Alev_ptr.assign(nlevels + 1, 0);
   for (int64_t e = 0; e < nnzA; ++e) Alev_ptr[ent_level[e] + 1]++;
@@ -631,9 +753,10 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
   {
     std::vector<int64_t> pos(Alev_ptr.begin(), Alev_ptr.end() - 1);
     for (int64_t e = 0; e < nnzA; ++e) Alev_ent[pos[ent_level[e]]++] = (int32_t)e;
+    // front slots are distinct: a strict order, so the parallel sort equals std::sort
     for (int l = 0; l < nlevels; ++l)
-      std::sort(Alev_ent.begin() + Alev_ptr[l], Alev_ent.begin() + Alev_ptr[l + 1],
-                [&](int32_t a, int32_t b) { return Adest[a] < Adest[b]; });
+      parallel_sort(Alev_ent.begin() + Alev_ptr[l], Alev_ent.begin() + Alev_ptr[l + 1],
+                    [&](int32_t a, int32_t b) { return Adest[a] < Adest[b]; });
   }
   // rows of A (for the row scaling kernel)
   Arowptr.assign(n + 1, 0);
@@ -645,6 +768,7 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
     for (int64_t c = 0; c < n; ++c)
       for (int64_t e = Acolptr[c]; e < Acolptr[c + 1]; ++e) Arow_ent[pos[Arow[e]]++] = (int32_t)e;
   }
+  phase(9);
   analysis_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return "";
 }

@@ -754,8 +754,10 @@ static int build_schedule(smlu_handle* h) {
   if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
   if (const char* e = std::getenv("SMLU_T128MIN")) h->t128_min = std::atoll(e);
   h->small_k = !(std::getenv("SMLU_SMALLK") && std::atoi(std::getenv("SMLU_SMALLK")) == 0);
-  // MFMA 128 tile: code 130 (v2: 16-byte operand traffic, kernels_gemm.hip)
-  const int mfma_tile = 130;
+  // MFMA 128 tile: code 131 (v3: LDS-DMA staging, kernels_gemm.hip); the F22 launches (k = ns, the
+  // long-k shapes) take 135, the same tile with the next slice's barrier between its last two
+  // k-quads (+3 % at k >= 2048, neutral at the k = 384 trailing shapes: tools/gemm_bench)
+  const int mfma_tile = 131;
   // GEMM-form TRSM (k_tri_inv + GEMM tasks) needs the growth epilogue of the MFMA/64 tiles
   {
     const char* e = std::getenv("SMLU_TRSM_GEMM");
@@ -821,6 +823,7 @@ static int build_schedule(smlu_handle* h) {
     for (auto& g : cand) t128 += (int64_t)((g.m + 127) / 128) * ((g.n + 127) / 128);
     int tile = t128 >= h->t128_min ? 128 : 64;
     if (tile == 128 && h->opts.use_mfma) tile = mfma_tile;   // fp64 MFMA variant of the 128 tile
+    if (tile == 131 && step < 0) tile = 135;
     if (tile == 64 && h->small_k) {                    // every k <= 64: one-shot K staging
       int kmax = 0;
       for (auto& g : cand) kmax = std::max(kmax, g.k);
@@ -4396,6 +4399,10 @@ int64_t smlu_last_error_col(const smlu_handle* h) {
 }
 
 static double plan_stat(const Plan& P, const std::string& k) {
+  if (k.rfind("phase_ms", 0) == 0) {   // phase_ms0 .. phase_ms9 (Plan::phase_ms)
+    const int i = std::atoi(k.c_str() + 8);
+    return i >= 0 && i < 10 ? P.phase_ms[i] : std::numeric_limits<double>::quiet_NaN();
+  }
   if (k == "n") return (double)P.n;
   if (k == "nnzA") return (double)P.nnzA;
   if (k == "nsuper") return (double)P.nsup;
@@ -4483,8 +4490,9 @@ double smlu_stat(const smlu_handle* h, const char* key) {
     for (const Launch& L : h->fac) {
       const bool gemm = L.kind == K_GEMM || L.kind == K_GEMMU || L.kind == K_GEMMO || L.kind == K_GEMM22;
       const bool trsm = L.kind == K_TRSML;
-      if (v == "mfma128" && gemm && L.aux == 130) ++c;
-      else if (v == "mfma128_trsm" && trsm && L.aux == 130) ++c;
+      const bool mfma = L.aux == 130 || L.aux == 131 || L.aux == 135;
+      if (v == "mfma128" && gemm && mfma) ++c;
+      else if (v == "mfma128_trsm" && trsm && mfma) ++c;
       else if (v == "valu128" && gemm && L.aux == 128) ++c;
       else if (v == "k64" && gemm && L.aux == 65) ++c;
       else if (v == "k64_trsm" && trsm && L.aux == 65) ++c;

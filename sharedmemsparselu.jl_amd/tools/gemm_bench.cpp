@@ -47,7 +47,7 @@ int main(int argc, char** argv) {
       int tile = tiles_list[variant];
       double* C = variant == 0 ? C1 : C2;
       GemmTask t{}; t.A = A; t.B = B; t.C = C; t.m = m; t.n = n; t.k = k; t.lda = lda; t.ldb = ldb; t.ldc = ldc;
-      const int tsm = (tile == 132 || tile == 133) ? 256 : tile >= 128 ? 128 : 64, tsn = tile >= 128 ? 128 : 64;
+      const int tsm = tile >= 128 ? 128 : 64, tsn = tsm;
       t.tiles_m = (m + tsm - 1) / tsm; t.tile0 = 0;
       int64_t tiles = (int64_t)t.tiles_m * ((n + tsn - 1) / tsn);
       CK(hipMemcpy(dt, &t, sizeof t, hipMemcpyHostToDevice));
