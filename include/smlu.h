@@ -32,12 +32,12 @@ extern "C" {
 #define SMLU_SINGULAR           1   /* zero pivot column (UMFPACK SingularException, src/SharedMemSparseLU.jl:74) */
 #define SMLU_PIVOT_WEAK         2   /* a pivot failed the threshold test (growth > 1/pivot_tol) */
 #define SMLU_ERR_ARG          (-1)  /* bad argument / DimensionMismatch (src/SharedMemSparseLU.jl:288-290) */
-#define SMLU_ERR_PATTERN      (-2)  /* refactor called with a different sparsity pattern */
+#define SMLU_ERR_PATTERN      (-2)  /* refactor called with a different sparsity pattern, or a given L/U
+                                       pattern outside the structural fill of (Rs.*A)[p,q] */
 #define SMLU_ERR_ALLOC        (-3)  /* host or device allocation failed */
 #define SMLU_ERR_HIP          (-4)  /* HIP runtime error */
 #define SMLU_ERR_NODEVICE     (-5)  /* no gfx950 device visible: the library never falls back to the CPU */
 #define SMLU_ERR_STATE        (-6)  /* handle has no numeric factorization / illegal device status */
-#define SMLU_ERR_PATTERN      (-7)  /* a given L/U pattern is not the structural fill of (Rs.*A)[p,q] */
 
 /* ---- ordering choices ------------------------------------------------------------- */
 #define SMLU_ORDER_AUTO         0   /* geometric ND if grid[] given, else graph nested dissection */

@@ -40,14 +40,15 @@ struct GemmTask {
   int64_t tile0;
 };
 
-// Fused U rows of an outer block (k_urows): one 64-column block of the columns right of the
-// block; rows [ob0, ob1) of the block solved sub-panel by sub-panel (tinv slots slot0 + u).
+// Fused U rows of an outer block (k_urows): one kUrowsCols-column block of the columns right of
+// the block; rows [ob0, ob1) of the block solved sub-panel by sub-panel (tinv slots slot0 + u).
+constexpr int kUrowsCols = 32;
 struct URowTask {
   int32_t s;
   int32_t ob0, ob1;
   int32_t slot0;
   int32_t ld;      // M for L-panel columns, ns for U12 columns
-  int32_t ncols;   // <= 64
+  int32_t ncols;   // <= kUrowsCols
   int64_t coff;    // store offset of (row 0, first column) of the block
 };
 

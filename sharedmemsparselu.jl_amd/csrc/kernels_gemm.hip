@@ -826,192 +826,147 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma3(const GemmTask* __rest
 
 // ------------------------------------------------------------------------------------
 // U rows of an outer block, fused (the end-of-block step of the GEMM-form fronts).  One
-// 256-thread workgroup per 64-column block of the columns right of the block (L-panel columns or
-// U12 columns) runs the whole sub-panel sequence on its columns; for each 64-row sub-panel u:
-//   T: C_u = L_uu^-1 C_u in GEMM form, C_u - NL_u C_u (NL_u = I - L_uu^-1, tinv slot0 + u);
-//   R: the rows below u inside the block, C_r -= L_ru C_u (k = 64), with -C_u kept in LDS.
-// These are exactly the K_TRSML + K_GEMMU tiles it replaces, with the same per-element
-// arithmetic (acc = C, then one fused multiply-add per k in ascending k: the fp64 MFMA does
-// them in order), so the factors are bitwise those of the per-sub-panel launches.  fp64 MFMA
-// 16x16x4 with the operands swapped (B fragment first) so that lane l holds rows (l & 15) of a
-// 16 x 16 block and C is read and written in 128-byte column runs; phase R's A fragments come
-// straight from HBM/L2 (one 8-byte load feeds 4 MFMAs), B from LDS.  One workgroup per CU
-// (4 waves, 20 accumulator blocks each in phase R).
+// 256-thread workgroup per 32-column block of the columns right of the block (L-panel columns or
+// U12 columns) runs the whole sub-panel sequence on its columns with the block REGISTER-RESIDENT:
+// the OB rows [ob0, ob1) x 32 columns (up to 384 x 32) are loaded once -- wave wv holds the 16-row
+// blocks wv, wv + 4, ..., so sub-panel u's four row blocks are one per wave -- and for each 64-row
+// sub-panel u:
+//   T: C_u <- C_u - NL_u C_u (NL_u = I - L_uu^-1, tinv slot0 + u): the owner waves publish -C_u
+//      in LDS, apply the MFMA GEMM form in their registers, publish the new -C_u;
+//   R: every wave updates its row blocks below u inside the block, C_r -= L_ru C_u (k = 64), L
+//      fragments straight from HBM/L2 (the next block's in flight during the current one's MFMAs).
+// The block is stored once at the end: one HBM round trip per column block instead of one per
+// sub-panel (round 4 re-loaded and re-stored the rows below u for every u, a latency chain of
+// ~115 us per workgroup).  Per element the same operations in the same order as the per-sub-panel
+// launches it replaces (acc = C, then one fp64 MFMA-FMA per k ascending with -C_u as the first
+// operand), so the factors are bitwise unchanged.
 // ------------------------------------------------------------------------------------
-#ifndef KQR
-#define KQR 4     // k-quads of L fragments per round trip in phase R
-#endif
-#ifndef UROWS_WG_PER_CU
-#define UROWS_WG_PER_CU 2
-#endif
-#define ULDB 80   // LDS row stride of -C_u [k][col]: k, k+1 rows in opposite bank halves
-// Global accesses walk one per-lane pointer (a VGPR pair) per operand in steps of 4 columns,
-// the remaining offsets being instruction immediates; no branch around a load (values outside
-// the block are read and discarded by a select, row/column overruns stay inside the padded
-// allocation: kUrowsPad).  Loads beyond the last k-quad or row block are skipped wave-uniformly.
+#define UR_NC 32    // columns per workgroup
+#define UR_RB 6     // 16-row blocks per wave (OB <= 384 = 4 waves x 6 x 16)
+#define UR_LD 36    // LDS row stride of -C_u [k][col] (doubles)
 // c ? x : +0.0 as a bit mask (keeps the compiler from sinking the load into a branch)
 __device__ __forceinline__ double sel0(bool c, double x) {
   return __longlong_as_double(__double_as_longlong(x) & (c ? -1LL : 0LL));
 }
-__global__ __launch_bounds__(256, UROWS_WG_PER_CU) void k_urows(const URowTask* __restrict__ tasks, const SNode* __restrict__ sn,
+__global__ __launch_bounds__(256, 2) void k_urows(const URowTask* __restrict__ tasks, const SNode* __restrict__ sn,
                                                   double* __restrict__ store, const double* __restrict__ tinv) {
-  __shared__ double Bs[64 * ULDB];
+  __shared__ double Bs[64 * UR_LD];
   const URowTask t = tasks[blockIdx.x];
   const SNode s = sn[t.s];
   const int64_t M = (int64_t)s.ns + s.nu;
   const int64_t ld = t.ld;
-  const int nc = t.ncols;
+  const int nc = t.ncols;                 // <= 32
+  const int nrows = t.ob1 - t.ob0;        // <= 384
   const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, lk = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   gdbl* const C = gbl(store + t.coff);   // (row, col) at col * ld + row
   const gdbl* const Lp = gbl(store + s.Loff);
-  for (int u = 0;; ++u) {
+  // this lane's element r of block (i, cb): row ob0 + 16 (wv + 4 i) + li, column 16 cb + lk + 4 r
+  v4d acc[UR_RB][2];
+#pragma unroll
+  for (int i = 0; i < UR_RB; ++i) {
+    const int lr = 16 * (wv + 4 * i) + li;
+    const bool rin = lr < nrows;
+    const int row = t.ob0 + (rin ? lr : 0);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = 16 * cb + lk + 4 * r;
+        const bool in = rin && col < nc;
+        acc[i][cb][r] = sel0(in, C[(int64_t)(in ? col : 0) * ld + row]);
+      }
+  }
+  // -C_u of this wave's block i into the LDS image [k = row within the sub-panel][col]
+  auto publish = [&](int i) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Bs[(16 * wv + li) * UR_LD + 16 * cb + lk + 4 * r] = -acc[i][cb][r];
+  };
+  const int nsub = (nrows + 63) >> 6;
+#pragma unroll 1
+  for (int u = 0; u < nsub; ++u) {
     const int kbu = t.ob0 + 64 * u;
-    if (kbu >= t.ob1) break;
     const int wu = min(64, t.ob1 - kbu);
     const int nkq = (wu + 3) >> 2;
-    // stage -C_u (the B operand of phase T), zero outside wu x nc: wave wv stages columns wv + 4i
+    // ---- T: the four row blocks of sub-panel u are block i = u of each wave
+    v4d tc[2];
+#pragma unroll
+    for (int i = 0; i < UR_RB; ++i)
+      if (i == u) {
+        publish(i);
+        tc[0] = acc[i][0];
+        tc[1] = acc[i][1];
+      }
+    // the wave's NL fragments (rows 16 wv + li of NL_u), all 16 k-quads in flight
+    double na[16];
     {
-      double v[16];
-      const gdbl* p = C + (int64_t)wv * ld + kbu + lane;
+      const gdbl* pn = gbl(tinv + (int64_t)(t.slot0 + u) * 8192) + lk * 64 + 16 * wv + li;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        v[i] = *p;
-        p += 4 * ld;
-      }
-#pragma unroll
-      for (int i = 0; i < 16; ++i) Bs[lane * ULDB + wv + 4 * i] = sel0(lane < wu && wv + 4 * i < nc, -v[i]);
+      for (int kq = 0; kq < 16; ++kq) na[kq] = sel0(16 * wv + li < wu && 4 * kq + lk < wu, pn[256 * kq]);
     }
-    // phase T: wave wv owns rows 32 (wv & 1) + [0, 32), columns 32 (wv >> 1) + [0, 32)
-    {
-      const int rb0 = 32 * (wv & 1), cb0 = 32 * (wv >> 1);
-      v4d acc[2][2];
-      {
-        gdbl* p = C + (int64_t)(cb0 + lk) * ld + kbu + rb0 + li;
+    __syncthreads();   // -C_u published
 #pragma unroll
-        for (int c4 = 0; c4 < 8; ++c4) {   // columns cb0 + 4 c4 + lk = cb0 + 16 bj + lk + 4 r
-          const int bj = c4 >> 2, r = c4 & 3, col = cb0 + 4 * c4 + lk;
+    for (int kq = 0; kq < 16; ++kq) {
+      if (kq >= nkq) continue;
+      const int k = 4 * kq + lk;
 #pragma unroll
-          for (int bi = 0; bi < 2; ++bi) {
-            const double x = p[16 * bi];
-            acc[bi][bj][r] = sel0(rb0 + 16 * bi + li < wu && col < nc, x);
-          }
-          p += 4 * ld;
-        }
-      }
-      __syncthreads();   // -C_u staged
-      // the wave's NL fragments, 8 k-quads per round trip
-      const gdbl* pn = gbl(tinv + (int64_t)(t.slot0 + u) * 8192) + lk * 64 + rb0 + li;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        double na[2][8];
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-#pragma unroll
-          for (int bi = 0; bi < 2; ++bi)
-            na[bi][kk] = sel0(rb0 + 16 * bi + li < wu && 4 * (8 * h + kk) + lk < wu, pn[16 * bi]);
-          pn += 256;
-        }
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) {
-          const int kq = 8 * h + kk;
-          if (kq >= nkq) continue;
-          const int k = 4 * kq + lk;
-          double fb[2];
-#pragma unroll
-          for (int bj = 0; bj < 2; ++bj) fb[bj] = Bs[k * ULDB + cb0 + 16 * bj + li];
-#pragma unroll
-          for (int bi = 0; bi < 2; ++bi)
-#pragma unroll
-            for (int bj = 0; bj < 2; ++bj)
-              acc[bi][bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[bj], na[bi][kk], acc[bi][bj], 0, 0, 0);
-        }
-      }
-      __syncthreads();   // every wave is done reading the old -C_u
-      {
-        gdbl* p = C + (int64_t)(cb0 + lk) * ld + kbu + rb0 + li;
-#pragma unroll
-        for (int c4 = 0; c4 < 8; ++c4) {
-          const int bj = c4 >> 2, r = c4 & 3, col = cb0 + 4 * c4 + lk;
-#pragma unroll
-          for (int bi = 0; bi < 2; ++bi) {
-            const int row = rb0 + 16 * bi + li;
-            const double v = acc[bi][bj][r];
-            const bool in = row < wu && col < nc;
-            if (in) p[16 * bi] = v;
-            Bs[row * ULDB + col] = sel0(in, -v);
-          }
-          p += 4 * ld;
-        }
-      }
-      __syncthreads();
+      for (int cb = 0; cb < 2; ++cb)
+        tc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(Bs[k * UR_LD + 16 * cb + li], na[kq], tc[cb], 0, 0, 0);
     }
-    // phase R: rows [kbu + wu, ob1) in 16-row blocks; wave wv takes blocks wv, wv + 4, ... one at
-    // a time (4 accumulator blocks: the 64 columns), the next block's C and L fragments in flight
-    // while the current one's 64 MFMAs run
-    const int r0 = kbu + wu, mr = t.ob1 - r0;
-    const int nrb = (mr + 15) >> 4;
-    if (wv < nrb) {
-      v4d cc[4];
-      double fa[16];
-#if UROWS_WG_PER_CU == 1
-      v4d cn[4];
-      double fan[16];
-#endif
-      auto load_blk = [&](int rb, v4d (&c)[4], double (&f)[16]) {
-        const gdbl* p = C + (int64_t)lk * ld + r0 + 16 * rb + li;
+    __syncthreads();   // every wave is done reading the old -C_u
 #pragma unroll
-        for (int c4 = 0; c4 < 16; ++c4) {
-          c[c4 >> 2][c4 & 3] = *p;
-          p += 4 * ld;
-        }
-        const gdbl* pa = Lp + (int64_t)(kbu + lk) * M + r0 + 16 * rb + li;
-#pragma unroll
-        for (int kq = 0; kq < 16; ++kq) {
-          f[kq] = kq < nkq ? *pa : 0.0;
-          pa += 4 * M;
-        }
-      };
-#if UROWS_WG_PER_CU == 1
-      load_blk(wv, cc, fa);
-#endif
-#pragma unroll 1
-      for (int rb = wv; rb < nrb; rb += 4) {
-#if UROWS_WG_PER_CU == 1   // one workgroup per CU: the next block's loads in flight
-        if (rb + 4 < nrb) load_blk(rb + 4, cn, fan);
-#else                      // two per CU: the other workgroup covers the load latency
-        load_blk(rb, cc, fa);
-#endif
-        const bool rin = 16 * rb + li < mr;
-        v4d acc[4];
-#pragma unroll
-        for (int bj = 0; bj < 4; ++bj)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[bj][r] = sel0(rin && 16 * bj + lk + 4 * r < nc, cc[bj][r]);
-#pragma unroll
-        for (int kq = 0; kq < 16; ++kq) {
-          if (kq >= nkq) continue;
-          const int k = 4 * kq + lk;
-          const double a = sel0(rin && k < wu, fa[kq]);
-#pragma unroll
-          for (int bj = 0; bj < 4; ++bj)
-            acc[bj] = __builtin_amdgcn_mfma_f64_16x16x4f64(Bs[k * ULDB + 16 * bj + li], a, acc[bj], 0, 0, 0);
-        }
-        gdbl* p = C + (int64_t)lk * ld + r0 + 16 * rb + li;
-#pragma unroll
-        for (int c4 = 0; c4 < 16; ++c4) {
-          if (rin && 4 * c4 + lk < nc) *p = acc[c4 >> 2][c4 & 3];
-          p += 4 * ld;
-        }
-#if UROWS_WG_PER_CU == 1
-#pragma unroll
-        for (int j = 0; j < 4; ++j) cc[j] = cn[j];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) fa[j] = fan[j];
-#endif
+    for (int i = 0; i < UR_RB; ++i)
+      if (i == u) {
+        acc[i][0] = tc[0];
+        acc[i][1] = tc[1];
+        publish(i);
       }
+    __syncthreads();   // new -C_u published
+    // ---- R: this wave's row blocks below sub-panel u (blocks i > u), C_r -= L_ru C_u
+    double fa[16], fn[16];
+    auto lfrag = [&](int i, double (&f)[16]) {
+      const int lr = 16 * (wv + 4 * i) + li;
+      const bool rin = lr < nrows;
+      const gdbl* pa = Lp + (int64_t)(kbu + lk) * M + t.ob0 + (rin ? lr : 0);
+#pragma unroll
+      for (int kq = 0; kq < 16; ++kq) {
+        const bool kin = 4 * kq + lk < wu;
+        f[kq] = sel0(rin && kin, pa[kin ? (int64_t)4 * kq * M : 0]);
+      }
+    };
+    if (u + 1 < UR_RB && 16 * (wv + 4 * (u + 1)) < nrows) lfrag(u + 1, fa);
+#pragma unroll
+    for (int i = 1; i < UR_RB; ++i) {
+      if (i <= u || 16 * (wv + 4 * i) >= nrows) continue;
+      const bool more = i + 1 < UR_RB && 16 * (wv + 4 * (i + 1)) < nrows;
+      if (more) lfrag(i + 1, fn);
+#pragma unroll
+      for (int kq = 0; kq < 16; ++kq) {
+        if (kq >= nkq) continue;
+        const int k = 4 * kq + lk;
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          acc[i][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(Bs[k * UR_LD + 16 * cb + li], fa[kq], acc[i][cb], 0, 0, 0);
+      }
+      if (more)
+#pragma unroll
+        for (int kq = 0; kq < 16; ++kq) fa[kq] = fn[kq];
     }
-    __syncthreads();   // C_u / C_r stores before the next sub-panel's loads; Bs free
+    __syncthreads();   // Bs free for the next sub-panel
+  }
+#pragma unroll
+  for (int i = 0; i < UR_RB; ++i) {
+    const int lr = 16 * (wv + 4 * i) + li;
+    if (16 * (wv + 4 * i) >= nrows) continue;
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = 16 * cb + lk + 4 * r;
+        if (lr < nrows && col < nc) C[(int64_t)col * ld + t.ob0 + lr] = acc[i][cb][r];
+      }
   }
 }
 

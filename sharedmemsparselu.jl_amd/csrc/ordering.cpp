@@ -160,31 +160,33 @@ struct NDState {
     for (auto v : V) set_stamp(v, tag);
     std::vector<int32_t> order;
     std::vector<int64_t> lptr;
-    // connected components
-    {
+    // connected components (the BFS from V[0] is also the first step of the root search below)
+    bfs(V[0], tag, order, lptr);
+    if ((int64_t)order.size() < (int64_t)V.size()) {
       std::vector<std::vector<int32_t>> comps;
+      comps.emplace_back(order.begin(), order.end());
       for (auto v : V) {
         if (level[v] >= 0) continue;
         bfs(v, tag, order, lptr);
         comps.emplace_back(order.begin(), order.end());
       }
       for (auto& c : comps) clear_levels(c);
-      if (comps.size() > 1) {
-        for (auto& c : comps) {
-          const int64_t sz = (int64_t)c.size();
-          run(std::move(c), depth + 1, leafsz, off);
-          off += sz;
-        }
-        return;
+      for (auto& c : comps) {
+        const int64_t sz = (int64_t)c.size();
+        run(std::move(c), depth + 1, leafsz, off);
+        off += sz;
       }
+      return;
     }
-    // pseudo-peripheral root
+    // pseudo-peripheral root: BFS from the min-degree vertex of the last level while the
+    // eccentricity grows (at most 6 BFS); the last BFS computed is the one from `root`
     int32_t root = V[0];
     int64_t ecc = -1;
+    bool have = true;   // order/lptr hold the BFS from root
     for (int it = 0; it < 6; ++it) {
-      bfs(root, tag, order, lptr);
+      if (!have) bfs(root, tag, order, lptr);
+      have = true;
       int64_t h = (int64_t)lptr.size() - 2;
-      clear_levels(order);
       if (h <= ecc) break;
       ecc = h;
       // min-degree vertex in the last level
@@ -195,9 +197,12 @@ struct NDState {
         int64_t d = g.ptr[v + 1] - g.ptr[v];
         if (d < bd) { bd = d; best = v; }
       }
+      if (best == root) break;   // (a BFS from the same root would repeat this one)
+      clear_levels(order);
+      have = false;
       root = best;
     }
-    bfs(root, tag, order, lptr);
+    if (!have) bfs(root, tag, order, lptr);
     int64_t nlev = (int64_t)lptr.size() - 1;
     if (nlev < 3) {  // (nearly) a clique: no useful separator
       clear_levels(order);

@@ -1107,19 +1107,42 @@ void rank_layout(const Plan& P, int r, RankLayout& L) {
 
 double project_partition(const Plan& P, double tflops, double gbs, double lat_us, double* t1_out) {
   const double rate = tflops * 1e12, bw = gbs * 1e9, lat = lat_us * 1e-6;
-  const double step_lat = 80e-6;   // latency of one 64-column panel step (panel, inverses, TRSM)
+  // calibrated on one MI355X (round 5): 80 us per 64-column panel step (panel, inverses, TRSM,
+  // in-block update: 695 steps ~ 56 ms at 128^3), 0.32 ms per level (launch latencies, the small
+  // fronts' kernels and the per-refactor dominance check: C2 7.9 ms over 18 levels), and the
+  // caller's rate for the dense front work (52 TFLOP/s reproduces 0.49 s at 128^3 with both)
+  const double step_lat = 80e-6;
+  const double level_lat = 0.32e-3;
   auto panel_chain = [&](int64_t s) { return P.ns(s) > 128 ? step_lat * (double)((P.ns(s) + 63) / 64) : 0.0; };
+  // The fronts of one level that one GPU owns run batched (every launch of the level covers all of
+  // them, in lockstep): their dense work adds up, their panel chains overlap, so a level costs
+  // sum(flops) / rate + max(chain) on that GPU (round 4 summed the chains: 0.80 s projected at
+  // 128^3 against 0.49-0.50 s measured).
   double t1 = 0;
-  for (int64_t s = 0; s < P.nsup; ++s) t1 += P.front_flops[s] / rate + panel_chain(s);
+  for (int l = 0; l < P.nlevels; ++l) {
+    double fl = 0, ch = 0;
+    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+      fl += P.front_flops[P.lev_sup[k]];
+      ch = std::max(ch, panel_chain(P.lev_sup[k]));
+    }
+    t1 += fl / rate + ch + level_lat;
+  }
   if (t1_out) *t1_out = t1;
   std::vector<double> clk(P.nparts, 0.0);
-  for (int l = 0; l < P.nlevels; ++l)
+  std::vector<double> lev_fl(P.nparts), lev_ch(P.nparts);
+  for (int l = 0; l < P.nlevels; ++l) {
+    std::fill(lev_fl.begin(), lev_fl.end(), 0.0);
+    std::fill(lev_ch.begin(), lev_ch.end(), 0.0);
     for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
       const int64_t s = P.lev_sup[k];
-      if (!P.dist(s)) {
-        clk[P.owner[s]] += P.front_flops[s] / rate + panel_chain(s);
-        continue;
-      }
+      if (P.dist(s)) continue;
+      lev_fl[P.owner[s]] += P.front_flops[s];
+      lev_ch[P.owner[s]] = std::max(lev_ch[P.owner[s]], panel_chain(s));
+    }
+    for (int r = 0; r < P.nparts; ++r) clk[r] += lev_fl[r] / rate + lev_ch[r] + level_lat;
+    for (int64_t k = P.lev_ptr[l]; k < P.lev_ptr[l + 1]; ++k) {
+      const int64_t s = P.lev_sup[k];
+      if (!P.dist(s)) continue;
       const auto& G = P.group[s];
       double t = 0;
       for (int r : G) t = std::max(t, clk[r]);
@@ -1174,6 +1197,7 @@ double project_partition(const Plan& P, double tflops, double gbs, double lat_us
                      (long long)s, l, (long long)P.ns(s), (long long)P.M(s), G.size(), t, tend, P.front_flops[s]);
       for (int r : G) clk[r] = tend;
     }
+  }
   return *std::max_element(clk.begin(), clk.end());
 }
 

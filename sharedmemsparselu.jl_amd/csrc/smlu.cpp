@@ -829,6 +829,8 @@ static int build_schedule(smlu_handle* h) {
       for (auto& g : cand) kmax = std::max(kmax, g.k);
       if (kmax <= 64) tile = 65;
     }
+    if (step < 0 && !tpatch)   // F22: longest k first, so the launch's last tiles are short ones
+      std::stable_sort(cand.begin(), cand.end(), [](const GemmTask& a, const GemmTask& b) { return a.k > b.k; });
     Launch L;
     L.kind = step < 0 ? K_GEMM22 : kind;
     L.side = side;
@@ -1280,13 +1282,13 @@ static int build_schedule(smlu_handle* h) {
             }
             const int64_t M = (int64_t)r.ns + r.nu;
             const int32_t slot0 = (int32_t)slot_of(it.s, (it.ob0 % sbw(it.s)) / r.nb);
-            for (int64_t c = it.c0; c < it.c1; c += 64)
+            for (int64_t c = it.c0; c < it.c1; c += kUrowsCols)
               ur_tasks.push_back(URowTask{(int32_t)it.s, (int32_t)it.ob0, (int32_t)it.ob1, slot0, (int32_t)M,
-                                          (int32_t)std::min<int64_t>(64, it.c1 - c), r.Loff + c * M});
+                                          (int32_t)std::min<int64_t>(kUrowsCols, it.c1 - c), r.Loff + c * M});
             if (it.u12)
-              for (int64_t c = 0; c < r.nu; c += 64)
+              for (int64_t c = 0; c < r.nu; c += kUrowsCols)
                 ur_tasks.push_back(URowTask{(int32_t)it.s, (int32_t)it.ob0, (int32_t)it.ob1, slot0, r.ns,
-                                            (int32_t)std::min<int64_t>(64, r.nu - c), r.Uoff + c * r.ns});
+                                            (int32_t)std::min<int64_t>(kUrowsCols, r.nu - c), r.Uoff + c * r.ns});
           }
           L.cnt = (int64_t)ur_tasks.size() - L.off;
           if (L.cnt > 0) h->fac.push_back(L);

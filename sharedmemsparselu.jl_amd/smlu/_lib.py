@@ -29,7 +29,6 @@ SMLU_ERR_ALLOC = -3
 SMLU_ERR_HIP = -4
 SMLU_ERR_NODEVICE = -5
 SMLU_ERR_STATE = -6
-SMLU_ERR_PATTERN = -7
 
 ORDER_AUTO, ORDER_NATURAL, ORDER_GEOMETRIC_ND, ORDER_GRAPH_ND, ORDER_GIVEN, ORDER_AMD = range(6)
 

@@ -91,7 +91,7 @@ class Plan:
             raise RuntimeError(f"smlu_plan_rank_memory failed ({rc}): {C.last_error(None)}")
         return a.value, b.value, c.value
 
-    def project(self, nparts, tflops=50.0, gbs=50.0, lat_us=30.0):
+    def project(self, nparts, tflops=52.0, gbs=100.0, lat_us=20.0):
         """Projected partitioned factorization time (s) and the one-GPU time of the same model."""
         t1 = ctypes.c_double()
         t = C.lib().smlu_plan_project(self._h, int(nparts), float(tflops), float(gbs), float(lat_us),

@@ -213,4 +213,4 @@ def test_given_pattern_rejected(gpu, bad):
     L2.eliminate_zeros()
     with pytest.raises(smlu.SmluError) as ei:
         smlu.ParallelSparseLU(A, p=z["p"], q=z["q"], L_pattern=L2, U_pattern=U)
-    assert "(-7)" in str(ei.value)
+    assert "(-2)" in str(ei.value)
