@@ -746,6 +746,10 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
     }, 4096);
     if (outside) return "internal: A entry outside its front";
   }
+  {
+    const auto t = std::chrono::steady_clock::now();
+    phase_ms[10] += std::chrono::duration<double, std::milli>(t - tp).count();
+  }
   Alev_ptr.assign(nlevels + 1, 0);
   for (int64_t e = 0; e < nnzA; ++e) Alev_ptr[ent_level[e] + 1]++;
   for (int l = 0; l < nlevels; ++l) Alev_ptr[l + 1] += Alev_ptr[l];
@@ -754,9 +758,23 @@ std::string Plan::build(int64_t n_, const int64_t* colptr, const int64_t* rowval
     std::vector<int64_t> pos(Alev_ptr.begin(), Alev_ptr.end() - 1);
     for (int64_t e = 0; e < nnzA; ++e) Alev_ent[pos[ent_level[e]]++] = (int32_t)e;
     // front slots are distinct: a strict order, so the parallel sort equals std::sort
-    for (int l = 0; l < nlevels; ++l)
-      parallel_sort(Alev_ent.begin() + Alev_ptr[l], Alev_ent.begin() + Alev_ptr[l + 1],
-                    [&](int32_t a, int32_t b) { return Adest[a] < Adest[b]; });
+    const auto ts = std::chrono::steady_clock::now();
+    // sorted as (key, entry) records: the comparator touches contiguous memory only
+    std::vector<std::pair<int64_t, int32_t>> kv;
+    for (int l = 0; l < nlevels; ++l) {
+      const int64_t lo = Alev_ptr[l], cnt = Alev_ptr[l + 1] - lo;
+      kv.resize((size_t)cnt);
+      parallel_for(cnt, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) kv[i] = {Adest[Alev_ent[lo + i]], Alev_ent[lo + i]};
+      });
+      parallel_sort(kv.begin(), kv.end(), [](const std::pair<int64_t, int32_t>& a, const std::pair<int64_t, int32_t>& b) {
+        return a.first < b.first;
+      });
+      parallel_for(cnt, [&](int64_t a, int64_t b) {
+        for (int64_t i = a; i < b; ++i) Alev_ent[lo + i] = kv[i].second;
+      });
+    }
+    phase_ms[11] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
   }
   // rows of A (for the row scaling kernel)
   Arowptr.assign(n + 1, 0);

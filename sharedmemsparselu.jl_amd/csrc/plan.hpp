@@ -113,8 +113,8 @@ struct Plan {
   int64_t front_max = 0, ns_max = 0, nu_max = 0;
   double analysis_ms = 0;
   // analysis phases (ms): input, graph, ordering, etree, column counts, row structures, relax,
-  // levels / relmap, layout, A map
-  double phase_ms[10] = {0};
+  // levels / relmap, layout, A map (10, 11: the A map's entry pass and its level sort)
+  double phase_ms[12] = {0};
 
   // ---- multi-GPU partition (compute_owners) ----
   // Subtrees of the assembly tree are bin-packed onto ranks (each factored with no

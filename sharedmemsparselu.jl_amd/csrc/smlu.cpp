@@ -4403,7 +4403,7 @@ int64_t smlu_last_error_col(const smlu_handle* h) {
 static double plan_stat(const Plan& P, const std::string& k) {
   if (k.rfind("phase_ms", 0) == 0) {   // phase_ms0 .. phase_ms9 (Plan::phase_ms)
     const int i = std::atoi(k.c_str() + 8);
-    return i >= 0 && i < 10 ? P.phase_ms[i] : std::numeric_limits<double>::quiet_NaN();
+    return i >= 0 && i < 12 ? P.phase_ms[i] : std::numeric_limits<double>::quiet_NaN();
   }
   if (k == "n") return (double)P.n;
   if (k == "nnzA") return (double)P.nnzA;
