@@ -67,12 +67,10 @@ typedef struct smlu_opts {
     int32_t refine;       /* iterative-refinement steps in smlu_solve*: -1 (default) = up to 3 only
                              when the last factorization flagged weak pivots (the pivot-failure
                              fallback of the diagonal-tile pivoting); 0 = never;
-                             k > 0 = up to k steps (stops when the residual stops halving) */
-    int32_t vendor_gemm;  /* 0 (default) = every GEMM runs on the hand-written MFMA tiles;
-                             1 (or env SMLU_ROCBLAS) = the large plain Schur-update GEMMs
-                             (F22 -= L21*U12 and the trailing updates of the big fronts, one
-                             front per call) go to rocBLAS dgemm in deterministic mode (atomics
-                             off) when librocblas is present (a comparison path, not faster) */
+                             k > 0 = up to k steps (LAPACK dgerfs' stop: componentwise backward error
+                             <= 4 unit roundoffs or not halving) */
+    int32_t vendor_gemm;  /* reserved, ignored (round 5 removed the vendor GEMM comparison path:
+                             every GEMM runs on the hand-written MFMA tiles) */
 } smlu_opts;
 
 typedef struct smlu_handle smlu_handle;
@@ -336,6 +334,21 @@ int smlu_dev_front_hash(smlu_handle* h, unsigned long long* out);
 int smlu_dev_front_values(smlu_handle* h, int64_t s, double* out);
 int smlu_dev_front_offsets(smlu_handle* h, int64_t* out);
 int smlu_dev_copy(smlu_handle* h, int which, int64_t off, int64_t cnt, double* out, int64_t* len);
+
+/* ---- environment knobs (read by the library in one place, csrc/tune.cpp; nothing else in the
+ * environment changes its numerics or schedule) ---------------------------------------------
+ *   SMLU_OB=w          outer block width of the blocked fronts (multiple of 64; default 384)
+ *   SMLU_T128MIN=t     128x128 MFMA tiles for GEMM launches with >= t output tiles (default 512)
+ *   SMLU_SMALLK=0      no one-shot k <= 64 GEMM tile (tests: forces the 64x64 VALU tile)
+ *   SMLU_FULLPIV_NS=k  largest front with full-candidate pivoting (tests; default: 512, or 128
+ *                      for diagonally dominant values)
+ *   SMLU_SWEEP_SPIN=s  polls before a sync-free solve wait gives up and the solve is re-run on the
+ *                      per-block schedule (default 2^22; 0 = at once, tests)
+ *   SMLU_SOLVE_STEPS=1 per-block solve launches instead of the sync-free sweeps
+ *   SMLU_NO_GRAPH      eager launches instead of captured hipGraphs
+ *   SMLU_DEBUG_SYNC    synchronise after every launch (localises a failing kernel)
+ *   SMLU_NO_REPIVOT    no re-pivoting refactor after weak diagonal-tile pivots (tests)
+ */
 
 /* Library version string. */
 const char* smlu_version(void);

@@ -812,7 +812,7 @@ void Plan::compute_owners(int np, int64_t block) {
     if (s_parent[s] >= 0) W[s_parent[s]] += W[s];
   std::vector<char> top(nsup, 0);
   std::vector<int32_t> sub_owner(nsup, -1);
-  static const bool binpack = std::getenv("SMLU_PARTITION") && std::string(std::getenv("SMLU_PARTITION")) == "binpack";
+  constexpr bool binpack = false;   // rounds 1-3's bin-packing, kept for the record
   if (!binpack) {
     std::vector<int32_t> lo(nsup, -1), hi(nsup, -1);   // rank range of each top front
     // Cost model of a subtree set on k ranks (flop units): one rank does all of it; a single
@@ -909,7 +909,7 @@ void Plan::compute_owners(int np, int64_t block) {
         for (auto v : j.sub) sub_owner[v] = j.r0;
         continue;
       }
-      static const bool dbg = std::getenv("SMLU_PROJECT_DEBUG") != nullptr;
+      constexpr bool dbg = false;
       if (dbg && j.r1 - j.r0 >= 2) {
         std::fprintf(stderr, "map ranks [%d,%d):", j.r0, j.r1);
         for (auto v : j.sub) std::fprintf(stderr, " %lld(W %.3e ns %lld)", (long long)v, W[v], (long long)ns(v));
@@ -1176,7 +1176,7 @@ double project_partition(const Plan& P, double tflops, double gbs, double lat_us
       // factors b+1 and broadcasts it; it applies b to its other blocks after that broadcast
       std::map<int, double> c, pend;
       for (int r : G) { c[r] = t; pend[r] = 0.0; }
-      static const bool la = (std::getenv("SMLU_DIST_LOOKAHEAD") && std::atoi(std::getenv("SMLU_DIST_LOOKAHEAD")) == 1);
+      constexpr bool la = false;   // the schedule's depth-1 look-ahead is off
       for (int64_t b = 0; b < np; ++b) {
         const double c0 = (double)P.blk_c0(s, b), c1 = (double)P.blk_c1(s, b), w = c1 - c0;
         const int o = P.blk_owner(s, b);
@@ -1209,7 +1209,7 @@ double project_partition(const Plan& P, double tflops, double gbs, double lat_us
       }
       double tend = 0;
       for (int r : G) tend = std::max(tend, c[r] + pend[r]);
-      static const bool dbg = std::getenv("SMLU_PROJECT_DEBUG") != nullptr;
+      constexpr bool dbg = false;
       if (dbg)
         std::fprintf(stderr, "shared front %lld level %d ns %lld M %lld group %zu: start %.4f end %.4f (flops %.3e)\n",
                      (long long)s, l, (long long)P.ns(s), (long long)P.M(s), G.size(), t, tend, P.front_flops[s]);

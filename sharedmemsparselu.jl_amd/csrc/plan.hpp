@@ -17,6 +17,22 @@
 
 namespace smlu {
 
+// Tuning / test knobs of the library, read from the environment by tune() (tune.cpp, the only
+// place libsmlu reads it; documented in include/smlu.h).  Anything not listed here is not a knob.
+struct Tune {
+  int ob = 0;                 // SMLU_OB: outer block width (multiple of 64; 0 = the default 384)
+  int64_t t128_min = 512;     // SMLU_T128MIN: 128x128 MFMA tiles from this many output tiles per launch
+  bool small_k = true;        // SMLU_SMALLK=0: no one-shot k <= 64 GEMM tile
+  int64_t fullpiv_ns = -1;    // SMLU_FULLPIV_NS: largest ns with full-candidate pivoting (-1 = default rule)
+  int sweep_spin = 1 << 22;   // SMLU_SWEEP_SPIN: polls before a sync-free solve wait gives up (0: at once)
+  bool solve_steps = false;   // SMLU_SOLVE_STEPS=1: per-block solve launches instead of the sweeps
+  bool no_graph = false;      // SMLU_NO_GRAPH: eager launches, no captured graphs
+  bool debug_sync = false;    // SMLU_DEBUG_SYNC: synchronise after every launch (error localisation)
+  bool no_repivot = false;    // SMLU_NO_REPIVOT: no re-pivoting refactor after weak tile pivots
+};
+Tune tune();
+
+
 struct PlanOptions {
   int ordering = 0;          // SMLU_ORDER_*
   int64_t grid[3] = {0, 0, 0};

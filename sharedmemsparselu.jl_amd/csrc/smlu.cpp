@@ -128,7 +128,6 @@ struct Launch {
   int64_t off2 = 0, cnt2 = 0, nwg2 = 0;   // second work list (merged launches)
   double flops = 0;
   int side = 0;                           // 1 = issued on the look-ahead stream
-  int vendor = 0;                         // 1 = GEMM tasks [off, off+cnt) issued as rocBLAS dgemm calls
 };
 
 template <class T>
@@ -232,45 +231,6 @@ RcclApi* rccl_api() {
   api.lib = l;
   return &api;
 }
-
-// ---- rocBLAS for the large plain Schur-update GEMMs (loaded at run time; absent -> the
-// hand-written MFMA tile runs them).  Deterministic mode: atomics (split-K) off, so a repeated
-// refactorization is bitwise identical. ----------------------------------------------------------
-struct RocblasApi {
-  void* lib = nullptr;
-  int (*create)(void**);
-  int (*destroy)(void*);
-  int (*set_stream)(void*, hipStream_t);
-  int (*set_atomics)(void*, int);
-  int (*dgemm)(void*, int, int, int, int, int, const double*, const double*, int, const double*, int,
-               const double*, double*, int);
-};
-
-RocblasApi* rocblas_api() {
-  static RocblasApi api;
-  static bool tried = false;
-  if (tried) return api.lib ? &api : nullptr;
-  tried = true;
-  void* l = dlopen("librocblas.so.5", RTLD_NOW | RTLD_LOCAL);
-  if (!l) l = dlopen("librocblas.so", RTLD_NOW | RTLD_LOCAL);
-  if (!l) return nullptr;
-  bool ok = true;
-  auto sym = [&](const char* n) {
-    void* f = dlsym(l, n);
-    ok = ok && f != nullptr;
-    return f;
-  };
-  api.create = (decltype(api.create))sym("rocblas_create_handle");
-  api.destroy = (decltype(api.destroy))sym("rocblas_destroy_handle");
-  api.set_stream = (decltype(api.set_stream))sym("rocblas_set_stream");
-  api.set_atomics = (decltype(api.set_atomics))sym("rocblas_set_atomics_mode");
-  api.dgemm = (decltype(api.dgemm))sym("rocblas_dgemm");
-  if (!ok) return nullptr;
-  api.lib = l;
-  return &api;
-}
-constexpr int kRbOpNone = 111;          // rocblas_operation_none
-constexpr int kRbAtomicsNotAllowed = 0; // rocblas_atomics_not_allowed
 
 struct RcclState {
   ncclComm_t comm = nullptr;
@@ -455,11 +415,6 @@ struct smlu_handle {
   bool trsm_gemm = true;      // GEMM-form triangular solves of the blocked fronts
   bool trsm_gemm64_only = false;   // SMLU_TRSM_GEMM=2: only for diagonal-tile (nb = 64) fronts
   int64_t side_wg = 0;        // grid cap of look-ahead GEMMs (SMLU_SIDE_WG; 0 = uncapped)
-  void* rocblas = nullptr;    // rocBLAS handle (opts.vendor_gemm and librocblas present)
-  int64_t vendor_min = 256;   // rocBLAS for GEMM tasks with at least this many 128x128 tiles (SMLU_ROCBLAS_MIN)
-  int64_t vendor_calls = 0;   // rocBLAS dgemm calls per factorization
-  int vendor_kinds = 3;       // launch kinds routed to rocBLAS: 1 F22, 2 trailing, 4 U rows, 8 in-block (SMLU_ROCBLAS_KINDS)
-  std::vector<GemmTask> hgt;  // host copy of the GEMM tasks (rocBLAS calls read their operands from it)
   // ComplexF64 handle (smlu_create_z): the plan and factors are those of the real-equivalent K
   bool zc = false;
   bool cpair = false;                // pair-preserving pivots (complex handle, no row transversal)
@@ -545,10 +500,6 @@ struct smlu_handle {
     ev_fork = ev_join = nullptr;
     if (side) (void)hipStreamDestroy(side);
     side = nullptr;
-    if (rocblas) {
-      if (RocblasApi* R = rocblas_api()) (void)R->destroy(rocblas);
-      rocblas = nullptr;
-    }
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
   }
@@ -610,6 +561,7 @@ static int check_device(smlu_handle* h) {
 // ---------------------------------------------------------------------------------------
 static int build_schedule(smlu_handle* h) {
   Plan& P = h->plan;
+  const Tune tn = tune();
   const int64_t nsup = P.nsup;
   hipStream_t st = h->stream;
   // supernode records: fronts [0, nsup) with this rank's offsets (RankLayout); a shared front
@@ -627,7 +579,7 @@ static int build_schedule(smlu_handle* h) {
   // a complex handle's pair-preserving pivots search every fully-summed row (mode 1): the
   // diagonal-tile panels have no pair rule
   const int64_t full_piv_ns = (h->pivmode == 1 || h->cpair) ? std::numeric_limits<int64_t>::max()
-                              : std::getenv("SMLU_FULLPIV_NS") ? std::atoll(std::getenv("SMLU_FULLPIV_NS"))
+                              : tn.fullpiv_ns >= 0 ? tn.fullpiv_ns
                               : h->dominant ? (int64_t)kSmallM : (int64_t)kFullPivNs;
   for (int64_t s = 0; s < nsup; ++s) {
     SNode r{};
@@ -749,29 +701,21 @@ static int build_schedule(smlu_handle* h) {
     }
     return o;
   };
-  h->lookahead = std::getenv("SMLU_LOOKAHEAD") != nullptr;
-  if (const char* e = std::getenv("SMLU_SIDE_WG")) h->side_wg = std::atoll(e);
-  if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
-  if (const char* e = std::getenv("SMLU_T128MIN")) h->t128_min = std::atoll(e);
-  h->small_k = !(std::getenv("SMLU_SMALLK") && std::atoi(std::getenv("SMLU_SMALLK")) == 0);
+  if (tn.ob > 0) h->ob = tn.ob;
+  h->t128_min = tn.t128_min;
+  h->small_k = tn.small_k;
   // MFMA 128 tile: code 131 (v3: LDS-DMA staging, kernels_gemm.hip); the F22 launches (k = ns, the
   // long-k shapes) take 135, the same tile with the next slice's barrier between its last two
   // k-quads (+3 % at k >= 2048, neutral at the k = 384 trailing shapes: tools/gemm_bench)
   const int mfma_tile = 131;
   // GEMM-form TRSM (k_tri_inv + GEMM tasks) needs the growth epilogue of the MFMA/64 tiles
-  {
-    const char* e = std::getenv("SMLU_TRSM_GEMM");
-    const int v = e ? std::atoi(e) : 2;   // 2 measured best: 32-wide panels keep k_step_trsm
-    h->trsm_gemm = h->opts.use_mfma && v != 0;
-    h->trsm_gemm64_only = v == 2;
-  }
+  // (the 32-wide panels keep k_step_trsm: measured best)
+  h->trsm_gemm = h->opts.use_mfma;
+  h->trsm_gemm64_only = true;
   // GEMM tasks whose A or B operand lives in the tinv buffer (allocated after the schedule)
   std::vector<std::pair<int64_t, int64_t>> tinv_patch;   // (gt index * 2 + operand B?, offset)
   h->gemm_flops = 0;
   h->gemm_launches = h->gemm128_launches = 0;
-  h->vendor_calls = 0;
-  if (const char* e = std::getenv("SMLU_ROCBLAS_MIN")) h->vendor_min = std::max<int64_t>(1, std::atoll(e));
-  if (const char* e = std::getenv("SMLU_ROCBLAS_KINDS")) h->vendor_kinds = std::atoi(e);
   h->gemm_bytes = 0;
   h->gemm22_flops = 0;
   h->dense_flops = P.flops;
@@ -782,43 +726,6 @@ static int build_schedule(smlu_handle* h) {
                              int side = 0, const std::vector<int64_t>* tpatch = nullptr) {
     if (cand.empty()) return;
     const bool count = kind != K_TRSML;   // GEMM-form TRSM is accounted as "trsm", not GEMM
-    // large plain Schur updates (F22, trailing): one rocBLAS dgemm per task; the rest stays in
-    // one batched launch of the hand-written tiles
-    const int vbit = step < 0 ? 1 : kind == K_GEMMO ? 2 : kind == K_GEMMU ? 4 : kind == K_GEMM ? 8 : 0;
-    if (h->rocblas && !side && !tpatch && (h->vendor_kinds & vbit)) {
-      std::vector<GemmTask> big, rest;
-      double flb = 0;
-      for (auto& g : cand) {
-        const int64_t t128 = (int64_t)((g.m + 127) / 128) * ((g.n + 127) / 128);
-        if (t128 >= h->vendor_min) {
-          big.push_back(g);
-          flb += 2.0 * g.m * (double)g.n * g.k;
-        } else {
-          rest.push_back(g);
-        }
-      }
-      if (!big.empty()) {
-        Launch V;
-        V.kind = step < 0 ? K_GEMM22 : kind;
-        V.step = step;
-        V.vendor = 1;
-        V.off = (int64_t)gt.size();
-        V.cnt = (int64_t)big.size();
-        V.flops = flb;
-        for (auto& g : big) {
-          h->gemm_bytes += 8.0 * ((double)g.m * g.k + (double)g.k * g.n + 2.0 * g.m * g.n);
-          gt.push_back(g);
-        }
-        h->fac.push_back(V);
-        h->gemm_flops += flb;
-        h->gemm_launches += V.cnt;
-        h->vendor_calls += V.cnt;
-        if (step < 0) h->gemm22_flops += flb;
-        cand.swap(rest);
-        fl -= flb;
-        if (cand.empty()) return;
-      }
-    }
     int64_t t128 = 0;
     for (auto& g : cand) t128 += (int64_t)((g.m + 127) / 128) * ((g.n + 127) / 128);
     int tile = t128 >= h->t128_min ? 128 : 64;
@@ -863,8 +770,7 @@ static int build_schedule(smlu_handle* h) {
   auto gform = [&](int64_t s) {
     return h->trsm_gemm && (h->hsn[s].nb == kNbTile || !h->trsm_gemm64_only);
   };
-  if (const char* e = std::getenv("SMLU_SB")) h->sb = std::atoi(e);
-  h->sb = std::max<int64_t>(h->ob, (h->sb / h->ob) * h->ob);
+  h->sb = h->ob;   // two-level blocking (a super-block level measured slower: DESIGN.md §8)
   auto sbw = [&](int64_t s) -> int64_t { return (gform(s) && !h->lookahead && h->nranks == 1) ? h->sb : h->ob; };
   const int64_t spf = std::max<int64_t>(h->sb, h->ob) / 32;   // swap / tile-inverse slots per front
   // fused panels (k_panel_blk<16, true>: panel + tile inverses + in-block row interchanges) for
@@ -872,12 +778,11 @@ static int build_schedule(smlu_handle* h) {
   // 2 (default): panel + the in-block row interchanges (no k_laswp inside the block) + the tile
   // inverses by 16 x 16 blocks on the matrix cores (no k_tri_inv); 1: without the inverses;
   // 0: three launches
-  const int fuse_mode = !(h->trsm_gemm && h->trsm_gemm64_only && h->ob <= 64 + 16 * 20) ? 0
-                        : std::getenv("SMLU_FUSED_PANEL") ? std::atoi(std::getenv("SMLU_FUSED_PANEL")) : 2;
+  const int fuse_mode = !(h->trsm_gemm && h->trsm_gemm64_only && h->ob <= 64 + 16 * 20) ? 0 : 2;
   const bool fuse_panel = fuse_mode > 0, fuse_inv = fuse_mode == 2;
   // fused U rows at the end of an outer block (k_urows) for the GEMM-form fronts; SMLU_FUSED_UROWS=0:
   // one TRSM + one update launch per sub-panel
-  const bool fuse_urows = h->ob <= 384 && !(std::getenv("SMLU_FUSED_UROWS") && std::atoi(std::getenv("SMLU_FUSED_UROWS")) == 0);
+  const bool fuse_urows = h->ob <= 384;
   // tinv operand encoding in tpatch: offset * 2 + (1 if the operand is B, 0 if A)
   auto tinv_slot_off = [](int64_t slot, bool upper) { return slot * 8192 + (upper ? 4096 : 0); };
   for (int l = 0; l < P.nlevels; ++l) {
@@ -1509,7 +1414,7 @@ static int build_schedule(smlu_handle* h) {
       // blocks (`pending`).  Off by default: the broadcast is a rendezvous (receivers post it
       // after their own trailing updates), so the deferred work only loads the next owner --
       // the schedule model projects 3.0x instead of 4.3x at 256^3 / 8 ranks with it on
-      static const bool dist_lookahead = (std::getenv("SMLU_DIST_LOOKAHEAD") && std::atoi(std::getenv("SMLU_DIST_LOOKAHEAD")) == 1);
+      constexpr bool dist_lookahead = false;
       std::vector<Launch> pending;
       for (int64_t b = 0; b < np; ++b) {
         const int64_t ob = P.blk_c0(t, b), oe = P.blk_c1(t, b), w = oe - ob;
@@ -1770,16 +1675,12 @@ static int build_schedule(smlu_handle* h) {
     add_comm(seq, seg, cm, std::move(op));
   };
   auto holder = [&](int64_t c) { return P.dist(c) ? P.blk_owner(c, P.npblk(c) - 1) : P.owner[c]; };
-  static const bool no_tiny = std::getenv("SMLU_NO_TINY_SOLVE") != nullptr;   // dev knob
-  static const bool no_micro = std::getenv("SMLU_NO_MICRO_SOLVE") != nullptr;  // dev knob
+  constexpr bool no_tiny = false, no_micro = false;
   // large fronts: one sync-free sweep launch per level and direction (default) or one launch per
   // 64-column block (SMLU_SOLVE_STEPS=1, the previous schedule)
-  const bool sweep_solve = !(std::getenv("SMLU_SOLVE_STEPS") && std::atoi(std::getenv("SMLU_SOLVE_STEPS")) == 1);
+  const bool sweep_solve = !tn.solve_steps;
   int64_t ssync_n = 0, ntick = 0;   // flags and ticket counters of the sweep launches
-  static const int64_t big_work = [] {
-    const char* e = std::getenv("SMLU_SOLVE_BIGWORK");   // dev knob (sweeps)
-    return e ? std::atoll(e) : kSolveBigWork;
-  }();
+  constexpr int64_t big_work = kSolveBigWork;
   for (int l = 0; l < P.nlevels; ++l) {
     std::vector<int64_t> tiny, small, bigs;
     for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {
@@ -2137,41 +2038,6 @@ static int build_schedule(smlu_handle* h) {
   }
 
   h->nlaunch = (int64_t)h->fac.size();
-  if (const char* path = std::getenv("SMLU_DUMP_SCHEDULE")) {   // dev: per-launch table for trace joins
-    if (FILE* fp = std::fopen(path, "w")) {
-      std::fprintf(fp, "idx,kind,name,step,tile,nwg,cnt,flops,kmax,mn\n");
-      for (size_t i = 0; i < h->fac.size(); ++i) {
-        const Launch& L = h->fac[i];
-        if (L.vendor) {   // one row per rocBLAS call (one kernel dispatch each), tile code 200
-          for (int64_t t = 0; t < L.cnt; ++t) {
-            const GemmTask& q = gt[L.off + t];
-            std::fprintf(fp, "%zu,%d,%s,%d,200,0,1,%.0f,%d,%.0f\n", i, L.kind, kKindName[L.kind], L.step,
-                         2.0 * q.m * (double)q.n * q.k, q.k, (double)q.m * q.n);
-          }
-          continue;
-        }
-        int kmax = 0;
-        double mn = 0;
-        const bool g = L.kind == K_GEMM || L.kind == K_GEMMU || L.kind == K_GEMMO || L.kind == K_GEMM22 ||
-                       L.kind == K_TRSML;
-        if (g)
-          for (int64_t t = 0; t < L.cnt; ++t) {
-            kmax = std::max(kmax, gt[L.off + t].k);
-            mn += (double)gt[L.off + t].m * gt[L.off + t].n;
-          }
-        double rd = 0;
-        if (L.kind == K_EXTADD)   // mn = front elements written, flops column = child values read
-          for (int64_t t = 0; t < L.cnt; ++t) {
-            const XCol& x = xc[L.off + t];
-            mn += (double)P.M(x.p);
-            for (int64_t q = 0; q < x.cnt; ++q) rd += (double)P.nu(xt[x.off + q].child);
-          }
-        std::fprintf(fp, "%zu,%d,%s,%d,%lld,%lld,%lld,%.0f,%d,%.0f\n", i, L.kind, kKindName[L.kind], L.step,
-                     (long long)L.aux, (long long)L.nwg, (long long)L.cnt, L.kind == K_EXTADD ? rd : L.flops, kmax, mn);
-      }
-      std::fclose(fp);
-    }
-  }
   // upload
   HIPCHK(h->sn.upload(h->hsn.data(), h->hsn.size(), st));
   HIPCHK(h->ilist.upload(ilist.data(), ilist.size(), st));
@@ -2226,14 +2092,6 @@ static int build_schedule(smlu_handle* h) {
   }
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
   h->ninv = (int64_t)invfront.size();
-  // SMLU_DIAG_INV=1: the solves apply the large fronts' diagonal blocks as products with their
-  // inverses (finish_factor launches k_diag_inv after every factorization).  Off by default: the
-  // sweeps are hand-off bound, the product saved nothing (13.89 ms vs 13.77 ms substituting, 128^3)
-  if (h->ninv > 0 && std::getenv("SMLU_DIAG_INV") && std::atoi(std::getenv("SMLU_DIAG_INV")) == 1) {
-    HIPCHK(h->invbase.upload(invbase.data(), invbase.size(), st));
-    HIPCHK(h->invfront.upload(invfront.data(), invfront.size(), st));
-    HIPCHK(h->dinvbuf.alloc((size_t)h->ninv * 2 * 4096));
-  }
   if (!gptr.empty()) {
     HIPCHK(h->gptr.upload(gptr.data(), gptr.size(), st));
     HIPCHK(h->gent.upload(gent.data(), gent.size(), st));
@@ -2257,7 +2115,7 @@ static int build_schedule(smlu_handle* h) {
     HIPCHK(h->sstatus.alloc(1));
     HIPCHK(hipMemsetAsync(h->sstatus.p, 0, sizeof(int32_t), st));
   }
-  if (const char* e = std::getenv("SMLU_SWEEP_SPIN")) h->sweep_spin = std::atoi(e);
+  h->sweep_spin = tn.sweep_spin;
   if (h->nranks > 1) max_list = std::max<int64_t>(max_list, dist_slots);
   if (!tinv_patch.empty() || h->nranks > 1) {   // operands in the tile-inverse slots: patch in the buffer address
     HIPCHK(h->tinv.alloc((size_t)max_list * 8192));
@@ -2268,27 +2126,6 @@ static int build_schedule(smlu_handle* h) {
     }
   }
   HIPCHK(h->gtasks.upload(gt.data(), gt.size(), st));
-  h->hgt = gt;
-  if (const char* path = std::getenv("SMLU_DUMP_LAUNCHES")) {   // dev: tools/gemm_launch_report.py
-    if (FILE* fp = std::fopen(path, "w")) {
-      std::fprintf(fp, "idx,kind,step,cnt,nwg,tile,flops,m_max,n_max,k_max\n");
-      for (size_t i = 0; i < h->fac.size(); ++i) {
-        const Launch& L = h->fac[i];
-        int mm = 0, nn = 0, kk = 0;
-        const bool gemm = L.kind == K_GEMM || L.kind == K_GEMMO || L.kind == K_GEMM22 || L.kind == K_GEMMU ||
-                          L.kind == K_TRSML;
-        if (gemm)
-          for (int64_t t = L.off; t < L.off + L.cnt; ++t) {
-            mm = std::max(mm, gt[t].m);
-            nn = std::max(nn, gt[t].n);
-            kk = std::max(kk, gt[t].k);
-          }
-        std::fprintf(fp, "%zu,%d,%d,%lld,%lld,%lld,%.6e,%d,%d,%d\n", i, L.kind, L.step, (long long)L.cnt,
-                     (long long)L.nwg, gemm ? (long long)L.aux : -1LL, L.flops, mm, nn, kk);
-      }
-      std::fclose(fp);
-    }
-  }
   HIPCHK(h->stasks.upload(st_tasks.data(), st_tasks.size(), st));
   HIPCHK(h->urtasks.upload(ur_tasks.data(), ur_tasks.size(), st));
   HIPCHK(h->xcols.upload(xc.data(), xc.size(), st));
@@ -2341,39 +2178,11 @@ static int build_schedule(smlu_handle* h) {
 static int setup_device(smlu_handle* h) {
   Plan& P = h->plan;
   HIPCHK(hipSetDevice(h->device));
-  // the critical path (panels, swaps, solves, next-block updates) runs on a high-priority
-  // stream; the look-ahead trailing updates on a low-priority one
+  // one high-priority stream per handle (the schedule is one stream-ordered sequence)
   int prio_lo = 0, prio_hi = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  if (std::getenv("SMLU_NO_PRIORITY")) prio_lo = prio_hi = 0;
   if (!h->stream) HIPCHK(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi));
-  if (!h->side) {
-    // SMLU_SIDE_RESERVE=r: keep r CUs of every 8 (one per XCD per step) free of look-ahead work
-    const char* rs = std::getenv("SMLU_SIDE_RESERVE");
-    int reserve = rs ? std::atoi(rs) : 0;
-    if (reserve > 0) {
-      hipDeviceProp_t pr;
-      HIPCHK(hipGetDeviceProperties(&pr, h->device));
-      int ncu = pr.multiProcessorCount;
-      std::vector<uint32_t> mask((ncu + 31) / 32, 0);
-      int kept = 0;
-      for (int c = 0; c < ncu; ++c)
-        if ((c / 8) % 32 >= reserve) { mask[c / 32] |= 1u << (c % 32); ++kept; }
-      HIPCHK(hipExtStreamCreateWithCUMask(&h->side, (uint32_t)mask.size(), mask.data()));
-      std::fprintf(stderr, "smlu: side stream on %d of %d CUs\n", kept, ncu);
-    } else {
-      HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_lo));
-    }
-  }
-  if (!h->rocblas && h->opts.vendor_gemm) {   // rocBLAS for the large plain Schur updates
-    if (RocblasApi* R = rocblas_api()) {
-      void* rb = nullptr;
-      if (R->create(&rb) == 0 && rb) {
-        if (R->set_stream(rb, h->stream) == 0 && R->set_atomics(rb, kRbAtomicsNotAllowed) == 0) h->rocblas = rb;
-        else (void)R->destroy(rb);
-      }
-    }
-  }
+  if (!h->side) HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_lo));
   if (!h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
   if (!h->ev_join) HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
   hipStream_t st = h->stream;
@@ -2473,17 +2282,6 @@ struct Timer {
 
 static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, double piv_tol) {
   hipStream_t st = L.side ? h->side : h->stream;
-  if (L.vendor) {   // C -= A*B per task, rocBLAS dgemm on the handle's stream
-    RocblasApi* R = rocblas_api();
-    const double minus1 = -1.0, one = 1.0;
-    for (int64_t i = L.off; i < L.off + L.cnt; ++i) {
-      const GemmTask& g = h->hgt[i];
-      if (R->dgemm(h->rocblas, kRbOpNone, kRbOpNone, g.m, g.n, g.k, &minus1, g.A, g.lda, g.B, g.ldb, &one,
-                   g.C, g.ldc) != 0)
-        return hipErrorLaunchFailure;
-    }
-    return hipSuccess;
-  }
   switch (L.kind) {
     case K_FORK: {
       hipError_t e = hipEventRecord(h->ev_fork, h->stream);
@@ -2579,8 +2377,8 @@ launches:
 // factorization runs eagerly).
 static int factor_segment(smlu_handle* h, Timer& tm, int seg) {
   hipStream_t st = h->stream;
-  static const bool dbg = std::getenv("SMLU_DEBUG_SYNC") != nullptr;
-  static const bool nograph = std::getenv("SMLU_NO_GRAPH") != nullptr;
+  const Tune tn = tune();
+  const bool dbg = tn.debug_sync, nograph = tn.no_graph;
   const int prof = h->opts.profile ? 1 : 0;
   const size_t nseg = h->fac_seg.size();
   if (h->fac_execs.size() != nseg || (seg == 0 && h->fac_exec_profile != prof)) {
@@ -2831,7 +2629,7 @@ static bool has_tile_fronts(const smlu_handle* h) {
 static int run_factor(smlu_handle* h) {
   int rc = run_factor_once(h);
   if (rc < 0) return rc;
-  const bool off = std::getenv("SMLU_NO_REPIVOT") != nullptr;   // dev/test knob
+  const bool off = tune().no_repivot;   // test knob
   if ((rc == SMLU_SINGULAR || h->weak > 0) && h->pivmode == 0 && !off && has_tile_fronts(h) &&
       h->opts.pivot_tol > 0 && !h->plan.given_order && h->nranks == 1) {
     h->repivot_node = h->flag_node;
@@ -2916,7 +2714,7 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
   }
   // batches of up to SMLU_SWEEP_MAX_RHS (<= 8) right-hand sides run the sweeps (NR-wide hand-off
   // slots), wider ones the per-block launches (fwdm / bwdm)
-  static const int sweep_max_rhs = std::getenv("SMLU_SWEEP_MAX_RHS") ? std::atoi(std::getenv("SMLU_SWEEP_MAX_RHS")) : 1;
+  constexpr int sweep_max_rhs = 1;   // batches run the per-block schedule (the NR-wide sweep slots measured slower)
   const bool steps = rh.n > std::min(8, std::max(1, sweep_max_rhs)) && h->nranks == 1;
   // The sync-free sweeps' waits are bounded: a wait that gives up raises sstatus, which is read back
   // after every solve that ran them; the solve is then re-run on the per-block schedule (fwdm / bwdm,
@@ -2970,7 +2768,7 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
   // One GPU: the forward and backward sweeps (~1,400 launches at 128^3, fixed pointers: the
   // handle's wrk / vbuf) are captured once per (mode, rhs count) into a hipGraph and replayed;
   // only the permutation kernels see the caller's b and x.
-  static const bool nograph = std::getenv("SMLU_NO_GRAPH") != nullptr;
+  const bool nograph = tune().no_graph;
   if (h->nranks == 1 && !nograph && !h->graph_failed) {
     const int key = mode * 256 + rh.n;
     hipGraphExec_t ex = nullptr;
@@ -3110,7 +2908,7 @@ static int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, 
   h->cpair = preorder != nullptr && !h->plan.matched;
   if (!p && !h->plan.matched) h->dominant = diagonally_dominant(n, colptr, rowval, nzval, h->opts.index_base);
   if (nranks > 1) {
-    if (const char* e = std::getenv("SMLU_OB")) h->ob = std::max(64, (std::atoi(e) / 64) * 64);
+    if (tune().ob > 0) h->ob = tune().ob;
     h->plan.compute_owners(nranks, h->ob);
     h->opts.profile = 0;   // per-kind event timing is single-GPU only
   }
@@ -3153,10 +2951,9 @@ void smlu_default_opts(smlu_opts* o) {
   o->device = 0;
   o->profile = 0;
   o->leaf_size = 64;
-  o->use_mfma = std::getenv("SMLU_VALU_GEMM") ? 0 : 1;   // fp64 MFMA by default
+  o->use_mfma = 1;   // fp64 MFMA tiles (use_mfma = 0: the VALU tiles, a test/comparison path)
   o->refine = -1;
-  // hand-written MFMA tiles by default; rocBLAS only on request (comparison path)
-  o->vendor_gemm = (std::getenv("SMLU_ROCBLAS") && !std::getenv("SMLU_NO_ROCBLAS")) ? 1 : 0;
+  o->vendor_gemm = 0;   // reserved (the vendor GEMM comparison path was removed in round 5)
 }
 
 int smlu_create(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* nzval,
@@ -3676,7 +3473,7 @@ int smlu_solve(smlu_handle* h, const double* b, double* x) {
 static int solve_multi_dev(smlu_handle* h, int64_t nrhs, const double* d_B, int64_t ldb, double* d_X,
                            int64_t ldx) {
   const int steps = auto_refine_steps(h);
-  const bool batched = steps == 0 && h->nranks == 1 && nrhs > 1 && !std::getenv("SMLU_NO_MULTI_RHS");
+  const bool batched = steps == 0 && h->nranks == 1 && nrhs > 1;
   if (!batched) {
     for (int64_t j = 0; j < nrhs; ++j) {
       int rc = solve_refined(h, d_B + j * ldb, d_X + j * ldx);
@@ -4525,7 +4322,7 @@ double smlu_stat(const smlu_handle* h, const char* key) {
   if (k == "gemm_launches") return (double)h->gemm_launches;
   if (k == "gemm_bytes") return h->gemm_bytes;
   if (k == "gemm128_launches") return (double)h->gemm128_launches;
-  if (k == "vendor_calls") return (double)h->vendor_calls;
+  if (k == "vendor_calls") return 0.0;   // no vendor GEMM path (round 5)
   if (k.rfind("ms_", 0) == 0) {
     std::string name = k.substr(3);
     double t = 0;

@@ -10,8 +10,7 @@
     valu128  SMLU_T128MIN=1, use_mfma=0       the VALU 128x128 tile k_gemm128
     default  as shipped (k_gemm_k64 for k <= 64 launches, fused panels with tile inverses,
              k_urows, 64x64 tiles below the MFMA threshold)
-    rocblas  SMLU_ROCBLAS=1 SMLU_ROCBLAS_MIN=1 every F22 / trailing GEMM task through rocBLAS dgemm
-             (deterministic mode; opt-in comparison path, the default runs our tiles only)
+  (round 5 removed the rocBLAS comparison variant together with the library's vendor GEMM path)
 * Error paths of the reference surface: SingularException from lu(A) (src/SharedMemSparseLU.jl:74)
   and lu!(F, A) (:247), lu! with a changed pattern (the reallocate branch :252-273), the
   re-pivoting refactor (a zero or weak diagonal-tile pivot re-factors with full-candidate
@@ -31,10 +30,9 @@ pytestmark = pytest.mark.gpu
 
 VARIANTS = {
     "default": ({}, {}),
-    "mfma128": ({"SMLU_T128MIN": "1", "SMLU_NO_ROCBLAS": "1"}, {}),
-    "valu64": ({"SMLU_T128MIN": str(1 << 60), "SMLU_SMALLK": "0", "SMLU_NO_ROCBLAS": "1"}, {}),
-    "valu128": ({"SMLU_T128MIN": "1", "SMLU_NO_ROCBLAS": "1"}, {"use_mfma": False}),
-    "rocblas": ({"SMLU_ROCBLAS": "1", "SMLU_ROCBLAS_MIN": "1"}, {}),
+    "mfma128": ({"SMLU_T128MIN": "1"}, {}),
+    "valu64": ({"SMLU_T128MIN": str(1 << 60), "SMLU_SMALLK": "0"}, {}),
+    "valu128": ({"SMLU_T128MIN": "1"}, {"use_mfma": False}),
 }
 
 
@@ -57,10 +55,7 @@ def check_variant_ran(F, variant):
         assert F.stat("launches_mfma128") == 0 and F.stat("launches_k64") == 0
     elif variant == "valu128":
         assert F.stat("launches_valu128") > 0 and F.stat("launches_mfma128") == 0
-    if variant == "rocblas":
-        assert F.stat("vendor_calls") > 0
-    else:
-        assert F.stat("vendor_calls") == 0
+    assert F.stat("vendor_calls") == 0
 
 
 @pytest.mark.parametrize("variant", list(VARIANTS))
@@ -82,7 +77,7 @@ def test_poisson3d_nd_gemm_variants(gpu, monkeypatch, N, variant):
     assert isapprox(x, spla.spsolve(A, b), TOL, TOL)
 
 
-@pytest.mark.parametrize("variant", ["default", "mfma128", "rocblas"])
+@pytest.mark.parametrize("variant", ["default", "mfma128"])
 def test_poisson3d_32_nd_oracle(gpu, monkeypatch, variant):
     # the largest oracle case (~2.6 s on one core): root separator of 1024 pivots
     A = mats.poisson3d(32)

@@ -133,37 +133,3 @@ def test_forced_sweep_timeout_reruns_per_block(gpu, monkeypatch, name):
     F.close()
     Ft.close()
 
-
-def test_diag_inverse_mode(gpu, monkeypatch):
-    """SMLU_DIAG_INV=1 (opt-in): the large fronts' 64x64 diagonal blocks applied as products with
-    inverses computed after every factorization (k_diag_inv) instead of the 64-step substitution,
-    in the sweeps and in the per-block launches alike: the solution agrees with the default to
-    rounding, and batch columns (per-block launches) are bitwise the single (sweep) solves."""
-    import torch
-    A = _cases()["poisson3d_28"]
-    n = A.shape[0]
-    F = smlu.ParallelSparseLU(A)
-    monkeypatch.setenv("SMLU_DIAG_INV", "1")
-    Fi = smlu.ParallelSparseLU(A)
-    monkeypatch.delenv("SMLU_DIAG_INV")
-    b = np.random.default_rng(8).random(n)
-    x, xi = np.empty(n), np.empty(n)
-    smlu.ldiv_(x, F, b)
-    smlu.ldiv_(xi, Fi, b)
-    assert isapprox(xi, x, TOL, TOL)
-    assert np.abs(A @ xi - b).max() <= 1e-12 * np.abs(b).max()
-    dev = torch.device("cuda:0")
-    B = torch.from_numpy(np.random.default_rng(9).random((4, n))).to(dev)
-    X = torch.empty_like(B)
-    Fi.solve_multi_device(X, B)
-    y = torch.empty(n, dtype=torch.float64, device=dev)
-    for j in range(4):
-        Fi.solve_device(y, B[j].contiguous())
-        assert torch.equal(y, X[j]), j
-    # a refactor recomputes the inverses from the new factors
-    A2 = mats.perturb_diag(A, 5)
-    smlu.lu_(Fi, A2)
-    smlu.ldiv_(xi, Fi, b)
-    assert np.abs(A2 @ xi - b).max() <= 1e-12 * np.abs(b).max()
-    F.close()
-    Fi.close()

@@ -1,8 +1,8 @@
 """Solve timings at 3D Poisson N^3 on one GPU (dev measurement): one right-hand side (median of 7
 solves), 8 right-hand sides batched (median of 3), each after a warm-up call, plus the refactor
-time.  Run it once per configuration (environment knobs are read once per process):
+time:
 
-    SMLU_SWEEP_MAX_RHS=8 python tools/solve_bench.py 128
+    python tools/solve_bench.py 128
 """
 import json
 import os
