@@ -101,14 +101,6 @@ struct Rhs {
 constexpr int kMultiRhs = 16;   // right-hand sides per solve launch
 constexpr int kSweepWK = 4;     // k_tri_sweep: 64-row blocks (worker waves) per work item
 constexpr int kSweepXB = 64;    // k_tri_sweep: external blocks x right-hand sides per run (LDS 32 KB)
-// Inverses of the large fronts' 64x64 diagonal blocks for the solves (k_diag_inv): block b of front s
-// (base[s] >= 0) at inv + ((base[s] + b) * 2 + upper) * 4096, column-major; base == nullptr or
-// base[s] < 0: substitution.
-struct DiagInv {
-  const int64_t* base;
-  const double* inv;
-};
-
 // One dense chunk of the reference's solve layout (src/SharedMemSparseLU.jl:101-243), 0-based:
 // the s x s diagonal block over x[c0, c0+s) at data[tri] (column-major, ld s) and the negated
 // nr x s rectangle over rows x[r0, r0+nr) at data[rect] (column-major, ld nr).

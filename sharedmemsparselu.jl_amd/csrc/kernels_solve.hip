@@ -546,57 +546,6 @@ __global__ __launch_bounds__(256) void k_fwd_pull(const FrontTile* __restrict__ 
   }
 }
 
-// Diagonal block of a large front for the vector held one element per lane: with the block's inverse
-// (row `lane` of it in row), a product -- the 64 broadcasts are independent of each other and the
-// dependent chain is dot64_split's 8 + 3 fp64 operations; without, the substitution (tri64_row).
-template <bool UPPER>
-__device__ __forceinline__ double diag_solve(double xi, const double (&row)[64], double dinv, int bw, bool inv) {
-  if (inv) return dot64_split(row, bw, [&](int j) { return readlane_f64(xi, j); });
-  return tri64_row<UPPER>(xi, row, dinv, bw);
-}
-
-// Inverses of the large fronts' 64x64 diagonal blocks (DiagInv), recomputed by the first launch of a
-// solve: one wave per block, lane c forms column c -- unit lower: x_i = -sum_{j<i} L_ij x_j
-// (x_c = 1); upper: x_i = (delta_ic - sum_{j>i} U_ij x_j) / U_ii -- with the block in LDS (rows
-// broadcast), x in registers.  Entries outside the bw x bw block are zero.
-template <bool UPPER>
-__global__ __launch_bounds__(64) void k_diag_inv(const int32_t* __restrict__ front, const int64_t* __restrict__ base,
-                                                 const SNode* __restrict__ sn, const double* __restrict__ store,
-                                                 double* __restrict__ inv) {
-  __shared__ double sD[64][65];   // sD[j][i] = block(i, j)
-  const int64_t g = blockIdx.x;
-  const int s_id = front[g];
-  const SNode s = sn[s_id];
-  const int64_t M = (int64_t)s.ns + s.nu, jb = (g - base[s_id]) * 64;
-  const int bw = (int)min<int64_t>(64, (int64_t)s.ns - jb);
-  const double* D = store + s.Loff + jb * M + jb;
-  const int c = threadIdx.x;
-  for (int j = 0; j < 64; ++j) sD[j][c] = (c < bw && j < bw) ? D[(int64_t)j * M + c] : 0.0;
-  __syncthreads();
-  double x[64];
-  if (!UPPER) {
-#pragma unroll
-    for (int i = 0; i < 64; ++i) {
-      double acc = 0.0;
-#pragma unroll
-      for (int j = 0; j < i; ++j) acc = fma(sD[j][i], x[j], acc);
-      x[i] = (i < bw && c < bw) ? (i == c ? 1.0 : (i < c ? 0.0 : -acc)) : 0.0;
-    }
-  } else {
-#pragma unroll
-    for (int i = 63; i >= 0; --i) {
-      double acc = 0.0;
-#pragma unroll
-      for (int j = i + 1; j < 64; ++j) acc = fma(sD[j][i], x[j], acc);
-      const double di = i < bw ? recip(sD[i][i]) : 0.0;
-      x[i] = (i < bw && c < bw) ? ((i == c ? 1.0 : 0.0) - acc) * di : 0.0;
-    }
-  }
-  double* out = inv + (g * 2 + (UPPER ? 1 : 0)) * 4096 + (int64_t)c * 64;
-#pragma unroll
-  for (int i = 0; i < 64; ++i) out[i] = x[i];
-}
-
 // One 64-column step of a large front: the first CW waves of every workgroup solve the 64x64
 // diagonal block for the right-hand sides (tri64, the diagonal block's rows loaded once per wave,
 // CW right-hand sides at a time; each workgroup re-solves it, no inter-workgroup hand-off); the
@@ -607,8 +556,7 @@ __global__ __launch_bounds__(64) void k_diag_inv(const int32_t* __restrict__ fro
 template <bool UPPER, int NR>
 __global__ __launch_bounds__(NR == 1 ? 320 : 512) __attribute__((amdgpu_waves_per_eu(1, 2)))
 void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step, const SNode* __restrict__ sn,
-                 const double* __restrict__ store, double* __restrict__ x, double* __restrict__ vbuf, Rhs rh,
-                 DiagInv di) {
+                 const double* __restrict__ store, double* __restrict__ x, double* __restrict__ vbuf, Rhs rh) {
   constexpr int CW = NR == 1 ? 1 : 4;        // chain waves
   constexpr int PR = (NR + CW - 1) / CW;     // right-hand sides per chain wave
   __shared__ double xs[64][NR];
@@ -631,22 +579,14 @@ void k_tri_block(const FrontTile* __restrict__ ft, int nft, int step, const SNod
       xi[k] = (r < nr && lane < bw) ? vbuf[r * rh.ldv + s.voff + jb + lane] : 0.0;
     }
     double row[64];   // the diagonal block's row `lane`, loaded once for all right-hand sides
-    double dinv = 1.0;
-    const int64_t ib = di.base ? di.base[ft[fi].s] : -1;
-    if (ib >= 0) {   // row `lane` of the block's inverse
-      const double* Inv = di.inv + ((ib + jb / 64) * 2 + (UPPER ? 1 : 0)) * 4096;
-#pragma unroll
-      for (int j = 0; j < 64; ++j) row[j] = (lane < bw && j < bw) ? Inv[j * 64 + lane] : 0.0;
-    } else {
-      load_tri_row64<UPPER>(row, Lp + jb * M + jb, M, bw, lane);
-      dinv = UPPER ? diag_recip(Lp + jb * M + jb, M, bw, lane) : 1.0;
-      if (UPPER) tri64_scale_upper(row, dinv, bw);
-    }
+    load_tri_row64<UPPER>(row, Lp + jb * M + jb, M, bw, lane);
+    const double dinv = UPPER ? diag_recip(Lp + jb * M + jb, M, bw, lane) : 1.0;
+    if (UPPER) tri64_scale_upper(row, dinv, bw);
 #pragma unroll
     for (int k = 0; k < PR; ++k) {
       const int r = wv + k * CW;
       if (r < nr) {
-        const double y = diag_solve<UPPER>(xi[k], row, dinv, bw, ib >= 0);
+        const double y = tri64_row<UPPER>(xi[k], row, dinv, bw);
         if (lane < bw) {
           xs[lane][r] = y;
           if (chunk == 0) x[r * rh.ldx + s.first + jb + lane] = y;
@@ -767,7 +707,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* __restrict__ tick,
                  int32_t* __restrict__ flags0, double* __restrict__ xh, int32_t* __restrict__ status,
                  const SNode* __restrict__ sn, const double* __restrict__ store, double* __restrict__ x,
-                 double* __restrict__ vbuf, Rhs rh, int spin, DiagInv di) {
+                 double* __restrict__ vbuf, Rhs rh, int spin) {
   __shared__ double xs[64][NR];
   __shared__ unsigned long long s_ticket;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -802,23 +742,16 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
   // the diagonal block's row of a pivot row, loaded up front (off the chain's critical path)
   double drow[64];
   double dinv = 1.0;
-  const int64_t ib = di.base ? di.base[ft[fi].s] : -1;
   {
     const bool piv = has && myblk < nblk;
     const int64_t b = piv ? myblk : 0;
     const int bw = (int)min<int64_t>(64, ns - 64 * b);
     const int li = (int)(row - 64 * b);
-    if (ib >= 0) {   // row `li` of the block's inverse
-      const double* Inv = di.inv + ((ib + b) * 2 + (UPPER ? 1 : 0)) * 4096 + (piv ? li : 0);
 #pragma unroll
-      for (int j = 0; j < 64; ++j) drow[j] = (piv && j < bw) ? Inv[j * 64] : 0.0;
-    } else {
-#pragma unroll
-      for (int j = 0; j < 64; ++j)
-        drow[j] = (piv && j < bw && (UPPER ? j > li : j < li)) ? Lp[(64 * b + j) * M + row] : 0.0;
-      if (UPPER && piv) dinv = recip(Lp[(64 * b + li) * M + row]);
-      if (UPPER) tri64_scale_upper(drow, dinv, bw);
-    }
+    for (int j = 0; j < 64; ++j)
+      drow[j] = (piv && j < bw && (UPPER ? j > li : j < li)) ? Lp[(64 * b + j) * M + row] : 0.0;
+    if (UPPER && piv) dinv = recip(Lp[(64 * b + li) * M + row]);
+    if (UPPER) tri64_scale_upper(drow, dinv, bw);
   }
   double d[64];   // my row of the column block being applied, loaded before its x is available
   auto load_tile = [&](int64_t c, int bw) {
@@ -859,7 +792,7 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
         if (r < nr) {
-          const double y = diag_solve<UPPER>(o[r], drow, dinv, bw, ib >= 0);
+          const double y = tri64_row<UPPER>(o[r], drow, dinv, bw);
           const bool mine = lane < bw && has;
           if (mine) o[r] = y;
           atomic_write_f64(xhf + (b * kMultiRhs + r) * 64 + lane, mine ? y : 0.0);
@@ -1276,22 +1209,14 @@ hipError_t launch_fwd_gather(hipStream_t st, int cnt, const int32_t* list, const
   k_fwd_gather<<<dim3((unsigned)cnt, (unsigned)rh.n), 256, 0, st>>>(list, sn, chlist, relmap, rowperm, x, vbuf, rh);
   return hipGetLastError();
 }
-hipError_t launch_diag_inv(hipStream_t st, bool upper, int64_t nblocks, const int32_t* front, const int64_t* base,
-                           const SNode* sn, const double* store, double* inv) {
-  if (nblocks <= 0) return hipSuccess;
-  if (upper) k_diag_inv<true><<<(unsigned)nblocks, 64, 0, st>>>(front, base, sn, store, inv);
-  else k_diag_inv<false><<<(unsigned)nblocks, 64, 0, st>>>(front, base, sn, store, inv);
-  return hipGetLastError();
-}
 hipError_t launch_tri_block(hipStream_t st, bool upper, int64_t nwg, const FrontTile* ft, int nft,
-                            int step, const SNode* sn, const double* store, double* x, double* vbuf, Rhs rh,
-                            DiagInv di) {
+                            int step, const SNode* sn, const double* store, double* x, double* vbuf, Rhs rh) {
   if (nwg <= 0) return hipSuccess;
   if (rh.n < 1 || rh.n > kMaxRhs) return hipErrorInvalidValue;
   // one chain wave for a single vector (320 threads), four for a batch (512)
 #define SMLU_TRI(NRV, THR)                                                                           \
-  (upper ? (k_tri_block<true, NRV><<<(unsigned)nwg, THR, 0, st>>>(ft, nft, step, sn, store, x, vbuf, rh, di)) \
-         : (k_tri_block<false, NRV><<<(unsigned)nwg, THR, 0, st>>>(ft, nft, step, sn, store, x, vbuf, rh, di)))
+  (upper ? (k_tri_block<true, NRV><<<(unsigned)nwg, THR, 0, st>>>(ft, nft, step, sn, store, x, vbuf, rh)) \
+         : (k_tri_block<false, NRV><<<(unsigned)nwg, THR, 0, st>>>(ft, nft, step, sn, store, x, vbuf, rh)))
   if (rh.n == 1) SMLU_TRI(1, 320);
   else if (rh.n <= 4) SMLU_TRI(4, 512);
   else if (rh.n <= 8) SMLU_TRI(8, 512);
@@ -1312,14 +1237,13 @@ hipError_t launch_bwd_u12(hipStream_t st, int64_t nwg, const FrontTile* ft, int 
 }
 hipError_t launch_tri_sweep(hipStream_t st, bool upper, int64_t nwg, const FrontTile* ft, int nft,
                             unsigned long long* tick, int32_t* flags, double* xh, int32_t* status, const SNode* sn,
-                            const double* store, double* x, double* vbuf, Rhs rh, int spin, DiagInv di) {
+                            const double* store, double* x, double* vbuf, Rhs rh, int spin) {
   if (nwg <= 0) return hipSuccess;
-  // up to 8 right-hand sides (NR-wide hand-off slots; with the diagonal-block inverses each block's
-  // solve is one product per right-hand side); wider batches take the per-block schedule
+  // up to 8 right-hand sides (NR-wide hand-off slots); wider batches take the per-block schedule
   if (rh.n < 1 || rh.n > 8) return hipErrorInvalidValue;
 #define SWEEP(NR)                                                                                                   \
-  (upper ? (k_tri_sweep<true, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh, spin, di)) \
-         : (k_tri_sweep<false, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh, spin, di)))
+  (upper ? (k_tri_sweep<true, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh, spin)) \
+         : (k_tri_sweep<false, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh, spin)))
   if (rh.n == 1) SWEEP(1);
   else if (rh.n <= 4) SWEEP(4);
   else SWEEP(8);

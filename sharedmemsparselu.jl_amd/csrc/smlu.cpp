@@ -60,13 +60,11 @@ hipError_t launch_fwd_pull(hipStream_t, int64_t, const FrontTile*, int, const SN
 hipError_t launch_fwd_gather(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                              const int32_t*, double*, double*, Rhs);
 hipError_t launch_tri_block(hipStream_t, bool, int64_t, const FrontTile*, int, int, const SNode*,
-                            const double*, double*, double*, Rhs, DiagInv);
+                            const double*, double*, double*, Rhs);
 hipError_t launch_bwd_u12(hipStream_t, int64_t, const FrontTile*, int, const SNode*, const int32_t*,
                           const double*, const double*, double*, Rhs);
-hipError_t launch_diag_inv(hipStream_t, bool, int64_t, const int32_t*, const int64_t*, const SNode*, const double*,
-                           double*);
 hipError_t launch_tri_sweep(hipStream_t, bool, int64_t, const FrontTile*, int, unsigned long long*, int32_t*, double*,
-                            int32_t*, const SNode*, const double*, double*, double*, Rhs, int, DiagInv);
+                            int32_t*, const SNode*, const double*, double*, double*, Rhs, int);
 hipError_t launch_fwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const int32_t*,
                       const int32_t*, const double*, double*, double*, Rhs);
 hipError_t launch_bwd(hipStream_t, int, const int32_t*, const SNode*, const int32_t*, const double*,
@@ -106,11 +104,11 @@ thread_local std::string g_last_error;
 enum Kind : int {
   K_MEMSET_STORE, K_MEMSET_SCRATCH, K_SCATTER, K_EXTADD, K_FRONT_LDS, K_PANEL, K_TRSMU, K_TRSML,
   K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_GEMM22, K_LASWP, K_STEPTRSM, K_GEMMU,
-  K_GEMMO, K_FORK, K_JOIN, K_TRIINV, K_BWDU12C, K_VCOPY, K_FWDT, K_BWDT, K_SWEEPF, K_SWEEPB, K_UROWS, K_FWDP, K_NKIND
+  K_GEMMO, K_TRIINV, K_BWDU12C, K_VCOPY, K_FWDT, K_BWDT, K_SWEEPF, K_SWEEPB, K_UROWS, K_FWDP, K_NKIND
 };
 const char* kKindName[] = {"memset", "memset", "assemble", "assemble", "small", "panel",
                                   "trsm", "trsm", "gemm", "solve", "solve", "solve", "solve",
-                                  "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "sync", "sync", "trsm", "solve", "solve",
+                                  "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "trsm", "solve", "solve",
                                   "solve", "solve", "solve", "solve", "urows", "solve"};
 static_assert(sizeof(kKindName) / sizeof(kKindName[0]) == K_NKIND, "one kKindName entry per launch kind");
 constexpr int kSolveBigNs = 256;  // fronts with more pivots use the multi-workgroup solve
@@ -127,7 +125,6 @@ struct Launch {
   int64_t off = 0, cnt = 0, nwg = 0, aux = 0, aux2 = 0;
   int64_t off2 = 0, cnt2 = 0, nwg2 = 0;   // second work list (merged launches)
   double flops = 0;
-  int side = 0;                           // 1 = issued on the look-ahead stream
 };
 
 template <class T>
@@ -295,8 +292,6 @@ struct smlu_handle {
   Plan plan;
   int device = 0;
   hipStream_t stream = nullptr;
-  hipStream_t side = nullptr;             // look-ahead stream (trailing updates beyond the next block)
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::string err;
   int64_t errcol = -1;
   bool have_numeric = false;
@@ -325,10 +320,6 @@ struct smlu_handle {
   DBuf<int2> aents;
   DBuf<FrontTile> ftiles;
   DBuf<int32_t> gptr, gent;       // pull lists of the large fronts' forward gather (k_fwd_pull)
-  DBuf<int64_t> invbase;          // large fronts' diagonal-block inverses (k_diag_inv): first block per front
-  DBuf<int32_t> invfront;         // ... front of each block
-  DBuf<double> dinvbuf;           // ... L and U inverses, 2 x 4096 doubles per block
-  int64_t ninv = 0;
   DBuf<int32_t> ssync, sstatus;   // sync-free solve sweeps: block flags (epochs, never reset); timeouts
   DBuf<unsigned long long> stick; // ... one monotone ticket counter per sweep launch
   DBuf<double> sxh;               // ... hand-off slots: 64 x kMultiRhs doubles per flag
@@ -394,11 +385,7 @@ struct smlu_handle {
   int64_t comm_calls = 0;
   size_t fac_graph_events = 0;
   bool graph_failed = false;
-  bool lookahead = false;     // SMLU_LOOKAHEAD=1: trailing updates beyond the next block on a side stream
   int ob = kOBDefault;        // outer block width (SMLU_OB overrides; multiple of 64)
-  int64_t sb = kOBDefault;     // super-block width of the GEMM-form fronts (SMLU_SB; multiple of ob;
-                              // == ob: two-level scheme, the default -- SB 768..6144 measured 537..550 ms
-                              // vs 531 at 128^3: the extra sub-panel TRSMs cost more than k = SB gains)
   int64_t t128_min = 512;     // 128x128 GEMM tiles when a launch has at least this many
   bool small_k = true;        // k <= 64 launches use k_gemm_k64 (SMLU_SMALLK=0: off)
   bool dominant = false;      // A diagonally dominant (by rows or columns): last host values seen
@@ -413,8 +400,6 @@ struct smlu_handle {
   double repivot_growth = 0;
   SNode repivot_sn{};         //   and that node's record (mode, ns, nu) in the schedule that flagged it
   bool trsm_gemm = true;      // GEMM-form triangular solves of the blocked fronts
-  bool trsm_gemm64_only = false;   // SMLU_TRSM_GEMM=2: only for diagonal-tile (nb = 64) fronts
-  int64_t side_wg = 0;        // grid cap of look-ahead GEMMs (SMLU_SIDE_WG; 0 = uncapped)
   // ComplexF64 handle (smlu_create_z): the plan and factors are those of the real-equivalent K
   bool zc = false;
   bool cpair = false;                // pair-preserving pivots (complex handle, no row transversal)
@@ -450,9 +435,6 @@ struct smlu_handle {
     ftiles.free();
     gptr.free();
     gent.free();
-    invbase.free();
-    invfront.free();
-    dinvbuf.free();
     ssync.free();
     sstatus.free();
     stick.free();
@@ -495,11 +477,6 @@ struct smlu_handle {
     ev_kind.clear();
     rb.free();
     if (ev_caller) (void)hipEventDestroy(ev_caller);
-    if (ev_fork) (void)hipEventDestroy(ev_fork);
-    if (ev_join) (void)hipEventDestroy(ev_join);
-    ev_fork = ev_join = nullptr;
-    if (side) (void)hipStreamDestroy(side);
-    side = nullptr;
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
   }
@@ -631,8 +608,6 @@ static int build_schedule(smlu_handle* h) {
   std::vector<XContrib> xt;
   std::vector<FrontTile> ft;
   std::vector<int32_t> gptr, gent;   // k_fwd_pull lists
-  std::vector<int64_t> invbase;      // k_diag_inv: first block of each large front (-1: none)
-  std::vector<int32_t> invfront;
   std::vector<GemmTask> gt;
   std::vector<SwapTask> st_tasks;
   std::vector<URowTask> ur_tasks;
@@ -711,7 +686,6 @@ static int build_schedule(smlu_handle* h) {
   // GEMM-form TRSM (k_tri_inv + GEMM tasks) needs the growth epilogue of the MFMA/64 tiles
   // (the 32-wide panels keep k_step_trsm: measured best)
   h->trsm_gemm = h->opts.use_mfma;
-  h->trsm_gemm64_only = true;
   // GEMM tasks whose A or B operand lives in the tinv buffer (allocated after the schedule)
   std::vector<std::pair<int64_t, int64_t>> tinv_patch;   // (gt index * 2 + operand B?, offset)
   h->gemm_flops = 0;
@@ -723,7 +697,7 @@ static int build_schedule(smlu_handle* h) {
   // GEMM launches: 128x128 tiles when the launch has enough of them to fill the GPU,
   // otherwise 64x64 tiles (same per-element arithmetic, bitwise-identical results).
   auto add_gemm_launch = [&](std::vector<GemmTask>& cand, double fl, int step, int kind = K_GEMM,
-                             int side = 0, const std::vector<int64_t>* tpatch = nullptr) {
+                             const std::vector<int64_t>* tpatch = nullptr) {
     if (cand.empty()) return;
     const bool count = kind != K_TRSML;   // GEMM-form TRSM is accounted as "trsm", not GEMM
     int64_t t128 = 0;
@@ -740,7 +714,6 @@ static int build_schedule(smlu_handle* h) {
       std::stable_sort(cand.begin(), cand.end(), [](const GemmTask& a, const GemmTask& b) { return a.k > b.k; });
     Launch L;
     L.kind = step < 0 ? K_GEMM22 : kind;
-    L.side = side;
     L.step = step;
     L.off = (int64_t)gt.size();
     L.aux = tile;
@@ -768,17 +741,15 @@ static int build_schedule(smlu_handle* h) {
   // fronts whose triangular solves run in GEMM form (tile inverses); they also take the
   // super-block level of the three-level blocking (SB columns; OB for the others)
   auto gform = [&](int64_t s) {
-    return h->trsm_gemm && (h->hsn[s].nb == kNbTile || !h->trsm_gemm64_only);
+    return h->trsm_gemm && h->hsn[s].nb == kNbTile;
   };
-  h->sb = h->ob;   // two-level blocking (a super-block level measured slower: DESIGN.md §8)
-  auto sbw = [&](int64_t s) -> int64_t { return (gform(s) && !h->lookahead && h->nranks == 1) ? h->sb : h->ob; };
-  const int64_t spf = std::max<int64_t>(h->sb, h->ob) / 32;   // swap / tile-inverse slots per front
+  const int64_t spf = h->ob / 32;   // swap / tile-inverse slots per front
   // fused panels (k_panel_blk<16, true>: panel + tile inverses + in-block row interchanges) for
   // the GEMM-form fronts (every 64-wide panel then belongs to one); SMLU_FUSED_PANEL=0: three launches
   // 2 (default): panel + the in-block row interchanges (no k_laswp inside the block) + the tile
   // inverses by 16 x 16 blocks on the matrix cores (no k_tri_inv); 1: without the inverses;
   // 0: three launches
-  const int fuse_mode = !(h->trsm_gemm && h->trsm_gemm64_only && h->ob <= 64 + 16 * 20) ? 0 : 2;
+  const int fuse_mode = !(h->trsm_gemm && h->ob <= 64 + 16 * 20) ? 0 : 2;
   const bool fuse_panel = fuse_mode > 0, fuse_inv = fuse_mode == 2;
   // fused U rows at the end of an outer block (k_urows) for the GEMM-form fronts; SMLU_FUSED_UROWS=0:
   // one TRSM + one update launch per sub-panel
@@ -951,14 +922,6 @@ static int build_schedule(smlu_handle* h) {
     max_list = std::max<int64_t>(max_list, dist_slots + (int64_t)big.size() * spf);
     // swap-list slot of sub-panel u of a front's current outer block
     auto slot_of = [&](int64_t s, int64_t u) { return dist_slots + bidx[s] * spf + u; };
-    bool side_busy = false;
-    auto join = [&]() {
-      if (!side_busy) return;
-      Launch J;
-      J.kind = K_JOIN;
-      h->fac.push_back(J);
-      side_busy = false;
-    };
     for (int64_t t = 0; t < maxsteps; ++t) {
       std::vector<int64_t> act;
       for (auto s : big) {
@@ -989,7 +952,7 @@ static int build_schedule(smlu_handle* h) {
             rmax = std::max(rmax, r.mode == 1 ? r.ns - kb : w);
             wmax = std::max<int64_t>(wmax, r.nb);
             ilist.push_back((int32_t)act[pos]);
-            ilist.push_back((int32_t)slot_of(act[pos], t % (sbw(act[pos]) / r.nb)));
+            ilist.push_back((int32_t)slot_of(act[pos], t % (h->ob / r.nb)));
             ++pos;
             ++cnt;
           }
@@ -1011,7 +974,7 @@ static int build_schedule(smlu_handle* h) {
         for (auto s : act) {
           if (!gform(s) || fuse_inv) continue;   // fused into the panel launch
           ilist.push_back((int32_t)s);
-          ilist.push_back((int32_t)slot_of(s, t % (sbw(s) / h->hsn[s].nb)));
+          ilist.push_back((int32_t)slot_of(s, t % (h->ob / h->hsn[s].nb)));
         }
         L.cnt = ((int64_t)ilist.size() - L.off) / 2;
         if (L.cnt > 0) h->fac.push_back(L);
@@ -1029,7 +992,7 @@ static int build_schedule(smlu_handle* h) {
           int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
           int64_t ncol = oend - ostart - w;
           if (ncol <= 0 || (fuse_panel && gform(s))) continue;   // fused panels swap these rows themselves
-          st_tasks.push_back(SwapTask{(int32_t)s, (int32_t)kb, 1, (int32_t)slot_of(s, t % (sbw(s) / r.nb)),
+          st_tasks.push_back(SwapTask{(int32_t)s, (int32_t)kb, 1, (int32_t)slot_of(s, t % (h->ob / r.nb)),
                                       (int32_t)ostart, (int32_t)oend, (int32_t)kb, (int32_t)(kb + w), wg});
           wg += (ncol + 63) / 64;
         }
@@ -1082,7 +1045,7 @@ static int build_schedule(smlu_handle* h) {
           const SNode& r = h->hsn[s];
           int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb, w = std::min<int64_t>(r.nb, r.ns - kb);
           int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
-          const int64_t slot = slot_of(s, t % (sbw(s) / r.nb));
+          const int64_t slot = slot_of(s, t % (h->ob / r.nb));
           if (oend - kb - w > 0) {
             GemmTask g{};
             g.B = g.C = store + r.Loff + (kb + w) * M + kb;
@@ -1102,7 +1065,7 @@ static int build_schedule(smlu_handle* h) {
             tp.push_back(tinv_slot_off(slot, true) * 2 + 1);
           }
         }
-        add_gemm_launch(cand, 0.0, (int)t, K_TRSML, 0, &tp);
+        add_gemm_launch(cand, 0.0, (int)t, K_TRSML, &tp);
       }
       // inner trailing update: rows [kb+w, M) x columns [kb+w, oend) of the outer block
       {
@@ -1136,7 +1099,6 @@ static int build_schedule(smlu_handle* h) {
         if (kb + w == oend) fin_all.push_back(s);
       }
       if (fin_all.empty()) continue;
-      join();   // the previous block's look-ahead update has written these columns
       {
         L = Launch();
         L.kind = K_LASWP;
@@ -1150,7 +1112,7 @@ static int build_schedule(smlu_handle* h) {
           int64_t ncol = M - (oend - ostart);
           if (ncol <= 0) continue;
           st_tasks.push_back(SwapTask{(int32_t)s, (int32_t)ostart, (int32_t)((oend - ostart + r.nb - 1) / r.nb),
-                                      (int32_t)slot_of(s, (ostart % sbw(s)) / r.nb), 0, (int32_t)M, (int32_t)ostart,
+                                      (int32_t)slot_of(s, (ostart % h->ob) / r.nb), 0, (int32_t)M, (int32_t)ostart,
                                       (int32_t)oend, wg});
           wg += (ncol + 63) / 64;
         }
@@ -1158,12 +1120,8 @@ static int build_schedule(smlu_handle* h) {
         L.nwg = wg;
         if (wg > 0) h->fac.push_back(L);
       }
-      // Three-level blocking: outer blocks (OB) are grouped in super-blocks (SB, GEMM-form
-      // fronts only, SMLU_SB).  At the end of an OB that does not close its SB, the OB's U rows
-      // and the trailing update reach only the SB's own columns [oend, se); at the end of the
-      // SB, its U rows for every column right of it are solved OB by OB (each OB's rows
-      // updated by the earlier ones, k = OB width), then one trailing update with k = SB
-      // width covers the rest of the front.  SB == OB is the plain two-level scheme.
+      // End of an outer block: its U rows on every column right of it (sub-panel by sub-panel,
+      // k_urows or GEMM-form TRSM), then the trailing update with k = OB width
       struct URows {
         int64_t s, ob0, ob1, c0, c1;   // OB rows [ob0, ob1); L-panel columns [c0, c1); + U12 if u12
         bool u12;
@@ -1186,7 +1144,7 @@ static int build_schedule(smlu_handle* h) {
               continue;
             }
             const int64_t M = (int64_t)r.ns + r.nu;
-            const int32_t slot0 = (int32_t)slot_of(it.s, (it.ob0 % sbw(it.s)) / r.nb);
+            const int32_t slot0 = (int32_t)slot_of(it.s, (it.ob0 % h->ob) / r.nb);
             for (int64_t c = it.c0; c < it.c1; c += kUrowsCols)
               ur_tasks.push_back(URowTask{(int32_t)it.s, (int32_t)it.ob0, (int32_t)it.ob1, slot0, (int32_t)M,
                                           (int32_t)std::min<int64_t>(kUrowsCols, it.c1 - c), r.Loff + c * M});
@@ -1219,7 +1177,7 @@ static int build_schedule(smlu_handle* h) {
             const int64_t wu = std::min<int64_t>(r.nb, it.ob1 - kbu);
             const int64_t n1 = it.c1 - it.c0;
             if (gform(s)) {   // U rows [kbu, kbu+wu) on the columns: L_uu^-1 C, in place
-              const int64_t off = tinv_slot_off(slot_of(s, (kbu % sbw(s)) / r.nb), false) * 2;
+              const int64_t off = tinv_slot_off(slot_of(s, (kbu % h->ob) / r.nb), false) * 2;
               if (n1 > 0) {
                 GemmTask g{};
                 g.B = g.C = store + r.Loff + it.c0 * M + kbu;
@@ -1269,7 +1227,7 @@ static int build_schedule(smlu_handle* h) {
           L.cnt = cnt;
           L.nwg = wg;
           if (wg > 0) h->fac.push_back(L);
-          add_gemm_launch(ctri, 0.0, (int)t, K_TRSML, 0, &tp);
+          add_gemm_launch(ctri, 0.0, (int)t, K_TRSML, &tp);
           add_gemm_launch(cand, fl, (int)t, K_GEMMU);
         }
       };
@@ -1300,83 +1258,21 @@ static int build_schedule(smlu_handle* h) {
           fl += 2.0 * (double)(ru1 - r0) * (double)r.nu * kk;
         }
       };
-      std::vector<URows> open_ob;                  // OBs that do not close their SB
-      std::vector<int64_t> close_sb;               // fronts whose SB ends here
+      std::vector<URows> items;
+      std::vector<GemmTask> c1;
+      double fl1 = 0;
       for (auto s : fin_all) {
         const SNode& r = h->hsn[s];
         const int64_t kb = t * r.nb, M = (int64_t)r.ns + r.nu;
         const int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
-        const int64_t ss = (ostart / sbw(s)) * sbw(s), se = std::min<int64_t>(r.ns, ss + sbw(s));
         if (oend == M) continue;   // nothing right of the block
-        if (oend < se) open_ob.push_back(URows{s, ostart, oend, oend, se, false});
-        else close_sb.push_back(s);
+        items.push_back(URows{s, ostart, oend, oend, r.ns, true});
+        rank_update(s, oend, M, oend, r.ns, false, ostart, oend, c1, fl1);
+        rank_update(s, oend, r.ns, oend, oend, true, ostart, oend, c1, fl1);   // U12 rows only
       }
-      // OBs inside their SB: U rows and trailing update on the SB's columns only
-      if (!open_ob.empty()) {
-        urows(open_ob);
-        std::vector<GemmTask> c1;
-        double fl1 = 0;
-        for (auto& it : open_ob) {
-          const SNode& r = h->hsn[it.s];
-          rank_update(it.s, it.ob1, (int64_t)r.ns + r.nu, it.c0, it.c1, false, it.ob0, it.ob1, c1, fl1);
-        }
-        add_gemm_launch(c1, fl1, (int)t, K_GEMMO);
-      }
-      // SBs ending here: their U rows on every column right of the SB, OB by OB, then the
-      // trailing update with k = SB width (look-ahead, when on, splits it over two streams)
-      if (!close_sb.empty()) {
-        int64_t nob = 0;
-        for (auto s : close_sb) {
-          const int64_t kb = t * h->hsn[s].nb, ostart = (kb / h->ob) * h->ob;
-          const int64_t ss = (ostart / sbw(s)) * sbw(s);
-          nob = std::max<int64_t>(nob, (ostart - ss) / h->ob + 1);
-        }
-        for (int64_t b = 0; b < nob; ++b) {
-          std::vector<URows> items;
-          std::vector<GemmTask> cb;
-          double flb = 0;
-          for (auto s : close_sb) {
-            const SNode& r = h->hsn[s];
-            const int64_t kb = t * r.nb, ostart = (kb / h->ob) * h->ob, M = (int64_t)r.ns + r.nu;
-            const int64_t ss = (ostart / sbw(s)) * sbw(s), se = std::min<int64_t>(r.ns, ostart + h->ob);
-            const int64_t b0 = ss + b * h->ob;
-            if (b0 >= se) continue;
-            const int64_t b1 = std::min<int64_t>(se, b0 + h->ob);
-            items.push_back(URows{s, b0, b1, se, r.ns, true});
-            // later OBs' rows of the SB receive this OB's contribution (right of the SB)
-            if (b1 < se) rank_update(s, b1, se, se, r.ns, true, b0, b1, cb, flb);
-            (void)M;
-          }
-          urows(items);
-          add_gemm_launch(cb, flb, (int)t, K_GEMMO);
-        }
-        std::vector<GemmTask> c1, c2;
-        double fl1 = 0, fl2 = 0;
-        for (auto s : close_sb) {
-          const SNode& r = h->hsn[s];
-          const int64_t M = (int64_t)r.ns + r.nu, kb = t * r.nb;
-          const int64_t ostart = (kb / h->ob) * h->ob, oend = std::min<int64_t>(r.ns, ostart + h->ob);
-          const int64_t ss = (ostart / sbw(s)) * sbw(s);
-          const int64_t oend2 = h->lookahead ? std::min<int64_t>(r.ns, oend + h->ob) : r.ns;
-          rank_update(s, oend, M, oend, oend2, false, ss, oend, c1, fl1);
-          if (h->lookahead) {
-            rank_update(s, oend, M, oend2, r.ns, false, ss, oend, c2, fl2);
-            rank_update(s, oend, r.ns, oend, oend, true, ss, oend, c2, fl2);   // U12 rows only
-          } else {
-            rank_update(s, oend, r.ns, oend, oend, true, ss, oend, c1, fl1);  // U12 rows only
-          }
-        }
-        if (!c2.empty()) {
-          Launch F;
-          F.kind = K_FORK;
-          h->fac.push_back(F);
-          add_gemm_launch(c2, fl2, (int)t, K_GEMMO, 1);
-          side_busy = true;
-        }
-        add_gemm_launch(c1, fl1, (int)t, K_GEMMO);
-      }
+      urows(items);
+      add_gemm_launch(c1, fl1, (int)t, K_GEMMO);
     }
-    join();
     // F22 -= L21 * U12 for the blocked fronts of this level
     {
       std::vector<GemmTask> cand;
@@ -1478,7 +1374,7 @@ static int build_schedule(smlu_handle* h) {
               cand.push_back(g);
               tp.push_back(tinv_slot_off(u, true) * 2 + 1);
             }
-            add_gemm_launch(cand, 0.0, step, K_TRSML, 0, &tp);
+            add_gemm_launch(cand, 0.0, step, K_TRSML, &tp);
             if (M - kb - wk > 0 && oe - kb - wk > 0) {
               GemmTask g{};
               g.A = Lb + kb * M + kb + wk;
@@ -1585,7 +1481,7 @@ static int build_schedule(smlu_handle* h) {
               fl += 2.0 * m * (double)(T.c1 - T.c0) * wu;
             }
           }
-          add_gemm_launch(ctri, 0.0, (int)(kbu / 64), K_TRSML, 0, &tp);
+          add_gemm_launch(ctri, 0.0, (int)(kbu / 64), K_TRSML, &tp);
           add_gemm_launch(cand, fl, (int)(kbu / 64), K_GEMMU);
         }
         {
@@ -1719,11 +1615,6 @@ static int build_schedule(smlu_handle* h) {
       // gather: one thread per front row pulls its own value and the children's contributions (in
       // child order) -- k_fwd_pull; pull lists per front row: gptr (CSR, relative to the front's
       // block) -> gent (vbuf index of each contribution)
-      if (invbase.empty()) invbase.assign((size_t)h->nnodes, -1);
-      for (auto s : bigs) {   // diagonal-block inverses for the solves of this front
-        invbase[s] = (int64_t)invfront.size();
-        for (int64_t b = 0; b < ((int64_t)h->hsn[s].ns + 63) / 64; ++b) invfront.push_back((int32_t)s);
-      }
       Launch L;
       L.kind = K_FWDP;
       L.off = (int64_t)ft.size();
@@ -2091,7 +1982,6 @@ static int build_schedule(smlu_handle* h) {
     expand_all(h->bwd, h->bwd_seg, true, h->bwdm, h->bwdm_seg);
   }
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
-  h->ninv = (int64_t)invfront.size();
   if (!gptr.empty()) {
     HIPCHK(h->gptr.upload(gptr.data(), gptr.size(), st));
     HIPCHK(h->gent.upload(gent.data(), gent.size(), st));
@@ -2182,9 +2072,6 @@ static int setup_device(smlu_handle* h) {
   int prio_lo = 0, prio_hi = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   if (!h->stream) HIPCHK(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi));
-  if (!h->side) HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_lo));
-  if (!h->ev_fork) HIPCHK(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming));
-  if (!h->ev_join) HIPCHK(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming));
   hipStream_t st = h->stream;
   // this rank's layout: the plan's own on one GPU; ordinary fronts + owned column blocks of
   // the shared fronts on a partitioned handle
@@ -2252,7 +2139,7 @@ struct Timer {
   hipStream_t st = nullptr;
   hipError_t begin(int kind, hipEvent_t* stop, hipStream_t s) {
     st = s;
-    if (!h->opts.profile || kind == K_FORK || kind == K_JOIN) { *stop = nullptr; return hipSuccess; }
+    if (!h->opts.profile) { *stop = nullptr; return hipSuccess; }
     if (used == h->ev_pool.size()) {
       hipEvent_t a, b;
       hipError_t e = hipEventCreate(&a);
@@ -2281,16 +2168,8 @@ struct Timer {
 };
 
 static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, double piv_tol) {
-  hipStream_t st = L.side ? h->side : h->stream;
+  hipStream_t st = h->stream;
   switch (L.kind) {
-    case K_FORK: {
-      hipError_t e = hipEventRecord(h->ev_fork, h->stream);
-      return e != hipSuccess ? e : hipStreamWaitEvent(h->side, h->ev_fork, 0);
-    }
-    case K_JOIN: {
-      hipError_t e = hipEventRecord(h->ev_join, h->side);
-      return e != hipSuccess ? e : hipStreamWaitEvent(h->stream, h->ev_join, 0);
-    }
     case K_MEMSET_STORE:
       return hipMemsetAsync(h->store.p + L.off, 0, (size_t)L.cnt * sizeof(double), st);
     case K_MEMSET_SCRATCH:
@@ -2321,7 +2200,7 @@ static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, d
     case K_GEMMU:
     case K_GEMMO:
     case K_GEMM22:
-      return launch_gemm(st, L.nwg, h->gtasks.p + L.off, (int)L.cnt, (int)L.aux, L.side ? h->side_wg : 0);
+      return launch_gemm(st, L.nwg, h->gtasks.p + L.off, (int)L.cnt, (int)L.aux, 0);
     case K_TRSML:
       return launch_gemm_g(st, L.nwg, h->gtasks.p + L.off, (int)L.cnt, (int)L.aux, 0, h->info.p,
                            h->growth.p, piv_tol);
@@ -2357,10 +2236,9 @@ launches:
   for (size_t li = lo; li < hi; ++li) {
     const Launch& L = h->fac[li];
     hipEvent_t stop;
-    HIPCHK(tm.begin(L.kind, &stop, L.side ? h->side : st));
+    HIPCHK(tm.begin(L.kind, &stop, st));
     hipError_t e = run_launch(h, L, diag_tol, piv_tol);
     if (e == hipSuccess && dbg) e = hipStreamSynchronize(st);
-    if (e == hipSuccess && dbg) e = hipStreamSynchronize(h->side);
     if (e != hipSuccess) {
       char buf[256];
       std::snprintf(buf, sizeof buf, "HIP error '%s' in launch kind=%d step=%d off=%lld cnt=%lld nwg=%lld aux=%lld aux2=%lld",
@@ -2439,11 +2317,6 @@ static int read_status(smlu_handle* h, const int32_t* info, int64_t nnodes, cons
 // After the last segment: pivot status of this rank's fronts.
 static int finish_factor(smlu_handle* h, Timer& tm, std::chrono::steady_clock::time_point t0) {
   Plan& P = h->plan;
-  hipStream_t st = h->stream;
-  if (h->dinvbuf.p) {   // the large fronts' diagonal-block inverses of the new factors, for the solves
-    HIPCHK(launch_diag_inv(st, false, h->ninv, h->invfront.p, h->invbase.p, h->sn.p, h->store.p, h->dinvbuf.p));
-    HIPCHK(launch_diag_inv(st, true, h->ninv, h->invfront.p, h->invbase.p, h->sn.p, h->store.p, h->dinvbuf.p));
-  }
   long long rec[16];
   int rs = read_status(h, h->info.p, h->nnodes, reinterpret_cast<const int32_t*>(h->growth.p), 2, rec);
   if (rs != SMLU_OK) return rs;
@@ -2584,9 +2457,6 @@ static void release_schedule(smlu_handle* h) {
   h->ftiles.free();
   h->gptr.free();
   h->gent.free();
-  h->invbase.free();
-  h->invfront.free();
-  h->dinvbuf.free();
   h->ssync.free();
   h->stick.free();
   h->sxh.free();
@@ -2668,10 +2538,10 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, d
                                h->rowperm.p, w, v, rh);
     case K_TRIF:
       return launch_tri_block(st, false, L.nwg, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p,
-                              h->store.p, w, v, rh, DiagInv{h->invbase.p, h->dinvbuf.p});
+                              h->store.p, w, v, rh);
     case K_TRIB:
       return launch_tri_block(st, true, L.nwg, h->ftiles.p + L.off, (int)L.cnt, L.step, h->sn.p,
-                              h->store.p, w, v, rh, DiagInv{h->invbase.p, h->dinvbuf.p});
+                              h->store.p, w, v, rh);
     case K_BWDU:
       return launch_bwd_u12(st, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->sn.p, h->rows.p, h->store.p, w, v,
                             rh);
@@ -2679,7 +2549,7 @@ static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, d
     case K_SWEEPB:
       return launch_tri_sweep(st, L.kind == K_SWEEPB, L.nwg, h->ftiles.p + L.off, (int)L.cnt, h->stick.p + L.aux2,
                               h->ssync.p + L.aux, h->sxh.p + L.aux * 64 * kMultiRhs, h->sstatus.p, h->sn.p, h->store.p,
-                              w, v, rh, h->sweep_spin, DiagInv{h->invbase.p, h->dinvbuf.p});
+                              w, v, rh, h->sweep_spin);
     case K_BWDU12C:
       return launch_bwd_u12_cols(st, h->sn.p, L.node, h->hsn[L.node].ns, L.aux, L.aux2, (int)L.cnt, h->rows.p,
                                  h->store.p, w, h->vbuf.p);
