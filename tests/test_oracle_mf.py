@@ -164,7 +164,7 @@ def test_repivot_restatement():
 
 
 def fold_complex(L, U, p, q, n):
-    """Python restatement of smlu.cpp: export_complex -- the complex n x n factors from the scalar
+    """Python restatement of complex.cpp: export_complex -- the complex n x n factors from the scalar
     LU of the real-equivalent K under pair-preserving pivots, pairs kept in either order."""
     sw = p[0::2] > p[1::2]
     pc, qc = np.minimum(p[0::2], p[1::2]) // 2, q[0::2] // 2
