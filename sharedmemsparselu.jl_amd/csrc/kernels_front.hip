@@ -245,7 +245,7 @@ __global__ __launch_bounds__(64 * NW) void k_front_small(const int32_t* __restri
   }
   // factorization
   int flag = 0, err = -1;   // wave 0, lane 0
-  double gmax = 0.0;
+  double gmax = 0.0, glane = 0.0;   // growth: lane 0 of wave 0 (full searches), per lane of wave 0 (fast ones)
   __shared__ int s_second;   // pair rule: position of the current pair's other row
   for (int k = 0; k < ns; ++k) {
     if (s.cpair && wv == 0) {   // ComplexF64 real-equivalent: pair-preserving pivots (mf.c rule)
@@ -294,13 +294,31 @@ __global__ __launch_bounds__(64 * NW) void k_front_small(const int32_t* __restri
     } else if (wv == 0) {
       double am = -1.0, amo = 0.0;
       int ai = k;
+      bool beats = false, weak = false;
+      const double akk = lds[k * ld + k], pk = fabs(akk);
       for (int i = k + lane; i < M; i += 64) {
         double v = fabs(lds[k * ld + i]);
         if (i < ns) {
           if (v > am) { am = v; ai = i; }
+          beats |= diag_tol * v > pk;
         } else if (v > amo) {
           amo = v;
         }
+        weak |= piv_tol * v > pk;
+      }
+      // the diagonal stays unless a candidate beats it by 1/diag_tol (choose_pivot): one ballot
+      // decides, and the weak-pivot test and the growth need no reduction either -- a product
+      // or quotient by one positive number is monotone, so the per-lane maxima give the values
+      // of the full reduction exactly (growth: each lane's max(|a_ik|)/|a_kk|, reduced at the end)
+      if (akk != 0.0 && __ballot(beats) == 0ull) {
+        const double ml = fmax(am, amo);
+        if (ml > 0.0) glane = fmax(glane, ml / pk);
+        const bool anyweak = __ballot(weak) != 0ull;
+        if (lane == 0) {
+          if (anyweak) flag |= 2;
+          s_piv = k;
+        }
+        goto searched;
       }
       am = wave_max_idx(am, ai);
       amo = wave_max(amo);
@@ -317,6 +335,7 @@ __global__ __launch_bounds__(64 * NW) void k_front_small(const int32_t* __restri
         s_piv = piv;
       }
     }
+  searched:
     __syncthreads();
     const int piv = s_piv;
     if (piv != k) {
@@ -348,6 +367,7 @@ __global__ __launch_bounds__(64 * NW) void k_front_small(const int32_t* __restri
     for (int i = lane; i < M; i += 64) *fel(f, i, j) = lds[j * ld + i];
   }
   for (int i = tid; i < ns; i += NT) rowperm[s.first + i] = s_perm[i];
+  if (wv == 0) gmax = fmax(gmax, wave_max(glane));
   if (tid == 0) {
     if (flag) publish_info(info + sid, flag, err);
     if (gmax > 0.0) atomic_max_pos(&growth[0], gmax);
