@@ -348,6 +348,8 @@ int smlu_dev_copy(smlu_handle* h, int which, int64_t off, int64_t cnt, double* o
  *   SMLU_NO_GRAPH      eager launches instead of captured hipGraphs
  *   SMLU_DEBUG_SYNC    synchronise after every launch (localises a failing kernel)
  *   SMLU_NO_REPIVOT    no re-pivoting refactor after weak diagonal-tile pivots (tests)
+ * and, not a library knob: OMP_NUM_THREADS, when set, caps the host threads of the analysis
+ * (otherwise the hardware threads, at most 32; the plan does not depend on the thread count).
  */
 
 /* Library version string. */

@@ -37,9 +37,14 @@ int64_t Plan::local_index(int64_t s, int64_t g) const {
 
 namespace {
 
-// Host threads for the analysis (bounded: the 256^3 plan is built on every rank of a node).
+// Host threads for the analysis: the hardware threads, at most 32, and at most OMP_NUM_THREADS
+// when that is set (the 256^3 plan is built on every rank of a node, each rank with its share).
 int plan_threads() {
-  static const int t = (int)std::min(32u, std::max(1u, std::thread::hardware_concurrency()));
+  static const int t = [] {
+    int v = (int)std::min(32u, std::max(1u, std::thread::hardware_concurrency()));
+    const int cap = tune().host_threads;
+    return cap > 0 ? std::min(v, cap) : v;
+  }();
   return t;
 }
 

@@ -29,6 +29,7 @@ struct Tune {
   bool no_graph = false;      // SMLU_NO_GRAPH: eager launches, no captured graphs
   bool debug_sync = false;    // SMLU_DEBUG_SYNC: synchronise after every launch (error localisation)
   bool no_repivot = false;    // SMLU_NO_REPIVOT: no re-pivoting refactor after weak tile pivots
+  int host_threads = 0;       // OMP_NUM_THREADS: cap on the analysis threads (0 = not set)
 };
 Tune tune();
 

@@ -19,6 +19,7 @@ Tune tune() {
     v.no_graph = std::getenv("SMLU_NO_GRAPH") != nullptr;
     v.debug_sync = std::getenv("SMLU_DEBUG_SYNC") != nullptr;
     v.no_repivot = std::getenv("SMLU_NO_REPIVOT") != nullptr;
+    if (const char* e = std::getenv("OMP_NUM_THREADS")) v.host_threads = std::atoi(e);
   }
   return v;
 }

@@ -151,3 +151,38 @@ def test_bench_ordering_compare():
         for o in ("nd", "amd"):
             assert row[o]["nnzLU"] > 0 and row[o]["upd"] > 0
     assert c3["nd"]["upd"] < c3["amd"]["upd"]
+
+
+_PLAN_HASH = """
+import hashlib, sys
+sys.path.insert(0, %r)
+import numpy as np
+import smlu
+from smlu import matrices as mats
+P = smlu.Plan(mats.poisson3d(64))
+first, parent, rowptr, rows, p0 = P.fronts()
+h = hashlib.sha256()
+for a in (first, parent, rowptr, rows, p0):
+    h.update(np.ascontiguousarray(a, np.int64).tobytes())
+print(h.hexdigest())
+"""
+
+
+def test_plan_independent_of_thread_count():
+    """The threaded analysis (nested-dissection halves on their own threads above 200k vertices,
+    row structures by tree height, the A map's parallel sort) gives the same plan on 1 thread as
+    on the default count: 64^3 forks at the top bisection."""
+    import subprocess
+    import sys
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "sharedmemsparselu.jl_amd")
+    out = []
+    for threads in ("1", None):
+        env = dict(os.environ)
+        env.pop("OMP_NUM_THREADS", None)
+        if threads:
+            env["OMP_NUM_THREADS"] = threads
+        r = subprocess.run([sys.executable, "-c", _PLAN_HASH % pkg], env=env, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr
+        out.append(r.stdout.strip())
+    assert out[0] == out[1]
