@@ -195,6 +195,7 @@ __device__ __forceinline__ int choose_pivot(double akk, double amax, int arg, in
 // local column << 16 | local row).  The growth maximum is reduced over the front's columns and
 // reported once.
 // ------------------------------------------------------------------------------------
+typedef double f64x4 __attribute__((ext_vector_type(4)));
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void k_front_small(const int32_t* __restrict__ list,
                                                          const SNode* __restrict__ sn,
@@ -354,11 +355,69 @@ __global__ __launch_bounds__(64 * NW) void k_front_small(const int32_t* __restri
     const double pinv = recip(lds[k * ld + k]);
     for (int i = k + 1 + tid; i < M; i += NT) lds[k * ld + i] = lds[k * ld + i] * pinv;
     __syncthreads();
-    for (int j = k + 1 + wv; j < M; j += NW) {
-      const double u = lds[j * ld + k];
-      if (u != 0.0)
-        for (int i = k + 1 + lane; i < M; i += 64)
-          lds[j * ld + i] = fma(-lds[k * ld + i], u, lds[j * ld + i]);
+    // Schur update of the pivot block and the U12 rows only; F22 (rows and columns >= ns) takes
+    // all ns rank-1 updates at once after the loop, on the matrix cores.  Wave jobs: U12 column
+    // groups (lanes over 64 columns, rows (k, ns) in a loop) and the pivot columns (k, ns) (lanes
+    // over the rows (k, M)), dealt round-robin.  Per element the same fma as the rank-1 pass over
+    // the whole front, skipped when u == 0.
+    const int nb = (M - ns + 63) / 64, nl = ns - k - 1;
+    for (int q = wv; q < nb + nl; q += NW) {
+      if (q < nb) {
+        const int j = ns + 64 * q + lane;
+        if (j < M) {
+          double* cj = lds + j * ld;
+          const double u = cj[k];
+          if (u != 0.0) {
+            int i = k + 1;
+            for (; i + 4 <= ns; i += 4) {
+              const double a0 = cj[i], a1 = cj[i + 1], a2 = cj[i + 2], a3 = cj[i + 3];
+              const double l0 = lds[k * ld + i], l1 = lds[k * ld + i + 1], l2 = lds[k * ld + i + 2],
+                           l3 = lds[k * ld + i + 3];
+              cj[i] = fma(-l0, u, a0);
+              cj[i + 1] = fma(-l1, u, a1);
+              cj[i + 2] = fma(-l2, u, a2);
+              cj[i + 3] = fma(-l3, u, a3);
+            }
+            for (; i < ns; ++i) cj[i] = fma(-lds[k * ld + i], u, cj[i]);
+          }
+        }
+      } else {
+        const int j = k + 1 + (q - nb);
+        const double u = lds[j * ld + k];
+        if (u != 0.0)
+          for (int i = k + 1 + lane; i < M; i += 64)
+            lds[j * ld + i] = fma(-lds[k * ld + i], u, lds[j * ld + i]);
+      }
+    }
+    __syncthreads();
+  }
+  // F22 -= L21 * U12 with k = ns on the fp64 matrix cores, 16 x 16 output blocks dealt to the
+  // waves: C starts as the block's F22 values, A = -L21 (rows ns.., k-quads of the pivot
+  // columns), B = U12; per element the ns products are fused in ascending k, as the rank-1 pass
+  // did (which skipped u == 0: the two differ only in the sign of an exactly zero entry).
+  if (M > ns) {
+    const int nu = M - ns, nt = (nu + 15) / 16;
+    const int li = lane & 15, lg = lane >> 4;
+    for (int t = wv; t < nt * nt; t += NW) {
+      const int r0 = ns + 16 * (t % nt), c0 = ns + 16 * (t / nt);
+      const int ra = r0 + li, cb = c0 + li;
+      f64x4 acc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = r0 + lg + 4 * r;
+        acc[r] = (i < M && cb < M) ? lds[cb * ld + i] : 0.0;
+      }
+      for (int kq = 0; kq < ns; kq += 4) {
+        const int kk = kq + lg;
+        const double fa = (kk < ns && ra < M) ? -lds[kk * ld + ra] : 0.0;
+        const double fb = (kk < ns && cb < M) ? lds[cb * ld + kk] : 0.0;
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = r0 + lg + 4 * r;
+        if (i < M && cb < M) lds[cb * ld + i] = acc[r];
+      }
     }
     __syncthreads();
   }
