@@ -232,15 +232,35 @@ __global__ __launch_bounds__(64 * NW) void k_front_small(const int32_t* __restri
     lds[(en.y >> 16) * ld + (en.y & 0xffff)] = Rs[arow[en.x]] * a[en.x];
   }
   __syncthreads();
+  // children's F22 blocks, added in child order (a barrier between children): the lane's two rows
+  // of the child's row map are read once per child, and a wave's columns go eight at a time --
+  // their column indices and values all in flight before the first LDS addition
   for (int q = s.chbeg; q < s.chend; ++q) {
     const SNode c = sn[chlist[q]];
-    const int nuc = c.nu;
+    const int nuc = c.nu;   // <= M <= 128: two rows per lane
     if (nuc == 0) continue;
     const int32_t* rm = relmap + c.rowptr;
     const gdbl* src = gbl(scratch + c.Foff);
-    for (int jc = wv; jc < nuc; jc += NW) {
-      double* col = lds + rm[jc] * ld;
-      for (int i = lane; i < nuc; i += 64) col[rm[i]] += src[(int64_t)jc * nuc + i];
+    const bool h0 = lane < nuc, h1 = lane + 64 < nuc;
+    const int ri0 = h0 ? rm[lane] : 0, ri1 = h1 ? rm[lane + 64] : 0;
+    for (int jc0 = wv; jc0 < nuc; jc0 += 8 * NW) {
+      int cj[8];
+      double v0[8], v1[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int jc = jc0 + u * NW;
+        const bool on = jc < nuc;
+        cj[u] = on ? rm[jc] : 0;
+        v0[u] = (on && h0) ? src[(int64_t)jc * nuc + lane] : 0.0;
+        v1[u] = (on && h1) ? src[(int64_t)jc * nuc + lane + 64] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (jc0 + u * NW >= nuc) break;
+        double* col = lds + cj[u] * ld;
+        if (h0) col[ri0] += v0[u];
+        if (h1) col[ri1] += v1[u];
+      }
     }
     __syncthreads();
   }
