@@ -862,6 +862,22 @@ __global__ __launch_bounds__(64) void k_panel_wave(const int32_t* __restrict__ l
 }
 
 typedef double v4d __attribute__((ext_vector_type(4)));
+// Dev instrumentation (-DSMLU_PANEL_TRACE, tools/panel_trace.py): workgroup 0 of every fused panel
+// launch records the 100 MHz clock at its phase boundaries.  The product build has no hook.
+#ifdef SMLU_PANEL_TRACE
+struct PanelTrace {
+  long long* buf;
+  unsigned long long* ctr;
+  long long n;
+};
+__device__ PanelTrace g_panel_trace;
+__device__ __forceinline__ void pmark(long long idx, int k) {
+  if (idx >= 0 && threadIdx.x == 0) g_panel_trace.buf[idx * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
+}
+#define PMARK(k) pmark(s_pidx, k)
+#else
+#define PMARK(k) ((void)0)
+#endif
 // Tail of the fused panel (k_panel_blk<NWV, true>): the finished tile (x, row positions pos)
 // goes to LDS as k_tri_inv reads it from HBM ([col][row], ld 65, identity outside w x w), wave v
 // forms columns 4v..4v+3 of NL = I - L^-1 and of NU = I - U^-1 with k_tri_inv's arithmetic, and
@@ -870,8 +886,10 @@ typedef double v4d __attribute__((ext_vector_type(4)));
 template <int NWV, int CW, bool INV>
 __device__ __forceinline__ void panel_fused_tail(const double (&x)[CW], int pos, bool has, int w, int kb,
                                                  int64_t M, const FrontPtrs& f, const SNode& s, int64_t slot,
-                                                 double* __restrict__ tinv, int ob, int lane, int wv) {
-  static_assert(NWV == 16 && CW == 4, "fused panel: 16 waves, 4 columns each");
+                                                 double* __restrict__ tinv, int ob, int lane, int wv,
+                                                 long long s_pidx) {
+  (void)s_pidx;
+  static_assert((NWV == 16 && CW == 4) || (NWV == 8 && CW == 8), "fused panel: 16 x 4 or 8 x 8 columns");
   __shared__ double sD[INV ? 64 * 65 : 1];
   const int tid = threadIdx.x;
   if (INV) {
@@ -891,7 +909,7 @@ __device__ __forceinline__ void panel_fused_tail(const double (&x)[CW], int pos,
   const int ostart = (kb / ob) * ob, oend = min((int)f.ns, ostart + ob);
   const int nother = oend - ostart - w;
   const bool moved = has && pos != lane;
-  constexpr int kMaxCols = 20;   // (OB - 64) / NWV columns per wave for OB <= 384
+  constexpr int kMaxCols = 320 / NWV;   // (OB - 64) / NWV columns per wave for OB <= 384
   double mv[kMaxCols];
 #pragma unroll
   for (int q = 0; q < kMaxCols; ++q) {
@@ -910,6 +928,7 @@ __device__ __forceinline__ void panel_fused_tail(const double (&x)[CW], int pos,
       f.L[(int64_t)col * M + kb + pos] = mv[q];
     }
   }
+  PMARK(3);
   if (!INV) return;
   // tile inverses X_L = L^-1, X_U = U^-1 by 16 x 16 blocks: the diagonal blocks by substitution
   // (lane = one column of one block), the off-diagonal blocks by the block recurrences
@@ -944,6 +963,7 @@ __device__ __forceinline__ void panel_fused_tail(const double (&x)[CW], int pos,
     }
   }
   __syncthreads();
+  PMARK(4);
   // one off-diagonal block (bi, bj) at distance d: T = sum_k F_{bi,k} X_{k,bj}, X = -X_{bi,bi} T.
   // MFMA 16x16x4: A fragment lane (row li, k lg), B fragment (k lg, col li); D lane holds
   // (row lg + 4r, col li), which is exactly the B fragment of k-quad r for the second product.
@@ -969,9 +989,11 @@ __device__ __forceinline__ void panel_fused_tail(const double (&x)[CW], int pos,
   for (int d = 1; d < 4; ++d) {
     const int nb = 4 - d;   // blocks at distance d: L (j + d, j), U (j, j + d), j < nb
     if (wv < nb) offdiag(XL, XL, wv + d, wv, wv, wv + d - 1);
-    else if (wv >= 8 && wv - 8 < nb) offdiag(XU, XU, wv - 8, wv - 8 + d, wv - 8 + 1, wv - 8 + d);
+    else if (wv >= NWV / 2 && wv - NWV / 2 < nb)
+      offdiag(XU, XU, wv - NWV / 2, wv - NWV / 2 + d, wv - NWV / 2 + 1, wv - NWV / 2 + d);
     __syncthreads();
   }
+  PMARK(5);
   double* out = tinv + slot * 8192;
   for (int idx = tid; idx < 4096; idx += 64 * NWV) {
     const int i = idx & 63, j = idx >> 6;
@@ -1009,6 +1031,17 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
   __shared__ double s_l[2][CW][64];
   __shared__ int s_p[2][CW];
   __shared__ int s_flag[NWV], s_err[NWV];
+  __shared__ double s_gmax[NWV];
+#ifdef SMLU_PANEL_TRACE
+  __shared__ long long s_pidx_sh;
+  if (threadIdx.x == 0)
+    s_pidx_sh = (blockIdx.x == 0 && g_panel_trace.buf) ? (long long)atomicAdd(g_panel_trace.ctr, 1ull) : -1;
+  __syncthreads();
+  const long long s_pidx = s_pidx_sh < (g_panel_trace.n) ? s_pidx_sh : -1;
+#else
+  const long long s_pidx = -1;
+#endif
+  PMARK(0);
   const int sid = list[2 * blockIdx.x];
   const SNode s = sn[sid];
   FrontPtrs f = front_ptrs(s, store, scratch);
@@ -1039,6 +1072,7 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
       else if (lane == ppos) who = q;
     }
   };
+  PMARK(1);
   for (int blk = 0; blk < NWV; ++blk) {
     const int k0 = blk * CW;
     if (k0 >= w) break;
@@ -1118,15 +1152,23 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
       if (c < w) P[(int64_t)c * M + pos] = x[j];
     }
   }
+  PMARK(2);
   lmax = wave_max(lmax);
   if (lane == 0) {
-    if (lmax > 0.0) atomic_max_pos(&growth[0], lmax);
+    s_gmax[wv] = lmax;
     s_flag[wv] = flag;
     s_err[wv] = err;
   }
   if constexpr (FUSED > 0)
-    panel_fused_tail<NWV, CW, FUSED == 2>(x, pos, has, w, kb, M, f, s, list[2 * blockIdx.x + 1], tinv, ob, lane, wv);
+    panel_fused_tail<NWV, CW, FUSED == 2>(x, pos, has, w, kb, M, f, s, list[2 * blockIdx.x + 1], tinv, ob, lane, wv,
+                                          s_pidx);
   __syncthreads();
+  PMARK(6);
+  if (wv == 1 && lane == 0) {   // the growth maximum (a read, maybe an atomic) beside wave 0's bookkeeping
+    double g = 0.0;
+    for (int v = 0; v < NWV; ++v) g = fmax(g, s_gmax[v]);
+    if (g > 0.0) atomic_max_pos(&growth[0], g);
+  }
   if (wv != 0) return;
   int32_t* rp = rowperm + s.first + kb;
   const int old = has ? rp[lane] : 0;
@@ -1148,7 +1190,33 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
     }
     if (fl) publish_info(info + sid, fl, er);
   }
+  PMARK(7);
 }
+
+#ifdef SMLU_PANEL_TRACE
+// Dev hook for tools/panel_trace.py: n > 0 arms the trace for the next n fused panel launches;
+// n == 0 copies the records (16 clock values per launch) out and disarms it.
+extern "C" int smlu_dev_panel_trace(long long n, long long* out) {
+  static long long* buf = nullptr;
+  static unsigned long long* ctr = nullptr;
+  static long long cap = 0;
+  using namespace smlu;
+  PanelTrace t{nullptr, nullptr, 0};
+  if (n > 0) {
+    if (buf) (void)hipFree(buf);
+    if (!ctr && hipMalloc(&ctr, sizeof(unsigned long long)) != hipSuccess) return -1;
+    if (hipMalloc(&buf, sizeof(long long) * 16 * n) != hipSuccess) return -1;
+    (void)hipMemset(buf, 0, sizeof(long long) * 16 * n);
+    (void)hipMemset(ctr, 0, sizeof(unsigned long long));
+    cap = n;
+    t = PanelTrace{buf, ctr, n};
+  } else if (buf) {
+    (void)hipDeviceSynchronize();
+    if (out && hipMemcpy(out, buf, sizeof(long long) * 16 * cap, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  }
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_panel_trace), &t, sizeof t) == hipSuccess ? 0 : -1;
+}
+#endif
 
 
 // Row swaps (LAPACK laswp) of the panels of a SwapTask on its column set; one workgroup per 64

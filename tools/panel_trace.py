@@ -1,0 +1,56 @@
+"""Dev: phase timing of the fused 64-column panel (k_panel_blk<16, 2>) at 128^3 from the kernel's own
+clock marks (smlu_dev_panel_trace; workgroup 0 of every launch of one refactor): start, blocks
+begin (tile loaded), blocks done, tail start, row interchanges done, diagonal-block inverses done,
+off-diagonal blocks done, tail end, end.  Prints the median interval per phase.
+
+    (library built with -DSMLU_PANEL_TRACE) SMLU_LIB=... python tools/panel_trace.py [--side 128]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "sharedmemsparselu.jl_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--side", type=int, default=128)
+    args = ap.parse_args()
+    import torch
+    import smlu
+    import smlu._lib as C
+    from smlu import matrices as mats
+    A = mats.poisson3d(args.side)
+    F = smlu.ParallelSparseLU(A, profile=False)
+    torch.cuda.synchronize()
+    lib = C.lib()
+    fn = lib.smlu_dev_panel_trace
+    fn.argtypes = [ctypes.c_longlong, ctypes.c_void_p]
+    fn.restype = ctypes.c_int
+    n = 4096
+    assert fn(n, None) == 0
+    smlu.lu_(F, A)
+    torch.cuda.synchronize()
+    out = np.zeros(n * 16, np.int64)
+    assert fn(0, out.ctypes.data) == 0
+    t = out.reshape(n, 16)[:, :8].astype(np.float64) * 10e-3   # us
+    t = t[t[:, 0] > 0]
+    print(f"launches traced: {len(t)}")
+    names = ["start->blocks", "blocks", "blocks->tail", "row swaps", "diag inverses", "offdiag MFMA",
+             "tail->end(6)", "6->7 (rowperm, swaps, info)"]
+    d = np.diff(t, axis=1)
+    for k in range(7):
+        col = d[:, k]
+        col = col[np.isfinite(col) & (col >= 0)]
+        if len(col):
+            print(f"  {names[k]:30s} median {np.median(col):7.2f} us  p90 {np.percentile(col, 90):7.2f}")
+    tot = t[:, 7] - t[:, 0]
+    print(f"  total (mark 0 -> 7)            median {np.median(tot):7.2f} us")
+    F.close()
+
+
+if __name__ == "__main__":
+    main()
