@@ -51,7 +51,8 @@ __global__ void k_factor_reset(int64_t nnodes, int32_t* __restrict__ info, doubl
 // its slot), then each contributing child's F22 column added in child order -- and written
 // once, coalesced.  No memset of the fronts and no read-modify-write of the parent: every
 // front element is written exactly once per factorization, every child F22 element and its
-// row map read once.  The order of the additions per element is that of a zeroed front with
+// row map read from HBM once (a chunk loads a child's row-map window and its values together;
+// values whose rows fall in the next chunk are read again from L2).  The order of the additions per element is that of a zeroed front with
 // A stored and the children added in child order (deterministic, no atomics).
 // Lane q < 64 keeps the running position of contribution q in its child column (row maps are
 // ascending, chunks are visited in ascending row order); contributions beyond the 64th find
@@ -138,15 +139,16 @@ __global__ __launch_bounds__(256) void k_assemble(int64_t ntasks, const XCol* __
       }
       const double* src = srco >= 0 ? scratch + srco : store + (-1 - srco);
       const int32_t* rm = relmap + rmo;
+      // row map and values in one round trip: the values are loaded for the whole window, the
+      // ones whose rows fall beyond this chunk are read again by the next (from L2)
       int32_t rv[4];
+      double sv[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int64_t i = pos + lane + 64 * k;
         rv[k] = i < nuc ? rm[i] : 0x7fffffff;
+        sv[k] = i < nuc ? src[i] : 0.0;
       }
-      double sv[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) sv[k] = rv[k] < r1 ? src[pos + lane + 64 * k] : 0.0;
       int cn = 0;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
