@@ -339,7 +339,8 @@ int smlu_dev_copy(smlu_handle* h, int which, int64_t off, int64_t cnt, double* o
  * environment changes its numerics or schedule) ---------------------------------------------
  *   SMLU_OB=w          outer block width of the blocked fronts (multiple of 64; default 384)
  *   SMLU_T128MIN=t     128x128 MFMA tiles for GEMM launches with >= t output tiles (default 512)
- *   SMLU_SMALLK=0      no one-shot k <= 64 GEMM tile (tests: forces the 64x64 VALU tile)
+ *   SMLU_SMALLK=0      no one-shot k <= 64 GEMM tile (tests: forces the 64x64 VALU tile, and the
+ *                      GEMM-form TRSM onto the 128 tile when SMLU_T128MIN allows it)
  *   SMLU_FULLPIV_NS=k  largest front with full-candidate pivoting (tests; default: 512, or 128
  *                      for diagonally dominant values)
  *   SMLU_SWEEP_SPIN=s  polls before a sync-free solve wait gives up and the solve is re-run on the

@@ -1,11 +1,12 @@
 """Every kernel variant of the numeric refactor against the oracle, and the error paths.
 
-* GEMM tile variants.  A launch normally takes the fp64 MFMA 128x128 tile (`k_gemm128_mfma2`,
-  the v2 tile) only when it has >= 512 output tiles, which the oracle-sized cases never reach.
+* GEMM tile variants.  A launch normally takes the fp64 MFMA 128x128 tile (`k_gemm128_mfma3`,
+  the v3 tile) only when it has >= 512 output tiles, which the oracle-sized cases never reach.
   The schedule knobs force each variant on oracle-sized fronts, so the dominant kernel of the
-  128^3 refactor (`k_gemm128_mfma2<false>`) and its TRSM form (`<true>`, growth epilogue) are
-  compared with the oracle entry by entry:
-    mfma128  SMLU_T128MIN=1                   every GEMM launch on k_gemm128_mfma2
+  128^3 refactor (`k_gemm128_mfma3<false, *>`) and its TRSM form (`<true, *>`, growth epilogue)
+  are compared with the oracle entry by entry:
+    mfma128  SMLU_T128MIN=1, SMLU_SMALLK=0    every GEMM launch on k_gemm128_mfma3, the GEMM-form
+                                              TRSM included (by default it runs on k_gemm_k64)
     valu64   SMLU_T128MIN=2^60, SMLU_SMALLK=0 every GEMM launch on the VALU 64x64 tile k_gemm
     valu128  SMLU_T128MIN=1, use_mfma=0       the VALU 128x128 tile k_gemm128
     default  as shipped (k_gemm_k64 for k <= 64 launches, fused panels with tile inverses,
@@ -30,7 +31,7 @@ pytestmark = pytest.mark.gpu
 
 VARIANTS = {
     "default": ({}, {}),
-    "mfma128": ({"SMLU_T128MIN": "1"}, {}),
+    "mfma128": ({"SMLU_T128MIN": "1", "SMLU_SMALLK": "0"}, {}),
     "valu64": ({"SMLU_T128MIN": str(1 << 60), "SMLU_SMALLK": "0"}, {}),
     "valu128": ({"SMLU_T128MIN": "1"}, {"use_mfma": False}),
 }
@@ -68,7 +69,7 @@ def test_poisson3d_nd_gemm_variants(gpu, monkeypatch, N, variant):
     check_variant_ran(F, variant)
     assert F.stat("fronts_mode2") > 0
     if variant == "mfma128":
-        assert F.stat("launches_mfma128_trsm") > 0   # k_gemm128_mfma<true>
+        assert F.stat("launches_mfma128_trsm") > 0   # k_gemm128_mfma3<true, *>
     factor_parity(A, F)
     assert np.array_equal(F.p, F.q)
     b = np.random.default_rng(N).random(A.shape[0])

@@ -2,14 +2,20 @@
 # Dev A/B of library variants (via gpurun from the repo root): the 128^3 bench with each given
 # .so (SMLU_LIB), one line per variant with the per-kind kernel times, then optionally a pytest
 # selection against the LAST variant.
-# Usage: tools/ab_libs.sh "var/base.so var/x.so" [pytest -k expression]
+# Usage: tools/ab_libs.sh "var/base.so var/x.so var/y.so@KNOB=1" [pytest -k expression]
+# (an entry lib@NAME=VALUE runs that variant with the environment variable set)
 set -o pipefail
 mkdir -p gpurun_out
 LIBS=$1
 K=${2:-}
-for L in $LIBS; do
-  T=$(basename $L .so)
-  SMLU_LIB=$PWD/$L timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu --no-configs \
+n=0
+for E in $LIBS; do
+  n=$((n + 1))
+  L=${E%%@*}
+  EV=""
+  [ "$E" != "$L" ] && EV=${E#*@}
+  T=$(basename $L .so)_$n
+  env $EV SMLU_LIB=$PWD/$L timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu --no-configs \
     > gpurun_out/ab_$T.json 2> gpurun_out/ab_$T.log || { echo "$T FAILED"; tail -20 gpurun_out/ab_$T.log; exit 1; }
   python - <<PY
 import json; r=json.load(open("gpurun_out/ab_$T.json"))
