@@ -225,6 +225,84 @@ __device__ __forceinline__ double k64_tile(const gdbl* gA, int lda, const gdbl* 
   return gmax;
 }
 
+// The same one-shot tile on the fp64 matrix cores: each wave a 32 x 32 quadrant of 2 x 2
+// v_mfma_f64_16x16x4 blocks over the staged A / -B images (lane l of block (i, j) holds
+// C[16 i + (l & 15)][16 j + (l >> 4) + 4 r]).  Per element the MFMA's chain is one fused
+// multiply-add per k in ascending order, the zero-filled k >= K terms exact no-ops: bitwise the
+// VALU tile's result.
+typedef double v4d __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ double k64_tile_mfma(const gdbl* gA, int lda, const gdbl* gB, int ldb, gdbl* gC, int ldc,
+                                                int m, int n, int K, int m0, int n0,
+                                                double (&As)[64][GBM + 2], double (&Bs)[64][GBN + 2]) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = (wv & 1) * 32, wc = (wv >> 1) * 32;
+  const int li = lane & 15, lk = lane >> 4;
+  v4d acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = m0 + wr + 16 * i + li;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = n0 + wc + 16 * j + lk + 4 * r;
+        acc[i][j][r] = (col < n && row < m) ? gC[(int64_t)col * ldc + row] : 0.0;
+      }
+  }
+  // A: row = tid & 63, k = (tid >> 6) + 4r;  B: k = tid & 63, col = (tid >> 6) + 4r
+  const int ar = tid & 63, ak = tid >> 6;
+  double ra[16], rb[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int kk = ak + 4 * r, row = m0 + ar;
+    ra[r] = (row < m && kk < K) ? gA[(int64_t)kk * lda + row] : 0.0;
+    const int col = n0 + ak + 4 * r;
+    rb[r] = (col < n && ar < K) ? gB[(int64_t)col * ldb + ar] : 0.0;
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    As[ak + 4 * r][ar] = ra[r];
+    Bs[ar][ak + 4 * r] = -rb[r];
+  }
+  __syncthreads();
+  auto kquad = [&](int kq) {
+    const int k = 4 * kq + lk;
+    double fa[2], fb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) fa[i] = As[k][wr + 16 * i + li];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) fb[j] = Bs[k][wc + 16 * j + li];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[j], fa[i], acc[i][j], 0, 0, 0);
+  };
+  if (K == 64) {   // full panels (w = 64): straight-line
+#pragma unroll
+    for (int kq = 0; kq < 16; ++kq) kquad(kq);
+  } else {
+    const int nkq = (K + 3) >> 2;
+    for (int kq = 0; kq < nkq; ++kq) kquad(kq);
+  }
+  double gmax = 0.0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = m0 + wr + 16 * i + li;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = n0 + wc + 16 * j + lk + 4 * r;
+        if (col < n && row < m) {
+          gC[(int64_t)col * ldc + row] = acc[i][j][r];
+          gmax = fmax(gmax, fabs(acc[i][j][r]));
+        }
+      }
+  }
+  return gmax;
+}
+
 template <bool TRSM>
 __global__ __launch_bounds__(256) void k_gemm_k64(const GemmTask* __restrict__ tasks, int ntask, GrowthArgs ga) {
   __shared__ double As[64][GBM + 2];   // [k][row]
@@ -233,8 +311,8 @@ __global__ __launch_bounds__(256) void k_gemm_k64(const GemmTask* __restrict__ t
   const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
   int tm, tn;
   tile_rc<GBM>(t, b - t.tile0, tm, tn);
-  const double gmax = k64_tile(gbl(t.A), t.lda, gbl(t.B), t.ldb, gbl(t.C), t.ldc, t.m, t.n, t.k, tm * GBM,
-                               tn * GBN, As, Bs);
+  const double gmax = k64_tile_mfma(gbl(t.A), t.lda, gbl(t.B), t.ldb, gbl(t.C), t.ldc, t.m, t.n, t.k, tm * GBM,
+                                    tn * GBN, As, Bs);
   if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
 }
 
@@ -364,7 +442,6 @@ __global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__
 // along C's rows (column-major C stays coalesced): lane l of block (bi,bj) holds
 // C[row = 16 bi + (l & 15)][col = 16 bj + (l >> 4) + 4 r], r = 0..3.
 // ------------------------------------------------------------------------------------
-typedef double v4d __attribute__((ext_vector_type(4)));
 // Guard-free operand and C traffic on interior tiles (m, n in range), K guards only in the
 // last, partial slice (FULL = false: every access guarded).  +1-4 % over the guarded form
 // (k = 384 trailing shapes 48.4 -> 50.1 TFLOP/s, tools/gemm_bench).

@@ -88,16 +88,21 @@ def test_poisson3d_32_nd_oracle(gpu, monkeypatch, variant):
 
 
 def test_mfma_and_valu_tiles_bitwise(gpu, monkeypatch):
-    # the MFMA tile accumulates each C element in the same k order as the VALU 64 tile, one
-    # rounding per multiply-add: the factors are bitwise identical.  (use_mfma=0 also swaps the
+    # the MFMA tiles (128 x 128 and the one-shot k <= 64 tile) accumulate each C element in the
+    # same k order as the VALU 64 tile, one rounding per multiply-add: the factors are bitwise
+    # identical.  (use_mfma=0 also swaps the
     # GEMM-form triangular solves for k_step_trsm, so valu128 agrees to rounding only.)
     A = mats.poisson3d(20)
     Fm = make(A, "mfma128", monkeypatch)
     Fv = make(A, "valu64", monkeypatch)
     F2 = make(A, "valu128", monkeypatch)
+    Fd = make(A, "default", monkeypatch)   # k <= 64 launches on the one-shot MFMA tile
+    assert Fd.stat("launches_k64") > 0
     assert np.array_equal(Fv.L.indices, Fm.L.indices)
     assert np.array_equal(Fv.L.data, Fm.L.data)
     assert np.array_equal(Fv.U.data, Fm.U.data)
+    assert np.array_equal(Fv.L.data, Fd.L.data)
+    assert np.array_equal(Fv.U.data, Fd.U.data)
     assert abs(F2.L - Fm.L).max() <= 1e-13
     assert abs(F2.U - Fm.U).max() <= 1e-13 * abs(Fm.U).max()
 
