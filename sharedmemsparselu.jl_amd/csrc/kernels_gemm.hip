@@ -166,70 +166,12 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
 // One 64 x 64 output tile [m0, m0+64) x [n0, n0+64) of an m x n task (k <= 64), by the whole
 // 256-thread workgroup; returns the thread's max |result| (growth epilogue of the TRSM form).
 // All loads (C, A, B) complete before the first store, so B == C (in place) is allowed.
-__device__ __forceinline__ double k64_tile(const gdbl* gA, int lda, const gdbl* gB, int ldb, gdbl* gC, int ldc,
-                                           int m, int n, int K, int m0, int n0,
-                                           double (&As)[64][GBM + 2], double (&Bs)[64][GBN + 2]) {
-  const int tid = threadIdx.x;
-  const int tx = tid & 15, ty = tid >> 4;
-  double acc[4][4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + ty + 16 * j;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = m0 + tx + 16 * i;
-      acc[i][j] = (col < n && row < m) ? gC[(int64_t)col * ldc + row] : 0.0;
-    }
-  }
-  // A: row = tid & 63, k = (tid >> 6) + 4r;  B: k = tid & 63, col = (tid >> 6) + 4r
-  const int ar = tid & 63, ak = tid >> 6;
-  double ra[16], rb[16];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int kk = ak + 4 * r, row = m0 + ar;
-    ra[r] = (row < m && kk < K) ? gA[(int64_t)kk * lda + row] : 0.0;
-    const int col = n0 + ak + 4 * r;
-    rb[r] = (col < n && ar < K) ? gB[(int64_t)col * ldb + ar] : 0.0;
-  }
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    As[ak + 4 * r][ar] = ra[r];
-    Bs[ar][ak + 4 * r] = -rb[r];
-  }
-  __syncthreads();
-#pragma unroll 4
-  for (int kk = 0; kk < K; ++kk) {
-    double a[4], bb[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) a[i] = As[kk][tx + 16 * i];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bb[j] = Bs[kk][ty + 16 * j];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = fma(a[i], bb[j], acc[i][j]);
-  }
-  double gmax = 0.0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int col = n0 + ty + 16 * j;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = m0 + tx + 16 * i;
-      if (col < n && row < m) {
-        gC[(int64_t)col * ldc + row] = acc[i][j];
-        gmax = fmax(gmax, fabs(acc[i][j]));
-      }
-    }
-  }
-  return gmax;
-}
-
-// The same one-shot tile on the fp64 matrix cores: each wave a 32 x 32 quadrant of 2 x 2
+// On the fp64 matrix cores (round 5; the VALU form it replaced took 1.1 ms more in-block update
+// and 1.6 ms more GEMM-form TRSM time per 128^3 refactor): each wave a 32 x 32 quadrant of 2 x 2
 // v_mfma_f64_16x16x4 blocks over the staged A / -B images (lane l of block (i, j) holds
 // C[16 i + (l & 15)][16 j + (l >> 4) + 4 r]).  Per element the MFMA's chain is one fused
 // multiply-add per k in ascending order, the zero-filled k >= K terms exact no-ops: bitwise the
-// VALU tile's result.
+// VALU tiles' result.
 typedef double v4d __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ double k64_tile_mfma(const gdbl* gA, int lda, const gdbl* gB, int ldb, gdbl* gC, int ldc,
                                                 int m, int n, int K, int m0, int n0,
