@@ -159,6 +159,102 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
   if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
 }
 
+// The same 64 x 64 tile on the fp64 matrix cores (tile code 66, the default for k > 64 launches
+// below the 128-tile threshold; SMLU_SMALLK=0 keeps k_gemm): identical staging and slices, each
+// wave a 32 x 32 quadrant of 2 x 2 v_mfma_f64_16x16x4 blocks (lane l of block (i, j) holds
+// C[16 i + (l & 15)][16 j + (l >> 4) + 4 r]); per element one fused multiply-add per k in
+// ascending order, bitwise k_gemm's result.
+typedef double v4d __attribute__((ext_vector_type(4)));
+template <bool TRSM>
+__global__ __launch_bounds__(256) void k_gemm64_mfma(const GemmTask* __restrict__ tasks, int ntask, GrowthArgs ga) {
+  __shared__ double As[2][GBK][GBM + 2];
+  __shared__ double Bs[2][GBK][GBN + 2];
+  const int64_t b = xcd_remap(blockIdx.x, gridDim.x);
+  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
+  const gdbl* gA = gbl(t.A);
+  const gdbl* gB = gbl(t.B);
+  gdbl* gC = gbl(t.C);
+  int tm, tn;
+  tile_rc<GBM>(t, b - t.tile0, tm, tn);
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = (wv & 1) * 32, wc = (wv >> 1) * 32;
+  const int li = lane & 15, lk = lane >> 4;
+  v4d acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = m0 + wr + 16 * i + li;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = n0 + wc + 16 * j + lk + 4 * r;
+        acc[i][j][r] = (col < t.n && row < t.m) ? gC[(int64_t)col * t.ldc + row] : 0.0;
+      }
+  }
+  const int ar = tid & 63, ak = tid >> 6;
+  const int bk = tid & 15, bc = tid >> 4;
+  double ra[4], rb[4];
+  const int K = t.k;
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int kk = ak + 4 * r;
+      const int row = m0 + ar;
+      ra[r] = (row < t.m && k0 + kk < K) ? gA[(int64_t)(k0 + kk) * t.lda + row] : 0.0;
+      const int col = n0 + bc + 16 * r;
+      rb[r] = (col < t.n && k0 + bk < K) ? gB[(int64_t)col * t.ldb + k0 + bk] : 0.0;
+    }
+  };
+  auto sstore = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      As[buf][ak + 4 * r][ar] = ra[r];
+      Bs[buf][bk][bc + 16 * r] = -rb[r];
+    }
+  };
+  const int nk = (K + GBK - 1) / GBK;
+  gload(0);
+  sstore(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) gload((kt + 1) * GBK);
+#pragma unroll
+    for (int kq = 0; kq < GBK / 4; ++kq) {
+      const int k = 4 * kq + lk;
+      double fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = As[cur][k][wr + 16 * i + li];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = Bs[cur][k][wc + 16 * j + li];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) sstore(cur ^ 1);
+    __syncthreads();
+  }
+  double gmax = 0.0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = m0 + wr + 16 * i + li;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = n0 + wc + 16 * j + lk + 4 * r;
+        if (col < t.n && row < t.m) {
+          gC[(int64_t)col * t.ldc + row] = acc[i][j][r];
+          gmax = fmax(gmax, fabs(acc[i][j][r]));
+        }
+      }
+  }
+  if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
+}
+
 // Small-k variant of k_gemm (every task of the launch has k <= 64: the in-block updates and the
 // GEMM-form triangular solves): the whole K extent of the A and B tiles is staged in one shot
 // (32 loads per thread in flight together with the 16 C loads), so a launch pays one memory
@@ -172,7 +268,6 @@ __global__ __launch_bounds__(256) void k_gemm(const GemmTask* __restrict__ tasks
 // C[16 i + (l & 15)][16 j + (l >> 4) + 4 r]).  Per element the MFMA's chain is one fused
 // multiply-add per k in ascending order, the zero-filled k >= K terms exact no-ops: bitwise the
 // VALU tiles' result.
-typedef double v4d __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ double k64_tile_mfma(const gdbl* gA, int lda, const gdbl* gB, int ldb, gdbl* gC, int ldc,
                                                 int m, int n, int K, int m0, int n0,
                                                 double (&As)[64][GBM + 2], double (&Bs)[64][GBN + 2]) {
@@ -1088,6 +1183,8 @@ hipError_t launch_gemm_g(hipStream_t st, int64_t ntiles, const GemmTask* tasks, 
         tasks, ntask, ntiles);
   else if (tile == 65 && trsm) k_gemm_k64<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 65) k_gemm_k64<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  else if (tile == 66 && trsm) k_gemm64_mfma<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
+  else if (tile == 66) k_gemm64_mfma<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (trsm) k_gemm<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else k_gemm<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   return hipGetLastError();

@@ -180,7 +180,7 @@ static int build_schedule(smlu_handle* h) {
     if (tile == 64 && h->small_k) {                    // every k <= 64: one-shot K staging
       int kmax = 0;
       for (auto& g : cand) kmax = std::max(kmax, g.k);
-      if (kmax <= 64) tile = 65;
+      tile = kmax <= 64 ? 65 : h->opts.use_mfma ? 66 : 64;   // 66: the 64 tile on the matrix cores
     }
     if (step < 0 && !tpatch)   // F22: longest k first, so the launch's last tiles are short ones
       std::stable_sort(cand.begin(), cand.end(), [](const GemmTask& a, const GemmTask& b) { return a.k > b.k; });

@@ -262,6 +262,7 @@ double smlu_stat(const smlu_handle* h, const char* key) {
       else if (v == "k64" && gemm && L.aux == 65) ++c;
       else if (v == "k64_trsm" && trsm && L.aux == 65) ++c;
       else if (v == "valu64" && gemm && L.aux == 64) ++c;
+      else if (v == "mfma64" && gemm && L.aux == 66) ++c;
       else if (v == "valu64_trsm" && trsm && L.aux == 64) ++c;
       else if (v == "tri_inv" && L.kind == K_TRIINV) ++c;
       else if (v == "panel_tall" && L.kind == K_PANEL && L.nwg > 512) ++c;
