@@ -999,20 +999,45 @@ __global__ __launch_bounds__(256) void k_dominance(int64_t n, const int64_t* __r
                                                    const double* __restrict__ a, int32_t* __restrict__ flags) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  // entries eight at a time (all loads of a group in flight together), summed in order
   double d = 0.0, off = 0.0;
-  for (int64_t e = colptr[i]; e < colptr[i + 1]; ++e) {
-    const double v = fabs(a[e]);
-    if (arow[e] == i) d += v;
-    else off += v;
+  const int64_t c1 = colptr[i + 1];
+  for (int64_t e0 = colptr[i]; e0 < c1; e0 += 8) {
+    double v[8];
+    int32_t r[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v[k] = e0 + k < c1 ? a[e0 + k] : 0.0;
+      r[k] = e0 + k < c1 ? arow[e0 + k] : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (r[k] < 0) continue;
+      if (r[k] == i) d += fabs(v[k]);
+      else off += fabs(v[k]);
+    }
   }
   if (!(d > 0.0 && d >= off)) flags[0] = 0;
   d = 0.0;
   off = 0.0;
-  for (int64_t t = rowptr[i]; t < rowptr[i + 1]; ++t) {
-    const int32_t e = ent[t];
-    const double v = fabs(a[e]);
-    if (acol[e] == i) d += v;
-    else off += v;
+  const int64_t r1 = rowptr[i + 1];
+  for (int64_t t0 = rowptr[i]; t0 < r1; t0 += 8) {
+    int32_t e[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = t0 + k < r1 ? ent[t0 + k] : -1;
+    double v[8];
+    int32_t c[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v[k] = e[k] >= 0 ? a[e[k]] : 0.0;
+      c[k] = e[k] >= 0 ? acol[e[k]] : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (e[k] < 0) continue;
+      if (c[k] == i) d += fabs(v[k]);
+      else off += fabs(v[k]);
+    }
   }
   if (!(d > 0.0 && d >= off)) flags[1] = 0;
 }
@@ -1025,35 +1050,41 @@ __global__ __launch_bounds__(256) void k_dominance(int64_t n, const int64_t* __r
 // none), out[10] = how many such nodes.  Legal words are the ones publish_info / the growth epilogues
 // write: bit 0 zero pivot, bit 1 weak pivot, bits 2.. = 1 + the front-local column of the first zero
 // pivot, at most ns (0 <= v < (ns + 1) << 2).  Any other word is not a pivot status and is never
-// read as one (the host fails with SMLU_ERR_STATE).  One workgroup of 1024 threads.
-__global__ __launch_bounds__(1024) void k_status(const int32_t* __restrict__ info, int64_t nnodes,
-                                                 const SNode* __restrict__ sn,
-                                                 const int32_t* __restrict__ words, int nwords,
-                                                 long long* __restrict__ out, long long seq) {
-  __shared__ long long s_weak[1024], s_nbad[1024];
-  __shared__ long long s_sing[1024], s_flag[1024], s_bad[1024];
-  const int tid = threadIdx.x;
+// read as one (the host fails with SMLU_ERR_STATE).  One workgroup of 1024 threads; above
+// kStatusSplit nodes the scan runs first over kStatusParts workgroups (k_status_part, five partial
+// results each at out[16 + 5 p ...]) and k_status reduces those (128^3: 0.54 ms -> a few us).
+constexpr int64_t kStatusSplit = 16384;
+constexpr int kStatusParts = 512;
+struct StatusAcc {
   long long weak = 0, nbad = 0, sing = LLONG_MAX, flag = LLONG_MAX, bad = LLONG_MAX;
-  if (info)
-    for (int64_t i = tid; i < nnodes; i += 1024) {
-      const int32_t v = info[i];
-      const bool legal = v >= 0 && (!sn || (int64_t)v < (((int64_t)sn[i].ns + 1) << 2));
-      if (!legal) {
-        ++nbad;
-        if (i < bad) bad = i;
-        continue;
-      }
-      weak += (v >> 1) & 1;
-      if ((v & 1) && i < sing) sing = i;
-      if ((v & 3) && i < flag) flag = i;
+};
+__device__ __forceinline__ void status_scan(StatusAcc& a, const int32_t* __restrict__ info, const SNode* __restrict__ sn,
+                                            int64_t i0, int64_t nnodes, int64_t stride) {
+  for (int64_t i = i0; i < nnodes; i += stride) {
+    const int32_t v = info[i];
+    const bool legal = v >= 0 && (!sn || (int64_t)v < (((int64_t)sn[i].ns + 1) << 2));
+    if (!legal) {
+      ++a.nbad;
+      if (i < a.bad) a.bad = i;
+      continue;
     }
-  s_weak[tid] = weak;
-  s_nbad[tid] = nbad;
-  s_sing[tid] = sing;
-  s_flag[tid] = flag;
-  s_bad[tid] = bad;
+    a.weak += (v >> 1) & 1;
+    if ((v & 1) && i < a.sing) a.sing = i;
+    if ((v & 3) && i < a.flag) a.flag = i;
+  }
+}
+// workgroup reduction of the five fields (NT threads), result in s_*[0]
+template <int NT>
+__device__ __forceinline__ void status_reduce(StatusAcc a, long long* s_weak, long long* s_nbad, long long* s_sing,
+                                              long long* s_flag, long long* s_bad) {
+  const int tid = threadIdx.x;
+  s_weak[tid] = a.weak;
+  s_nbad[tid] = a.nbad;
+  s_sing[tid] = a.sing;
+  s_flag[tid] = a.flag;
+  s_bad[tid] = a.bad;
   __syncthreads();
-  for (int w = 512; w > 0; w >>= 1) {
+  for (int w = NT / 2; w > 0; w >>= 1) {
     if (tid < w) {
       s_weak[tid] += s_weak[tid + w];
       s_nbad[tid] += s_nbad[tid + w];
@@ -1063,6 +1094,43 @@ __global__ __launch_bounds__(1024) void k_status(const int32_t* __restrict__ inf
     }
     __syncthreads();
   }
+}
+__global__ __launch_bounds__(256) void k_status_part(const int32_t* __restrict__ info, int64_t nnodes,
+                                                     const SNode* __restrict__ sn, long long* __restrict__ part) {
+  __shared__ long long s_weak[256], s_nbad[256], s_sing[256], s_flag[256], s_bad[256];
+  StatusAcc a;
+  status_scan(a, info, sn, (int64_t)blockIdx.x * 256 + threadIdx.x, nnodes, (int64_t)gridDim.x * 256);
+  status_reduce<256>(a, s_weak, s_nbad, s_sing, s_flag, s_bad);
+  if (threadIdx.x == 0) {
+    long long* o = part + 5 * blockIdx.x;
+    o[0] = s_weak[0];
+    o[1] = s_nbad[0];
+    o[2] = s_sing[0];
+    o[3] = s_flag[0];
+    o[4] = s_bad[0];
+  }
+}
+__global__ __launch_bounds__(1024) void k_status(const int32_t* __restrict__ info, int64_t nnodes,
+                                                 const SNode* __restrict__ sn,
+                                                 const int32_t* __restrict__ words, int nwords,
+                                                 long long* __restrict__ out, long long seq, int nparts) {
+  __shared__ long long s_weak[1024], s_nbad[1024];
+  __shared__ long long s_sing[1024], s_flag[1024], s_bad[1024];
+  const int tid = threadIdx.x;
+  StatusAcc a;
+  if (info && nparts > 0) {
+    if (tid < nparts) {
+      const long long* o = out + 16 + 5 * tid;
+      a.weak = o[0];
+      a.nbad = o[1];
+      a.sing = o[2];
+      a.flag = o[3];
+      a.bad = o[4];
+    }
+  } else if (info) {
+    status_scan(a, info, sn, tid, nnodes, 1024);
+  }
+  status_reduce<1024>(a, s_weak, s_nbad, s_sing, s_flag, s_bad);
   if (tid == 0) {
     const long long sg = s_sing[0], fl = s_flag[0], bd = s_bad[0];
     out[1] = s_weak[0];
@@ -1274,7 +1342,12 @@ hipError_t launch_front_hash(hipStream_t st, int64_t nsup, const SNode* sn, cons
 }
 hipError_t launch_status(hipStream_t st, const int32_t* info, int64_t nnodes, const SNode* sn, const int32_t* words,
                          int nwords, long long* out, long long seq) {
-  k_status<<<1, 1024, 0, st>>>(info, nnodes, sn, words, nwords, out, seq);
+  int nparts = 0;
+  if (info && nnodes > kStatusSplit) {   // out holds 16 + 5 * kStatusParts words (schedule.cpp)
+    nparts = kStatusParts;
+    k_status_part<<<(unsigned)nparts, 256, 0, st>>>(info, nnodes, sn, out + 16);
+  }
+  k_status<<<1, 1024, 0, st>>>(info, nnodes, sn, words, nwords, out, seq, nparts);
   return hipGetLastError();
 }
 hipError_t launch_axpy1(hipStream_t st, int64_t n, const double* d, double* x) {

@@ -1599,7 +1599,7 @@ int setup_device(smlu_handle* h) {
   const int64_t nnodes = P.nsup + (int64_t)h->lay.blocks.size();
   HIPCHK(h->info.alloc((size_t)std::max<int64_t>(nnodes, 1)));
   HIPCHK(init_kernel_attributes());
-  if (!h->rb.p) HIPCHK(h->rb.alloc(16));
+  if (!h->rb.p) HIPCHK(h->rb.alloc(16 + 5 * 512));   // record + k_status_part's partials
   return build_schedule(h);
 }
 
