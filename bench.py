@@ -487,7 +487,7 @@ def main():
                        "dense_flops": dense_flops, "ordering": args.ordering,
                        "parallelism": (f"tree-partition{world} (proportional mapping, RCCL p2p)"
                                        if partitioned else f"replicas{world}" if world > 1 else "single")},
-            "roofline": {"bound": "mfma", "kernel": "Schur-complement GEMM group: k_gemm128_mfma2 (fp64 MFMA 128x128 tile) + k_gemm_k64 (k <= 64) + k_gemm (VALU 64x64, small launches)",
+            "roofline": {"bound": "mfma", "kernel": "Schur-complement GEMM group: k_gemm128_mfma3 (fp64 MFMA 128x128 tile) + k_gemm_k64 (k <= 64, one-shot MFMA 64x64) + k_gemm64_mfma (MFMA 64x64, small launches)",
                          "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": (achieved / FP64_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic,
@@ -496,7 +496,7 @@ def main():
                          "flops_per_launch": gemm_flops / n_gemm if (n_gemm and not partitioned) else None,
                          "algorithmic_bytes_per_launch": F.stat("gemm_bytes") / n_gemm if (n_gemm and not partitioned) else None,
                          "traffic_source": traffic_src, "kernels_sha": sha,
-                         "note": "fp64 MFMA (v_mfma_f64_16x16x4) 128x128 tiles for large launches, fp64 VALU "
+                         "note": "fp64 MFMA (v_mfma_f64_16x16x4) 128x128 tiles for large launches, fp64 MFMA "
                                  "64x64 tiles for small ones; peak = MI355X fp64 dense peak; "
                                  "achieved = GEMM flops per refactor / HIP-event time of the GEMM "
                                  "launches per refactor (graph-captured events on the launch "
