@@ -2,8 +2,7 @@
 // pivoting-mode decision, and the refactor entry points (lu! of src/SharedMemSparseLU.jl:245-279).
 #include "handle.hpp"
 
-static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, double piv_tol) {
-  hipStream_t st = h->stream;
+static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, double piv_tol, hipStream_t st) {
   switch (L.kind) {
     case K_MEMSET_STORE:
       return hipMemsetAsync(h->store.p + L.off, 0, (size_t)L.cnt * sizeof(double), st);
@@ -68,12 +67,26 @@ static int enqueue_factor(smlu_handle* h, Timer& tm, bool dbg, int seg) {
   }
   // A given (p, q) order means "no pivoting on top": only a zero diagonal moves (diag_tol 0).
 launches:
+  // the size classes of one level's small fronts (K_FRONT_LDS launches of one overlap group)
+  // alternate between the handle's stream and its side stream: a fork event ahead of the group,
+  // a join event after its last launch
+  auto group = [&](size_t i) { return h->fac[i].kind == K_FRONT_LDS ? h->fac[i].aux2 : 0; };
+  int gi = 0;   // index of the current launch inside its group
   for (size_t li = lo; li < hi; ++li) {
     const Launch& L = h->fac[li];
+    const int64_t g = group(li);
+    const bool cont = g > 0 && li > lo && group(li - 1) == g;
+    const bool more = g > 0 && li + 1 < hi && group(li + 1) == g;
+    gi = cont ? gi + 1 : 0;
+    // fork: the side stream starts after everything before the group (recorded ahead of the
+    // group's first launch, waited on by the side stream before its first)
+    if (gi == 0 && more) HIPCHK(hipEventRecord(h->fork_ev, st));
+    if (gi == 1) HIPCHK(hipStreamWaitEvent(h->side, h->fork_ev, 0));
+    hipStream_t ls = (gi & 1) ? h->side : st;
     hipEvent_t stop;
-    HIPCHK(tm.begin(L.kind, &stop, st));
-    hipError_t e = run_launch(h, L, diag_tol, piv_tol);
-    if (e == hipSuccess && dbg) e = hipStreamSynchronize(st);
+    HIPCHK(tm.begin(L.kind, &stop, ls));
+    hipError_t e = run_launch(h, L, diag_tol, piv_tol, ls);
+    if (e == hipSuccess && dbg) e = hipStreamSynchronize(ls);
     if (e != hipSuccess) {
       char buf[256];
       std::snprintf(buf, sizeof buf, "HIP error '%s' in launch kind=%d step=%d off=%lld cnt=%lld nwg=%lld aux=%lld aux2=%lld",
@@ -82,6 +95,10 @@ launches:
       return fail(h, SMLU_ERR_HIP, buf);
     }
     HIPCHK(tm.end(stop));
+    if (gi >= 1 && !more) {   // join: the main stream continues after both branches
+      HIPCHK(hipEventRecord(h->join_ev, h->side));
+      HIPCHK(hipStreamWaitEvent(st, h->join_ev, 0));
+    }
   }
   return SMLU_OK;
 }

@@ -225,6 +225,10 @@ struct smlu_handle {
   Plan plan;
   int device = 0;
   hipStream_t stream = nullptr;
+  // second stream of the factor sequence: the small-front size classes of one level run on two
+  // streams (fork / join by events, captured into the same graph as parallel branches)
+  hipStream_t side = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   std::string err;
   int64_t errcol = -1;
   bool have_numeric = false;
@@ -410,6 +414,11 @@ struct smlu_handle {
     ev_kind.clear();
     rb.free();
     if (ev_caller) (void)hipEventDestroy(ev_caller);
+    if (fork_ev) (void)hipEventDestroy(fork_ev);
+    if (join_ev) (void)hipEventDestroy(join_ev);
+    fork_ev = join_ev = nullptr;
+    if (side) (void)hipStreamDestroy(side);
+    side = nullptr;
     if (stream) (void)hipStreamDestroy(stream);
     stream = nullptr;
   }

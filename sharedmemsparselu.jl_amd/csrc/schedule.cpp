@@ -376,6 +376,7 @@ static int build_schedule(smlu_handle* h) {
         }
         L.cnt = ((int64_t)ilist.size() - L.off) / 3;
         L.aux = Mmax;
+        L.aux2 = l + 1;   // overlap group: the size classes of one level are independent
         if (L.cnt > 0) h->fac.push_back(L);
       }
     }
@@ -1544,6 +1545,9 @@ int setup_device(smlu_handle* h) {
   int prio_lo = 0, prio_hi = 0;
   HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   if (!h->stream) HIPCHK(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi));
+  if (!h->side) HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_hi));
+  if (!h->fork_ev) HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
+  if (!h->join_ev) HIPCHK(hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
   hipStream_t st = h->stream;
   // this rank's layout: the plan's own on one GPU; ordinary fronts + owned column blocks of
   // the shared fronts on a partitioned handle
