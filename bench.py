@@ -325,6 +325,9 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--test-one-gpu", action="store_true",
                     help="rehearsal: all ranks on cuda:0, gloo transport (never for measurements)")
+    ap.add_argument("--check-single", action="store_true",
+                    help="partitioned run: after the timed steps, rank 0 factors the last values on one GPU "
+                         "and every rank's solution is compared with that one (rehearsals, VERDICT r05)")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: independent replicas instead of the partitioned factorization")
     ap.add_argument("--launch-check", action="store_true",
@@ -390,7 +393,7 @@ def main():
         vals.append(v)
     torch.cuda.synchronize()
 
-    kinds = ["gemm", "gemmu", "gemmo", "gemm22", "panel", "trsm", "urows", "small", "assemble", "memset"]
+    kinds = ["gemm", "gemmu", "gemmo", "gemm22", "panel", "trsm", "urows", "small", "assemble"]
     kind_ms = {k: 0.0 for k in kinds}
 
     def step(r):
@@ -438,6 +441,25 @@ def main():
                    "comm_bytes_recv_refactor": F.stat("comm_bytes_recv_refactor"),
                    "shared_fronts": int(F.stat("shared_fronts")),
                    "store_bytes_rank": F.stat("store_bytes_rank")})
+    fst = {k: F.stat(k) for k in ['dense_flops', 'gemm22_flops', 'gemm_bytes', 'gemm_flops', 'gemm_launches', 'launches', 'upd']}   # the handle's figures for the line (before any close)
+    if args.check_single and partitioned:
+        # the partitioned solution against the single-GPU factorization of the same values (the
+        # partitioned handles are released first: on a one-GPU rehearsal they share the card)
+        F.close()
+        dist.barrier()
+        xs = torch.zeros(n, dtype=torch.float64)
+        if rank == 0:
+            Fs = smlu.ParallelSparseLU(A, grid=grid, device=local)
+            Fs.refactor_device(vals[-1])
+            xd = torch.empty_like(b)
+            Fs.solve_device(xd, b)
+            torch.cuda.synchronize()
+            xs = xd.cpu()
+            Fs.close()
+        dist.broadcast(xs, 0)
+        xs = xs.numpy()
+        me["x_vs_single_gpu_max_rel"] = float(np.abs(xh - xs).max() / np.abs(xs).max())
+        me["single_gpu_residual"] = float(np.abs(Al @ xs - bh).max() / np.abs(bh).max())
     per_rank = [me]
     if world > 1:
         per_rank = [None] * world
@@ -445,12 +467,12 @@ def main():
 
     if rank == 0:
         K = args.steps
-        gemm_flops = F.stat("gemm_flops")
+        gemm_flops = fst["gemm_flops"]
         ms_gemm = (kind_ms["gemm"] + kind_ms["gemmu"] + kind_ms["gemmo"] + kind_ms["gemm22"]) / K
-        upd = F.stat("upd")
-        dense_flops = F.stat("dense_flops")
+        upd = fst["upd"]
+        dense_flops = fst["dense_flops"]
         achieved = gemm_flops / (ms_gemm * 1e-3) / 1e12 if ms_gemm > 0 else None
-        n_gemm = F.stat("gemm_launches")
+        n_gemm = fst["gemm_launches"]
         avg_us = ms_gemm * 1e3 / n_gemm if (n_gemm and ms_gemm > 0) else None
         # PMC traffic comes from a committed rocprofv3 profile (profiles/<round>/pmc_gemm_N.json);
         # it is reported only when that profile was taken from this exact library source
@@ -494,7 +516,7 @@ def main():
                          "launches_per_step": n_gemm if not partitioned else None,
                          "avg_launch_us": avg_us,
                          "flops_per_launch": gemm_flops / n_gemm if (n_gemm and not partitioned) else None,
-                         "algorithmic_bytes_per_launch": F.stat("gemm_bytes") / n_gemm if (n_gemm and not partitioned) else None,
+                         "algorithmic_bytes_per_launch": fst["gemm_bytes"] / n_gemm if (n_gemm and not partitioned) else None,
                          "traffic_source": traffic_src, "kernels_sha": sha,
                          "note": "fp64 MFMA (v_mfma_f64_16x16x4) 128x128 tiles for large launches, fp64 MFMA "
                                  "64x64 tiles for small ones; peak = MI355X fp64 dense peak; "
@@ -503,12 +525,12 @@ def main():
                                  "stream); traffic = HBM bytes per launch from rocprofv3 PMC "
                                  "(FETCH_SIZE x2 + WRITE_SIZE, " + traffic_src + ")"},
             "kernel_ms_per_step": {k: v / K for k, v in kind_ms.items()},
-            "launches_per_refactor": F.stat("launches"),
+            "launches_per_refactor": fst["launches"],
             # per-kind HIP-event times exist for the single-GPU path only (partitioned: None)
-            "gemm_split": ({"panel_tflops": (gemm_flops - F.stat("gemm22_flops")) / ((kind_ms["gemm"] + kind_ms["gemmu"] + kind_ms["gemmo"]) / K) / 1e9,
-                            "f22_tflops": F.stat("gemm22_flops") / (kind_ms["gemm22"] / K) / 1e9,
-                            "panel_gflop": (gemm_flops - F.stat("gemm22_flops")) / 1e9,
-                            "f22_gflop": F.stat("gemm22_flops") / 1e9}
+            "gemm_split": ({"panel_tflops": (gemm_flops - fst["gemm22_flops"]) / ((kind_ms["gemm"] + kind_ms["gemmu"] + kind_ms["gemmo"]) / K) / 1e9,
+                            "f22_tflops": fst["gemm22_flops"] / (kind_ms["gemm22"] / K) / 1e9,
+                            "panel_gflop": (gemm_flops - fst["gemm22_flops"]) / 1e9,
+                            "f22_gflop": fst["gemm22_flops"] / 1e9}
                            if ms_gemm > 0 and kind_ms["gemm22"] > 0 else None),
             "refactor_tflops": dense_flops / (ms_per_step * 1e-3) / 1e12,
             # measured HBM traffic of a whole refactor (PMC FETCH_SIZE x2 + WRITE_SIZE over every
@@ -523,6 +545,9 @@ def main():
         }
         if partitioned:
             res["rccl_nranks"] = min(r.get("rccl_nranks", 0) for r in per_rank)
+            res["transport"] = "host (gloo, one-GPU rehearsal)" if args.test_one_gpu else "rccl"
+            if args.check_single:
+                res["x_vs_single_gpu_max_rel"] = max(r["x_vs_single_gpu_max_rel"] for r in per_rank)
         if not args.no_cpu and world == 1:
             log("ordering comparison (host symbolic analysis) ...")
             res["config"]["ordering_compare"] = ordering_compare(N)

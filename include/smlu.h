@@ -62,8 +62,9 @@ typedef struct smlu_opts {
     int32_t profile;      /* 1 = record per-kernel-class HIP events during refactor/solve */
     int64_t leaf_size;    /* nested-dissection leaf size (default 64) */
     int32_t use_mfma;     /* 1 (default) = fp64 MFMA (v_mfma_f64_16x16x4) for the dense Schur
-                             updates of large launches; 0 = fp64 VALU tiles (env SMLU_VALU_GEMM).
-                             Bitwise-identical results; MFMA is faster on large tiles */
+                             updates and the GEMM-form triangular solves; 0 = a comparison path:
+                             the VALU 64x64 tile for k > 64 launches and k_step_trsm for the
+                             triangular solves (results equal to rounding) */
     int32_t refine;       /* iterative-refinement steps in smlu_solve*: -1 (default) = up to 3 only
                              when the last factorization flagged weak pivots (the pivot-failure
                              fallback of the diagonal-tile pivoting); 0 = never;
@@ -318,6 +319,17 @@ int     smlu_plan_partition(const smlu_plan* plan, int32_t nparts, int32_t* owne
  * broadcast staging). */
 int     smlu_plan_rank_memory(const smlu_plan* plan, int32_t nparts, int32_t rank, double* store_bytes,
                               double* scratch_bytes, double* stage_bytes);
+/* Host-only: rank `rank`'s whole schedule of a `nparts`-rank handle, built by the same code as
+ * smlu_dist_create but with no device (the pairing check of the collective schedule, e.g. 256^3
+ * on 8 ranks in a CPU test).  Its communication steps in execution order, flattened into `ops`
+ * (int64 words; ops = NULL: only *len): per step
+ *   seq (0 factor, 1 forward solve, 2 backward solve), type (0 exchange, 1 broadcast), root, bytes, cnt,
+ *   then cnt x (peer, sbytes, rbytes) for an exchange, or the cnt ranks of the group for a broadcast.
+ * bytes[0..4]: device bytes the rank allocates in all, its factor store, its front scratch, its
+ * staging + received-block buffer, and the pinned host staging of a host-memory transport; counts[0..2]:
+ * factor launches, shared fronts the rank works on, owned column blocks. */
+int     smlu_plan_rank_schedule(const smlu_plan* plan, int32_t nparts, int32_t rank, int64_t* ops, int64_t cap,
+                                int64_t* len, double bytes[5], int64_t counts[3]);
 /* Host-only critical-path projection of the partitioned factorization at `tflops` per GPU,
  * `gbs` GB/s per link and `lat_us` per message: returns the projected seconds, *t1 = one GPU. */
 double  smlu_plan_project(const smlu_plan* plan, int32_t nparts, double tflops, double gbs, double lat_us,
@@ -341,7 +353,7 @@ int smlu_dev_copy(smlu_handle* h, int which, int64_t off, int64_t cnt, double* o
  *   SMLU_T128MIN=t     128x128 MFMA tiles for GEMM launches with >= t output tiles (default 512)
  *   SMLU_SMALLK=0      no one-shot k <= 64 GEMM tile (tests: forces the 64x64 VALU tile, and the
  *                      GEMM-form TRSM onto the 128 tile when SMLU_T128MIN allows it)
- *   SMLU_FULLPIV_NS=k  largest front with full-candidate pivoting (tests; default: 512, or 128
+ *   SMLU_FULLPIV_NS=k  largest front with full-candidate pivoting (tests; default: 512, or 0
  *                      for diagonally dominant values)
  *   SMLU_SWEEP_SPIN=s  polls before a sync-free solve wait gives up and the solve is re-run on the
  *                      per-block schedule (default 2^22; 0 = at once, tests)

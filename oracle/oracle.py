@@ -245,12 +245,12 @@ def front_modes(fronts, pivmode, dominant_values, full_piv_ns=None):
     """The GPU schedule's candidate set per front (restated from DESIGN.md §4 / build_schedule):
     M <= 128 -> 0 (small front, all fully-summed rows); else ns <= limit -> 1 (all fully-summed
     rows), otherwise 2 (the 64 x 64 diagonal tile).  limit: unbounded after a re-pivoting refactor
-    (pivmode 1), 128 for dominant values, 512 otherwise."""
+    (pivmode 1), 0 for dominant values (every blocked front on the diagonal tile), 512 otherwise."""
     first, rowptr = fronts["first"], fronts["rowptr"]
     ns = np.diff(first)
     M = ns + np.diff(rowptr)
     if full_piv_ns is None:
-        full_piv_ns = np.iinfo(np.int64).max if pivmode == 1 else (SMALL_M if dominant_values else FULL_PIV_NS)
+        full_piv_ns = np.iinfo(np.int64).max if pivmode == 1 else (0 if dominant_values else FULL_PIV_NS)
     return np.where(M <= SMALL_M, 0, np.where(ns <= full_piv_ns, 1, 2)).astype(np.int32)
 
 

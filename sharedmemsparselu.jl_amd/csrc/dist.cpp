@@ -238,3 +238,66 @@ double smlu_plan_project(const smlu_plan* plan, int32_t nparts, double tflops, d
   return project_partition(P, tflops, gbs, lat_us, t1);
 }
 
+
+int smlu_plan_rank_schedule(const smlu_plan* plan, int32_t nparts, int32_t rank, int64_t* ops, int64_t cap,
+                            int64_t* len, double bytes[5], int64_t counts[3]) {
+  if (!plan || !len || nparts < 1 || rank < 0 || rank >= nparts || (ops && cap < 0))
+    return fail(nullptr, SMLU_ERR_ARG, "invalid arguments");
+  std::unique_ptr<smlu_handle> h(new (std::nothrow) smlu_handle());
+  if (!h) return fail(nullptr, SMLU_ERR_ALLOC, "allocation failed");
+  smlu_default_opts(&h->opts);
+  h->opts.index_base = 0;
+  int rc = SMLU_OK;
+  try {
+    h->plan = plan->plan;   // copy: the partition is this query's
+    h->rank = rank;
+    h->nranks = nparts;
+    h->dominant = true;     // the collective schedule does not depend on the pivoting mode
+    if (nparts > 1) {
+      if (tune().ob > 0) h->ob = tune().ob;
+      h->plan.compute_owners(nparts, h->ob);
+    }
+    rc = build_schedule_host(h.get());
+  } catch (const std::bad_alloc&) {
+    return fail(nullptr, SMLU_ERR_ALLOC, "host allocation failed");
+  }
+  if (rc != SMLU_OK) return fail(nullptr, rc, h->err);
+  int64_t k = 0;
+  auto put = [&](int64_t v) {
+    if (ops && k < cap) ops[k] = v;
+    ++k;
+  };
+  const std::vector<int>* seqs[3] = {&h->fac_comm, &h->fwd_comm, &h->bwd_comm};
+  for (int q = 0; q < 3; ++q)
+    for (int id : *seqs[q]) {
+      const CommOp& op = h->comm[id];
+      put(q);
+      put(op.type);
+      put(op.type == 1 ? op.root : -1);
+      put(op.type == 1 ? op.bytes : 0);
+      if (op.type == 1) {
+        put((int64_t)op.grp.size());
+        for (int32_t g : op.grp) put(g);
+      } else {
+        put((int64_t)op.peer.size());
+        for (size_t i = 0; i < op.peer.size(); ++i) {
+          put(op.peer[i]);
+          put(op.sbytes[i]);
+          put(op.rbytes[i]);
+        }
+      }
+    }
+  *len = k;
+  if (bytes)
+    for (int i = 0; i < 5; ++i) bytes[i] = h->host_bytes[i];
+  if (counts) {
+    counts[0] = (int64_t)h->fac.size();
+    int64_t sh = 0;
+    for (int64_t s = 0; s < h->plan.nsup && nparts > 1; ++s)
+      if (h->plan.dist(s) && std::binary_search(h->plan.group[s].begin(), h->plan.group[s].end(), rank)) ++sh;
+    counts[1] = sh;
+    counts[2] = (int64_t)h->lay.blocks.size();
+  }
+  if (ops && k > cap) return fail(nullptr, SMLU_ERR_ARG, "ops buffer too small");
+  return SMLU_OK;
+}

@@ -4,10 +4,6 @@
 
 static hipError_t run_launch(smlu_handle* h, const Launch& L, double diag_tol, double piv_tol, hipStream_t st) {
   switch (L.kind) {
-    case K_MEMSET_STORE:
-      return hipMemsetAsync(h->store.p + L.off, 0, (size_t)L.cnt * sizeof(double), st);
-    case K_MEMSET_SCRATCH:
-      return hipMemsetAsync(h->scratch.p + L.off, 0, (size_t)L.cnt * sizeof(double), st);
     case K_EXTADD:
       return launch_assemble(st, L.cnt, h->xcols.p + L.off, h->xtasks.p, h->aents.p, h->sn.p, h->relmap.p,
                              h->A.p, h->Arow.p, h->Rs.p, h->store.p, h->scratch.p);
@@ -70,34 +66,48 @@ launches:
   // the size classes of one level's small fronts (K_FRONT_LDS launches of one overlap group)
   // alternate between the handle's stream and its side stream: a fork event ahead of the group,
   // a join event after its last launch
+  // (profile mode: a group is timed once, on the main stream from before the fork to after the
+  // join, so the overlapped branches are not counted twice)
   auto group = [&](size_t i) { return h->fac[i].kind == K_FRONT_LDS ? h->fac[i].aux2 : 0; };
   int gi = 0;   // index of the current launch inside its group
+  hipEvent_t gstop = nullptr;
   for (size_t li = lo; li < hi; ++li) {
     const Launch& L = h->fac[li];
     const int64_t g = group(li);
     const bool cont = g > 0 && li > lo && group(li - 1) == g;
     const bool more = g > 0 && li + 1 < hi && group(li + 1) == g;
     gi = cont ? gi + 1 : 0;
+    const bool grouped = cont || more;
     // fork: the side stream starts after everything before the group (recorded ahead of the
     // group's first launch, waited on by the side stream before its first)
-    if (gi == 0 && more) HIPCHK(hipEventRecord(h->fork_ev, st));
+    if (gi == 0 && more) {
+      HIPCHK(tm.begin(L.kind, &gstop, st));
+      HIPCHK(hipEventRecord(h->fork_ev, st));
+    }
     if (gi == 1) HIPCHK(hipStreamWaitEvent(h->side, h->fork_ev, 0));
     hipStream_t ls = (gi & 1) ? h->side : st;
-    hipEvent_t stop;
-    HIPCHK(tm.begin(L.kind, &stop, ls));
+    hipEvent_t stop = nullptr;
+    if (!grouped) HIPCHK(tm.begin(L.kind, &stop, ls));
     hipError_t e = run_launch(h, L, diag_tol, piv_tol, ls);
     if (e == hipSuccess && dbg) e = hipStreamSynchronize(ls);
     if (e != hipSuccess) {
+      if (gi >= 1) {   // the side stream's branch is joined on the error path too (capture stays valid)
+        (void)hipEventRecord(h->join_ev, h->side);
+        (void)hipStreamWaitEvent(st, h->join_ev, 0);
+      }
       char buf[256];
       std::snprintf(buf, sizeof buf, "HIP error '%s' in launch kind=%d step=%d off=%lld cnt=%lld nwg=%lld aux=%lld aux2=%lld",
                     hipGetErrorString(e), L.kind, L.step, (long long)L.off, (long long)L.cnt,
                     (long long)L.nwg, (long long)L.aux, (long long)L.aux2);
       return fail(h, SMLU_ERR_HIP, buf);
     }
-    HIPCHK(tm.end(stop));
+    if (!grouped) HIPCHK(tm.end(stop));
     if (gi >= 1 && !more) {   // join: the main stream continues after both branches
       HIPCHK(hipEventRecord(h->join_ev, h->side));
       HIPCHK(hipStreamWaitEvent(st, h->join_ev, 0));
+      tm.st = st;
+      HIPCHK(tm.end(gstop));
+      gstop = nullptr;
     }
   }
   return SMLU_OK;
@@ -422,6 +432,14 @@ int refactor_csc_impl(smlu_handle* h, int64_t n, const int64_t* colptr, const in
   h->release_buffers();
   h->have_numeric = false;
   h->given_Rs = false;
+  // the caller's UMFPACK pattern (smlu_create_with_pivots) belongs to the old (p, q) and the old
+  // pattern of A: the new factors are exported on their own structural pattern
+  h->given_pattern = false;
+  h->gLp.clear();
+  h->gLi.clear();
+  h->gUp.clear();
+  h->gUi.clear();
+  h->pattern_dropped = 0;
   h->plan = Plan();
   std::string e;
   try {

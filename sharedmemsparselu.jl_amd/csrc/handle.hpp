@@ -99,11 +99,11 @@ constexpr int kOBDefault = 384;   // outer block of the two-level blocked front 
 extern thread_local std::string g_last_error;
 
 enum Kind : int {
-  K_MEMSET_STORE, K_MEMSET_SCRATCH, K_SCATTER, K_EXTADD, K_FRONT_LDS, K_PANEL, K_TRSMU, K_TRSML,
+  K_EXTADD, K_FRONT_LDS, K_PANEL, K_TRSMU, K_TRSML,
   K_GEMM, K_FWD, K_BWD, K_FWDG, K_TRIF, K_BWDU, K_TRIB, K_GEMM22, K_LASWP, K_STEPTRSM, K_GEMMU,
   K_GEMMO, K_TRIINV, K_BWDU12C, K_VCOPY, K_FWDT, K_BWDT, K_SWEEPF, K_SWEEPB, K_UROWS, K_FWDP, K_NKIND
 };
-inline const char* const kKindName[] = {"memset", "memset", "assemble", "assemble", "small", "panel",
+inline const char* const kKindName[] = {"assemble", "small", "panel",
                                   "trsm", "trsm", "gemm", "solve", "solve", "solve", "solve",
                                   "solve", "solve", "gemm22", "trsm", "trsm", "gemmu", "gemmo", "trsm", "solve", "solve",
                                   "solve", "solve", "solve", "solve", "urows", "solve"};
@@ -322,6 +322,8 @@ struct smlu_handle {
   int64_t comm_calls = 0;
   size_t fac_graph_events = 0;
   bool graph_failed = false;
+  bool host_only = false;      // schedule built without a device (smlu_plan_rank_schedule)
+  double host_bytes[5] = {0};  // ... and the bytes it would allocate (build_schedule_host)
   int ob = kOBDefault;        // outer block width (SMLU_OB overrides; multiple of 64)
   int64_t t128_min = 512;     // 128x128 GEMM tiles when a launch has at least this many
   bool small_k = true;        // k <= 64 launches use k_gemm_k64 (SMLU_SMALLK=0: off)
@@ -529,6 +531,7 @@ int create_impl(int64_t n, const int64_t* colptr, const int64_t* rowval, const d
 std::vector<int64_t> diagonal_match(int64_t n, const int64_t* colptr, const int64_t* rowval, const double* a,
                                     int64_t base);   // smlu.cpp
 int setup_device(smlu_handle* h);                        // schedule.cpp
+int build_schedule_host(smlu_handle* h);
 int rebuild_schedule(smlu_handle* h);
 bool has_tile_fronts(const smlu_handle* h);
 int run_factor(smlu_handle* h);                          // factor.cpp

@@ -1,4 +1,5 @@
-// kernels_gemm.hip — dense fp64 Schur-complement updates C -= A*B (VALU 64/128 tiles, MFMA 128 tile).
+// kernels_gemm.hip — dense fp64 Schur-complement updates C -= A*B (MFMA 128 and 64 tiles; the VALU
+// 64 tile k_gemm is the bitwise comparison tile and the use_mfma = 0 path).
 #include "kernels_common.hpp"
 
 namespace smlu {
@@ -354,131 +355,15 @@ __global__ __launch_bounds__(256) void k_gemm_k64(const GemmTask* __restrict__ t
 }
 
 // ------------------------------------------------------------------------------------
-// Dense update C -= A*B, large tiles: 128x128 output tile per 256-thread workgroup, 8x8
-// accumulators per thread (128 VGPRs), K staged through double-buffered LDS in slices of 16
-// with the next slice prefetched into registers.  Each thread owns rows {2tx,2tx+1}+32i and
-// columns {2ty,2ty+1}+32j so every fragment read is one conflict-free ds_read_b128.
-// Per k: 8 ds_read_b128 feed 64 v_fma_f64 (0.25 doubles of LDS per FMA).
-// ------------------------------------------------------------------------------------
-#define HBM_ 128
-#define HBK_ 16
-#define HLDB_ (HBM_ + 2)
-#ifndef KK_UNROLL
-#define KK_UNROLL 2
-#endif
-__device__ __forceinline__ void gemm128_tile(const GemmTask* __restrict__ tasks, int ntask, int64_t b,
-                                             double (&As)[2][HBK_][HBM_], double (&Bs)[2][HBK_][HLDB_]) {
-  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
-  const gdbl* gA = gbl(t.A);
-  const gdbl* gB = gbl(t.B);
-  gdbl* gC = gbl(t.C);
-  int tm, tn;
-  tile_rc<HBM_>(t, b - t.tile0, tm, tn);
-  const int m0 = tm * HBM_, n0 = tn * HBM_;
-  const int tid = threadIdx.x;
-  const int tx = tid & 15, ty = tid >> 4;
-  double acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = 0.0;
-  // global->register mapping: A: row = tid & 127, k = (tid >> 7) + 2r ; B: k = tid & 15, col = (tid >> 4) + 16r
-  const int ar = tid & 127, ak = tid >> 7;
-  const int bk = tid & 15, bc = tid >> 4;
-  const int K = t.k;
-  const int arow = m0 + ar;
-  const bool arow_ok = arow < t.m;
-  const gdbl* Ap = gA + arow;
-  double ra[8], rb[8];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int kk = k0 + ak + 2 * r;
-      ra[r] = (arow_ok && kk < K) ? Ap[(int64_t)kk * t.lda] : 0.0;
-      const int col = n0 + bc + 16 * r;
-      rb[r] = (col < t.n && k0 + bk < K) ? gB[(int64_t)col * t.ldb + k0 + bk] : 0.0;
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      As[buf][ak + 2 * r][ar] = ra[r];
-      Bs[buf][bk][bc + 16 * r] = rb[r];
-    }
-  };
-  const int nk = (K + HBK_ - 1) / HBK_;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * HBK_);
-#pragma unroll KK_UNROLL
-    for (int kk = 0; kk < HBK_; ++kk) {
-      double a[8], bb[8];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const double2 v = *reinterpret_cast<const double2*>(&As[cur][kk][2 * tx + 32 * i]);
-        a[2 * i] = v.x;
-        a[2 * i + 1] = v.y;
-        const double2 w = *reinterpret_cast<const double2*>(&Bs[cur][kk][2 * ty + 32 * i]);
-        bb[2 * i] = w.x;
-        bb[2 * i + 1] = w.y;
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) acc[i][j] = fma(a[i], bb[j], acc[i][j]);
-    }
-    if (kt + 1 < nk) sstore(cur ^ 1);
-    __syncthreads();
-  }
-  // epilogue in 4 batches of 2 columns: 16 C loads in flight, then 16 stores
-#pragma unroll
-  for (int jb = 0; jb < 8; jb += 2) {
-    double cv[2][8];
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int j = jb + jj;
-      const int col = n0 + 2 * ty + 32 * (j >> 1) + (j & 1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int row = m0 + 2 * tx + 32 * (i >> 1) + (i & 1);
-        cv[jj][i] = (col < t.n && row < t.m) ? gC[(int64_t)col * t.ldc + row] : 0.0;
-      }
-    }
-#pragma unroll
-    for (int jj = 0; jj < 2; ++jj) {
-      const int j = jb + jj;
-      const int col = n0 + 2 * ty + 32 * (j >> 1) + (j & 1);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int row = m0 + 2 * tx + 32 * (i >> 1) + (i & 1);
-        if (col < t.n && row < t.m) gC[(int64_t)col * t.ldc + row] = cv[jj][i] - acc[i][j];
-      }
-    }
-  }
-}
-
-// Tiles b = blockIdx.x + i * gridDim.x: a grid smaller than the tile count leaves CUs free for
-// the latency-bound panel chain running concurrently on the other stream (look-ahead).
-__global__ __launch_bounds__(256, 2) void k_gemm128(const GemmTask* __restrict__ tasks, int ntask,
-                                                    int64_t ntiles) {
-  __shared__ __attribute__((aligned(16))) double As[2][HBK_][HBM_];
-  __shared__ __attribute__((aligned(16))) double Bs[2][HBK_][HLDB_];
-  for (int64_t b = blockIdx.x; b < ntiles; b += gridDim.x) {
-    gemm128_tile(tasks, ntask, (int64_t)gridDim.x == ntiles ? xcd_remap(b, ntiles) : b, As, Bs);
-    __syncthreads();
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// fp64 MFMA variant of the same 128x128 tile (opts.use_mfma = 1, the default; opts.use_mfma = 0
-// or SMLU_VALU_GEMM selects the VALU tiles).  v_mfma_f64_16x16x4_f64; each wave owns a 64x64 quadrant = 4x4
+// 128 x 128 output tiles on the fp64 matrix cores (opts.use_mfma = 1, the default; use_mfma = 0
+// runs every launch on the VALU 64 tile k_gemm), K staged through double-buffered LDS slices of
+// 16.  v_mfma_f64_16x16x4_f64; each wave owns a 64x64 quadrant = 4x4
 // blocks.  The product is formed as C^T = B^T A^T so that the accumulator's lane index runs
 // along C's rows (column-major C stays coalesced): lane l of block (bi,bj) holds
 // C[row = 16 bi + (l & 15)][col = 16 bj + (l >> 4) + 4 r], r = 0..3.
-// ------------------------------------------------------------------------------------
+#define HBM_ 128
+#define HBK_ 16
+#define HLDB_ (HBM_ + 2)
 // Guard-free operand and C traffic on interior tiles (m, n in range), K guards only in the
 // last, partial slice (FULL = false: every access guarded).  +1-4 % over the guarded form
 // (k = 384 trailing shapes 48.4 -> 50.1 TFLOP/s, tools/gemm_bench).
@@ -574,32 +459,9 @@ __device__ __forceinline__ void gemm128_mfma_body(const GemmTask& t, int m0, int
 }
 
 
-// ------------------------------------------------------------------------------------
-// MFMA tile v2 (tile code 130; the default Schur-update kernel): the same 128 x 128 output tile
-// per 256-thread workgroup, each wave a 64 x 64 quadrant of 4 x 4 v_mfma_f64_16x16x4_f64 blocks,
-// the same per-element accumulation order (k ascending, one MFMA-FMA per k: bitwise identical to
-// gemm128_mfma_body and the VALU tiles), but half the memory instructions of v1:
-//  * 16-byte global loads: A as row pairs (m contiguous), B as k pairs (k contiguous);
-//  * A staged [k][128] in LDS with 16-byte stores; MFMA block rows are interleaved so that one
-//    conflict-free ds_read_b128 feeds two blocks: block i, lane row li holds tile row
-//    wr + 32 (i >> 1) + 2 li + (i & 1);
-//  * B staged [col][k] with k padded to 17 doubles: conflict-free b64 (and merged read2_b64) reads;
-//  * C read and written as row pairs (16-byte accesses, 256 contiguous bytes per 16 lanes);
-//  * the LDS fragments of the next k-quad are read while the current quad's 16 MFMAs run, and
-//    the next K slice's global loads are in flight across the whole slice.
-// Interior tiles only (m, n in range); edge tiles take gemm128_mfma_body<.., false>.
-// ------------------------------------------------------------------------------------
-#define B2LD 17   // odd: conflict-free ds_read_b64 and the compiler's merged ds_read2_b64 (k, k+4) pairs
-#ifndef MFMA2_NOEDGE
-#define MFMA2_NOEDGE 0
-#endif
+// Pair types and global accessors of the v3 tile.
 typedef double v2du __attribute__((ext_vector_type(2), aligned(8)));   // 8-byte aligned pairs (global)
 typedef double v2d __attribute__((ext_vector_type(2)));                 // 16-byte aligned pairs (LDS)
-struct Mfma2Lds {
-  double A[2][HBK_][HBM_];    // [buf][k][row]
-  double B[2][HBM_][B2LD];    // [buf][col][k], negated
-};
-
 // Global accesses: wave-uniform 64-bit base (SGPRs, recomputed by scalar ALU where used) + a
 // per-lane 32-bit byte offset fixed for the whole tile, so no 64-bit per-lane address is live
 // across the K loop (the v1 interior spilled its precomputed C addresses).
@@ -608,143 +470,6 @@ __device__ __forceinline__ v2d ldu2(const char* ubase, uint32_t off) {
 }
 __device__ __forceinline__ void stu2(char* ubase, uint32_t off, v2d v) {
   *(__attribute__((address_space(1))) v2du*)(ubase + off) = v;
-}
-
-template <bool TRSM>
-__device__ __forceinline__ void gemm128_mfma2_interior(const GemmTask& t, int m0, int n0, Mfma2Lds& S,
-                                                       const GrowthArgs& ga) {
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = (wv & 1) * 64, wc = (wv >> 1) * 64;
-  const int li = lane & 15, lk = lane >> 4;
-  const int K = t.k;
-  const int64_t lda = t.lda, ldb = t.ldb, ldc = t.ldc;
-  // C <-> accumulators as row pairs: blocks 2ip and 2ip+1 hold rows 2li and 2li+1 of a 32-row strip
-  const uint32_t c_lo = (uint32_t)(((int64_t)lk * ldc + 2 * li) * 8);
-  auto cbase = [&](int ip, int j, int r) {
-    return reinterpret_cast<char*>(t.C) + ((int64_t)(n0 + wc + 16 * j + 4 * r) * ldc + m0 + wr + 32 * ip) * 8;
-  };
-  v4d acc[4][4];
-#pragma unroll
-  for (int ip = 0; ip < 2; ++ip)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const v2d c = ldu2(cbase(ip, j, r), c_lo);
-        acc[2 * ip][j][r] = c.x;
-        acc[2 * ip + 1][j][r] = c.y;
-      }
-  // staging of one K slice: A row pair 2*lane at k = wv + 4q (16-byte loads along m);
-  // B k pair 2*(lane & 7) of column 8 wv + (lane >> 3) + 32 q (16-byte loads along k)
-  const uint32_t a_lo = (uint32_t)(lane * 16);
-  const uint32_t b_lo = (uint32_t)((((int64_t)(lane >> 3)) * ldb + 2 * (lane & 7)) * 8);
-  const int b_k = 2 * (lane & 7);
-  auto abase = [&](int k0, int q) {
-    return reinterpret_cast<const char*>(t.A) + ((int64_t)(k0 + wv + 4 * q) * lda + m0) * 8;
-  };
-  auto bbase = [&](int k0, int q) {
-    return reinterpret_cast<const char*>(t.B) + ((int64_t)(n0 + 8 * wv + 32 * q) * ldb + k0) * 8;
-  };
-  v2d ra[4], rb[4];
-  auto gload_full = [&](int k0) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      ra[q] = ldu2(abase(k0, q), a_lo);
-      rb[q] = ldu2(bbase(k0, q), b_lo);
-    }
-  };
-  auto gload_tail = [&](int k0) {   // partial slice: k >= K reads as zero
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      ra[q] = k0 + wv + 4 * q < K ? ldu2(abase(k0, q), a_lo) : v2d{0.0, 0.0};
-      if (k0 + b_k + 1 < K) {
-        rb[q] = ldu2(bbase(k0, q), b_lo);
-      } else {
-        rb[q].x = k0 + b_k < K ? *(const gdbl*)(bbase(k0, q) + b_lo) : 0.0;
-        rb[q].y = 0.0;
-      }
-    }
-  };
-  auto sstore = [&](int buf) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      *reinterpret_cast<v2d*>(&S.A[buf][wv + 4 * q][2 * lane]) = ra[q];
-      double* bd = &S.B[buf][8 * wv + (lane >> 3) + 32 * q][b_k];   // 8-byte aligned (odd row stride)
-      bd[0] = -rb[q].x;
-      bd[1] = -rb[q].y;
-    }
-  };
-  auto slice = [&](int cur) {
-#pragma unroll
-    for (int kq = 0; kq < HBK_ / 4; ++kq) {
-      const int k = 4 * kq + lk;
-      v2d fa[2];
-      double fb[4];
-#pragma unroll
-      for (int ip = 0; ip < 2; ++ip) fa[ip] = *reinterpret_cast<const v2d*>(&S.A[cur][k][wr + 32 * ip + 2 * li]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = S.B[cur][wc + 16 * j + li][k];
-#pragma unroll
-      for (int ip = 0; ip < 2; ++ip)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc[2 * ip][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[j], fa[ip].x, acc[2 * ip][j], 0, 0, 0);
-          acc[2 * ip + 1][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(fb[j], fa[ip].y, acc[2 * ip + 1][j], 0, 0, 0);
-        }
-    }
-  };
-  const int nk = (K + HBK_ - 1) / HBK_;
-  const int nfull = K / HBK_;
-  if (nfull > 0) gload_full(0);
-  else gload_tail(0);
-  sstore(0);
-  __syncthreads();
-  int kt = 0;
-  for (; kt + 1 < nfull; ++kt) {   // next slice complete: guard-free loads in flight
-    gload_full((kt + 1) * HBK_);
-    slice(kt & 1);
-    sstore((kt & 1) ^ 1);
-    __syncthreads();
-  }
-  if (kt + 1 < nk) {                // next slice partial
-    gload_tail((kt + 1) * HBK_);
-    slice(kt & 1);
-    sstore((kt & 1) ^ 1);
-    __syncthreads();
-    ++kt;
-  }
-  slice(kt & 1);                    // last slice
-  double gmax = 0.0;
-#pragma unroll
-  for (int ip = 0; ip < 2; ++ip)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const v2d c = v2d{acc[2 * ip][j][r], acc[2 * ip + 1][j][r]};
-        stu2(cbase(ip, j, r), c_lo, c);
-        if (TRSM) gmax = fmax(gmax, fmax(fabs(c.x), fabs(c.y)));
-      }
-  if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
-}
-
-template <bool TRSM>
-__global__ __launch_bounds__(256, 2) void k_gemm128_mfma2(const GemmTask* __restrict__ tasks, int ntask,
-                                                          GrowthArgs ga) {
-  __shared__ __attribute__((aligned(16))) double lds[sizeof(Mfma2Lds) / sizeof(double)];
-  const int64_t b = xcd_window_remap(blockIdx.x, gridDim.x);
-  const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
-  int tm, tn;
-  tile_rc<HBM_>(t, b - t.tile0, tm, tn);
-  const int m0 = tm * HBM_, n0 = tn * HBM_;
-  if (m0 + HBM_ <= t.m && n0 + HBM_ <= t.n) {
-    gemm128_mfma2_interior<TRSM>(t, m0, n0, *reinterpret_cast<Mfma2Lds*>(lds), ga);
-  } else if (!MFMA2_NOEDGE) {
-    auto& As = *reinterpret_cast<double(*)[2][HBK_][HBM_]>(lds);
-    auto& Bs = *reinterpret_cast<double(*)[2][HBK_][HLDB_]>(lds + 2 * HBK_ * HBM_);
-    gemm128_mfma_body<TRSM, false>(t, m0, n0, As, Bs, ga);
-  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -1176,11 +901,6 @@ hipError_t launch_gemm_g(hipStream_t st, int64_t ntiles, const GemmTask* tasks, 
   else if (tile == 135) k_gemm128_mfma3<false, true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 131 && trsm) k_gemm128_mfma3<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 131) k_gemm128_mfma3<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 130 && trsm) k_gemm128_mfma2<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 130) k_gemm128_mfma2<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 128)   // VALU 128 tile (SMLU_VALU_GEMM only; never used for the TRSM form)
-    k_gemm128<<<(unsigned)(maxwg > 0 ? std::min<int64_t>(ntiles, maxwg) : ntiles), 256, 0, st>>>(
-        tasks, ntask, ntiles);
   else if (tile == 65 && trsm) k_gemm_k64<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 65) k_gemm_k64<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 66 && trsm) k_gemm64_mfma<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);

@@ -5,6 +5,26 @@
 // ---------------------------------------------------------------------------------------
 // Schedule construction (host, once per plan)
 // ---------------------------------------------------------------------------------------
+// Staging of the communication steps: device send / receive staging (largest step) and the
+// pinned host staging of a host-memory transport (every peer's message side by side).
+static void stage_sizes(const smlu_handle* h, int64_t& ss, int64_t& rs, int64_t& hs, int64_t& hr) {
+  ss = rs = hs = hr = 0;
+  for (const CommOp& op : h->comm) {
+    int64_t a = 0, b = 0, sa = 0, sb = 0;
+    for (size_t i = 0; i < op.peer.size(); ++i) {
+      if (op.sbase[i] == 4) a = std::max(a, op.soff[i] + op.sbytes[i]);
+      if (op.rbase[i] == 5) b = std::max(b, op.roff[i] + op.rbytes[i]);
+      sa += op.sbytes[i];
+      sb += op.rbytes[i];
+    }
+    if (op.type == 1 && op.bbase == 4) a = std::max(a, op.bytes);
+    ss = std::max(ss, a);
+    rs = std::max(rs, b);
+    hs = std::max(hs, std::max(sa, op.type == 1 ? op.bytes : 0));
+    hr = std::max(hr, std::max(sb, op.type == 1 ? op.bytes : 0));
+  }
+}
+
 static int build_schedule(smlu_handle* h) {
   Plan& P = h->plan;
   const Tune tn = tune();
@@ -19,14 +39,15 @@ static int build_schedule(smlu_handle* h) {
   int64_t voff = 0;
   // Largest ns factored with full-candidate pivoting.  A diagonally dominant matrix needs no
   // row exchanges (partial pivoting keeps the diagonal and the Schur complements stay
-  // dominant), so there the mid-size fronts take the faster diagonal-tile path too; its growth
-  // check still flags weak pivots if a refactor's new values lose dominance (refinement then
-  // runs in the solves).  SMLU_FULLPIV_NS overrides (dev).
+  // dominant), so there every blocked front takes the faster diagonal-tile path (round 6: the
+  // mid-size fronts too -- C2 refactor 5.42 -> 3.51 ms, 128^3 465 -> 461 ms); its growth check
+  // still flags weak pivots if a refactor's new values lose dominance (the re-pivoting refactor
+  // then runs).  SMLU_FULLPIV_NS overrides (dev).
   // a complex handle's pair-preserving pivots search every fully-summed row (mode 1): the
   // diagonal-tile panels have no pair rule
   const int64_t full_piv_ns = (h->pivmode == 1 || h->cpair) ? std::numeric_limits<int64_t>::max()
                               : tn.fullpiv_ns >= 0 ? tn.fullpiv_ns
-                              : h->dominant ? (int64_t)kSmallM : (int64_t)kFullPivNs;
+                              : h->dominant ? (int64_t)0 : (int64_t)kFullPivNs;
   for (int64_t s = 0; s < nsup; ++s) {
     SNode r{};
     r.first = P.s_first[s];
@@ -175,7 +196,7 @@ static int build_schedule(smlu_handle* h) {
     // 64 x 64 tile: the 128 tile would take its generic edge body for the 64-wide strips
     // (round 5: TRSM 23.0 -> 21.3 ms per 128^3 refactor)
     int tile = t128 >= h->t128_min && !(kind == K_TRSML && h->small_k) ? 128 : 64;
-    if (tile == 128 && h->opts.use_mfma) tile = mfma_tile;   // fp64 MFMA variant of the 128 tile
+    if (tile == 128) tile = h->opts.use_mfma ? mfma_tile : 64;   // use_mfma = 0: the VALU 64 tile
     if (tile == 131 && step < 0) tile = 135;
     if (tile == 64 && h->small_k) {                    // every k <= 64: one-shot K staging
       int kmax = 0;
@@ -376,8 +397,31 @@ static int build_schedule(smlu_handle* h) {
         }
         L.cnt = ((int64_t)ilist.size() - L.off) / 3;
         L.aux = Mmax;
-        L.aux2 = l + 1;   // overlap group: the size classes of one level are independent
+        // overlap group: the size classes of one level run on two streams (factor.cpp).  That is
+        // race-free only because the scratch plan (plan.cpp: one F22 block per level, live until
+        // the parents' level) keeps every F22 a front of this level writes disjoint from every
+        // other one and from the children's F22 the level reads -- checked below
+        L.aux2 = l + 1;
         if (L.cnt > 0) h->fac.push_back(L);
+      }
+      std::vector<std::pair<int64_t, int64_t>> wr, rd;   // F22 ranges written / read by the level
+      for (int64_t k = LP[l]; k < LP[l + 1]; ++k) {
+        const int64_t s = LS[k];
+        if (h->hsn[s].mode != 0) continue;
+        const int64_t nu = P.nu(s);
+        if (nu > 0 && h->hsn[s].Foff >= 0) wr.push_back({h->hsn[s].Foff, h->hsn[s].Foff + nu * nu});
+        for (int64_t e = P.ch_ptr[s]; e < P.ch_ptr[s + 1]; ++e) {
+          const int64_t c = P.ch_list[e], nuc = P.nu(c);
+          if (nuc > 0 && h->hsn[c].Foff >= 0) rd.push_back({h->hsn[c].Foff, h->hsn[c].Foff + nuc * nuc});
+        }
+      }
+      std::sort(wr.begin(), wr.end());
+      for (size_t i = 1; i < wr.size(); ++i)
+        if (wr[i].first < wr[i - 1].second) return fail(h, SMLU_ERR_STATE, "internal: overlapping F22 blocks in one level");
+      for (const auto& r : rd) {   // a read range must not meet any written range
+        auto it = std::upper_bound(wr.begin(), wr.end(), std::make_pair(r.second, (int64_t)-1));
+        if (it != wr.begin() && std::prev(it)->second > r.first)
+          return fail(h, SMLU_ERR_STATE, "internal: a level's F22 block overlaps a child's F22 it reads");
       }
     }
     // blocked fronts
@@ -1403,10 +1447,12 @@ static int build_schedule(smlu_handle* h) {
 
   h->nlaunch = (int64_t)h->fac.size();
   // upload
-  HIPCHK(h->sn.upload(h->hsn.data(), h->hsn.size(), st));
-  HIPCHK(h->ilist.upload(ilist.data(), ilist.size(), st));
-  HIPCHK(h->xtasks.upload(xt.data(), xt.size(), st));
-  HIPCHK(h->aents.upload(ae.data(), ae.size(), st));
+  if (!h->host_only) {
+    HIPCHK(h->sn.upload(h->hsn.data(), h->hsn.size(), st));
+    HIPCHK(h->ilist.upload(ilist.data(), ilist.size(), st));
+    HIPCHK(h->xtasks.upload(xt.data(), xt.size(), st));
+    HIPCHK(h->aents.upload(ae.data(), ae.size(), st));
+  }
   // batched right-hand sides (one GPU): the sweep's single chain wave per block would run the NR
   // chains one after another, so batches keep the per-64-column-block launches (k_tri_block: the
   // diagonal block solved by four chain waves for four right-hand sides at a time).  The same
@@ -1454,12 +1500,31 @@ static int build_schedule(smlu_handle* h) {
     expand_all(h->fwd, h->fwd_seg, false, h->fwdm, h->fwdm_seg);
     expand_all(h->bwd, h->bwd_seg, true, h->bwdm, h->bwdm_seg);
   }
+  if (h->nranks > 1) max_list = std::max<int64_t>(max_list, dist_slots);
+  h->ssync_n = ssync_n;
+  if (h->host_only) {   // smlu_plan_rank_schedule: the schedule without a device
+    int64_t ss, rs, hs, hr;
+    stage_sizes(h, ss, rs, hs, hr);
+    int64_t nseg = 0;
+    for (const CommOp& op : h->comm) nseg += (int64_t)(op.pack.size() + op.unpack.size());
+    h->host_bytes[3] += 8.0 * ((ss + 7) / 8 + 1) + 8.0 * ((rs + 7) / 8 + 1);   // device staging
+    h->host_bytes[0] += h->host_bytes[3];
+    h->host_bytes[0] += sizeof(SNode) * (double)h->hsn.size() + 4.0 * ilist.size() + sizeof(XContrib) * (double)xt.size() +
+                        sizeof(int2) * (double)ae.size() + sizeof(FrontTile) * (double)ft.size() +
+                        4.0 * (gptr.size() + gent.size()) + 4.0 * ssync_n + 8.0 * ntick +
+                        8.0 * 64 * kMultiRhs * ssync_n + 4.0 +
+                        ((!tinv_patch.empty() || h->nranks > 1) ? 8.0 * 8192 * max_list : 0.0) +
+                        sizeof(GemmTask) * (double)gt.size() + sizeof(SwapTask) * (double)st_tasks.size() +
+                        sizeof(URowTask) * (double)ur_tasks.size() + sizeof(XCol) * (double)xc.size() +
+                        4.0 * kSwapStride * max_list + 8.0 * std::max<int64_t>(voff, 1) + sizeof(SegDesc) * (double)nseg;
+    h->host_bytes[4] = (double)hs + (double)hr;   // pinned host staging of a host-memory transport
+    return SMLU_OK;
+  }
   HIPCHK(h->ftiles.upload(ft.data(), ft.size(), st));
   if (!gptr.empty()) {
     HIPCHK(h->gptr.upload(gptr.data(), gptr.size(), st));
     HIPCHK(h->gent.upload(gent.data(), gent.size(), st));
   }
-  h->ssync_n = ssync_n;
   if (ssync_n > 0) {   // zeroed once per schedule: the sweeps never reset them (epochs, kernels_solve.hip)
     HIPCHK(h->ssync.alloc((size_t)ssync_n));
     HIPCHK(h->stick.alloc((size_t)ntick));
@@ -1479,7 +1544,6 @@ static int build_schedule(smlu_handle* h) {
     HIPCHK(hipMemsetAsync(h->sstatus.p, 0, sizeof(int32_t), st));
   }
   h->sweep_spin = tn.sweep_spin;
-  if (h->nranks > 1) max_list = std::max<int64_t>(max_list, dist_slots);
   if (!tinv_patch.empty() || h->nranks > 1) {   // operands in the tile-inverse slots: patch in the buffer address
     HIPCHK(h->tinv.alloc((size_t)max_list * 8192));
     for (auto& pt : tinv_patch) {
@@ -1496,21 +1560,8 @@ static int build_schedule(smlu_handle* h) {
   HIPCHK(h->vbuf.alloc((size_t)std::max<int64_t>(voff, 1)));
   // communication steps: staging sizes, then every pack / unpack copy as a device descriptor
   if (!h->comm.empty()) {
-    int64_t ss = 0, rs = 0, hs = 0, hr = 0;
-    for (const CommOp& op : h->comm) {
-      int64_t a = 0, b = 0, sa = 0, sb = 0;
-      for (size_t i = 0; i < op.peer.size(); ++i) {
-        if (op.sbase[i] == 4) a = std::max(a, op.soff[i] + op.sbytes[i]);
-        if (op.rbase[i] == 5) b = std::max(b, op.roff[i] + op.rbytes[i]);
-        sa += op.sbytes[i];   // host staging lays every peer's message side by side
-        sb += op.rbytes[i];
-      }
-      if (op.type == 1 && op.bbase == 4) a = std::max(a, op.bytes);
-      ss = std::max(ss, a);
-      rs = std::max(rs, b);
-      hs = std::max(hs, std::max(sa, op.type == 1 ? op.bytes : 0));
-      hr = std::max(hr, std::max(sb, op.type == 1 ? op.bytes : 0));
-    }
+    int64_t ss, rs, hs, hr;
+    stage_sizes(h, ss, rs, hs, hr);
     h->stage_bytes_s = ss;
     h->stage_bytes_r = rs;
     HIPCHK(h->stage_s.alloc((size_t)(ss + 7) / 8 + 1));
@@ -1538,19 +1589,10 @@ static int build_schedule(smlu_handle* h) {
   return SMLU_OK;
 }
 
-int setup_device(smlu_handle* h) {
-  Plan& P = h->plan;
-  HIPCHK(hipSetDevice(h->device));
-  // one high-priority stream per handle (the schedule is one stream-ordered sequence)
-  int prio_lo = 0, prio_hi = 0;
-  HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-  if (!h->stream) HIPCHK(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi));
-  if (!h->side) HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_hi));
-  if (!h->fork_ev) HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
-  if (!h->join_ev) HIPCHK(hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
-  hipStream_t st = h->stream;
-  // this rank's layout: the plan's own on one GPU; ordinary fronts + owned column blocks of
-  // the shared fronts on a partitioned handle
+// This rank's layout: the plan's own on one GPU; ordinary fronts + owned column blocks of the
+// shared fronts on a partitioned handle.
+static void rank_layout_of(smlu_handle* h) {
+  const Plan& P = h->plan;
   if (h->nranks > 1) {
     rank_layout(P, h->rank, h->lay);
   } else {
@@ -1564,19 +1606,72 @@ int setup_device(smlu_handle* h) {
     Y.store_size = P.factor_size;
     Y.scratch_size = P.scratch_size;
   }
-  HIPCHK(h->A.alloc((size_t)std::max<int64_t>(P.nnzA, 1)));
-  HIPCHK(h->Rs.alloc((size_t)P.n));
+}
+
+// Element counts of the large per-handle buffers (doubles).
+struct Sizes {
+  int64_t store, scratch, bcbuf;
+};
+static Sizes sizes_of(const smlu_handle* h) {
+  const Plan& P = h->plan;
+  Sizes z{};
   // k_urows reads up to 64 columns and 16 rows past a block (values discarded): pad the store
   int64_t maxM = 1;
   for (int64_t s = 0; s < P.nsup; ++s) maxM = std::max<int64_t>(maxM, P.M(s));
-  HIPCHK(h->store.alloc((size_t)(std::max<int64_t>(h->lay.store_size, 1) + 64 * maxM + 4096)));
-  HIPCHK(h->scratch.alloc((size_t)std::max<int64_t>(h->lay.scratch_size, 1)));
+  z.store = std::max<int64_t>(h->lay.store_size, 1) + 64 * maxM + 4096;
+  z.scratch = std::max<int64_t>(h->lay.scratch_size, 1);
+  z.bcbuf = 0;
   if (h->nranks > 1) {   // received pivot block + tile inverses + swap lists + rowperm
-    int64_t bc = 1;
+    z.bcbuf = 1;
     for (int64_t s = 0; s < P.nsup; ++s)
       if (P.dist(s) && std::binary_search(P.group[s].begin(), P.group[s].end(), h->rank))
-        bc = std::max<int64_t>(bc, P.M(s) * P.dob + (P.dob / 64) * 8192 + (P.dob / 64) * kSwapStride / 2 + P.dob / 2 + 64);
-    HIPCHK(h->bcbuf.alloc((size_t)bc));
+        z.bcbuf = std::max<int64_t>(z.bcbuf, P.M(s) * P.dob + (P.dob / 64) * 8192 + (P.dob / 64) * kSwapStride / 2 + P.dob / 2 + 64);
+  }
+  return z;
+}
+
+// Host-only build of a rank's schedule (smlu_plan_rank_schedule): the launch sequences and the
+// communication steps exactly as setup_device builds them, no device and no stream.  host_bytes:
+// [0] device bytes the handle would allocate, [1] factor store, [2] front scratch, [3] staging +
+// received-block buffer, [4] pinned host staging (host-memory transports).
+int build_schedule_host(smlu_handle* h) {
+  const Plan& P = h->plan;
+  h->host_only = true;
+  rank_layout_of(h);
+  const Sizes z = sizes_of(h);
+  const double n = (double)P.n, nnzA = (double)P.nnzA;
+  for (double& b : h->host_bytes) b = 0;
+  h->host_bytes[1] = 8.0 * z.store;
+  h->host_bytes[2] = 8.0 * z.scratch;
+  h->host_bytes[3] = 8.0 * z.bcbuf + (h->nranks > 1 ? 64.0 : 0.0);
+  h->nnodes = P.nsup + (int64_t)h->lay.blocks.size();
+  // A, Rs, wrk, wrk2, growth, Arowptr, Arow_ent, Arow, p0, q, rows, relmap, chlist, posfirst,
+  // rowperm, rowperm0, info, status record
+  h->host_bytes[0] = h->host_bytes[1] + h->host_bytes[2] + 8.0 * nnzA + 8.0 * n * 3 + 8.0 + 8.0 * (n + 1) +
+                     4.0 * nnzA * 2 + 8.0 * n * 3 + 4.0 * (double)(P.s_rows.size() + P.relmap.size() + P.ch_list.size()) +
+                     4.0 * n * 2 + 4.0 * (double)h->nnodes + 8.0 * (16 + 5 * 512);
+  return build_schedule(h);
+}
+
+int setup_device(smlu_handle* h) {
+  Plan& P = h->plan;
+  HIPCHK(hipSetDevice(h->device));
+  // one high-priority stream per handle (the schedule is one stream-ordered sequence)
+  int prio_lo = 0, prio_hi = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  if (!h->stream) HIPCHK(hipStreamCreateWithPriority(&h->stream, hipStreamNonBlocking, prio_hi));
+  if (!h->side) HIPCHK(hipStreamCreateWithPriority(&h->side, hipStreamNonBlocking, prio_hi));
+  if (!h->fork_ev) HIPCHK(hipEventCreateWithFlags(&h->fork_ev, hipEventDisableTiming));
+  if (!h->join_ev) HIPCHK(hipEventCreateWithFlags(&h->join_ev, hipEventDisableTiming));
+  hipStream_t st = h->stream;
+  rank_layout_of(h);
+  const Sizes z = sizes_of(h);
+  HIPCHK(h->A.alloc((size_t)std::max<int64_t>(P.nnzA, 1)));
+  HIPCHK(h->Rs.alloc((size_t)P.n));
+  HIPCHK(h->store.alloc((size_t)z.store));
+  HIPCHK(h->scratch.alloc((size_t)z.scratch));
+  if (h->nranks > 1) {
+    HIPCHK(h->bcbuf.alloc((size_t)z.bcbuf));
     HIPCHK(h->d_red.alloc(8));
   }
   HIPCHK(h->wrk.alloc((size_t)P.n));

@@ -255,10 +255,9 @@ double smlu_stat(const smlu_handle* h, const char* key) {
     for (const Launch& L : h->fac) {
       const bool gemm = L.kind == K_GEMM || L.kind == K_GEMMU || L.kind == K_GEMMO || L.kind == K_GEMM22;
       const bool trsm = L.kind == K_TRSML;
-      const bool mfma = L.aux == 130 || L.aux == 131 || L.aux == 135;
+      const bool mfma = L.aux == 131 || L.aux == 135;
       if (v == "mfma128" && gemm && mfma) ++c;
       else if (v == "mfma128_trsm" && trsm && mfma) ++c;
-      else if (v == "valu128" && gemm && L.aux == 128) ++c;
       else if (v == "k64" && gemm && L.aux == 65) ++c;
       else if (v == "k64_trsm" && trsm && L.aux == 65) ++c;
       else if (v == "valu64" && gemm && L.aux == 64) ++c;

@@ -104,6 +104,7 @@ SIGNATURES = {
     "smlu_plan_partition": (i32, [vp, i32, vp, i64p]),
     "smlu_plan_rank_memory": (i32, [vp, i32, i32, f64p, f64p, f64p]),
     "smlu_plan_project": (f64, [vp, i32, f64, f64, f64, f64p]),
+    "smlu_plan_rank_schedule": (i32, [vp, i32, i32, vp, i64, i64p, vp, vp]),
 }
 
 _lib = None

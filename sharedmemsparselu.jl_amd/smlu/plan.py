@@ -91,6 +91,41 @@ class Plan:
             raise RuntimeError(f"smlu_plan_rank_memory failed ({rc}): {C.last_error(None)}")
         return a.value, b.value, c.value
 
+    def rank_schedule(self, nparts, rank):
+        """Rank `rank`'s schedule of an `nparts`-rank handle built on the host (no device,
+        smlu_plan_rank_schedule): its communication steps in execution order as dicts
+        {seq: 'fac' | 'fwd' | 'bwd', type: 'exchange' | 'bcast', root, bytes, peers: [(peer, sbytes,
+        rbytes)] or group: [ranks]}, and {device_bytes, store_bytes, scratch_bytes, staging_bytes,
+        host_staging_bytes, launches, shared_fronts, owned_blocks}."""
+        L = C.lib()
+        n = ctypes.c_int64()
+        by = np.zeros(5)
+        cn = np.zeros(3, np.int64)
+        rc = L.smlu_plan_rank_schedule(self._h, int(nparts), int(rank), None, 0, ctypes.byref(n), C.ptr(by), C.ptr(cn))
+        if rc != 0:
+            raise RuntimeError(f"smlu_plan_rank_schedule failed ({rc}): {C.last_error(None)}")
+        ops = np.empty(max(n.value, 1), np.int64)
+        rc = L.smlu_plan_rank_schedule(self._h, int(nparts), int(rank), C.ptr(ops), n.value, ctypes.byref(n), None, None)
+        if rc != 0:
+            raise RuntimeError(f"smlu_plan_rank_schedule failed ({rc}): {C.last_error(None)}")
+        steps, k, seqs = [], 0, ("fac", "fwd", "bwd")
+        while k < n.value:
+            q, typ, root, nbytes, cnt = (int(v) for v in ops[k:k + 5])
+            k += 5
+            if typ == 1:
+                steps.append({"seq": seqs[q], "type": "bcast", "root": root, "bytes": nbytes,
+                              "group": [int(v) for v in ops[k:k + cnt]]})
+                k += cnt
+            else:
+                trip = ops[k:k + 3 * cnt].reshape(cnt, 3)
+                steps.append({"seq": seqs[q], "type": "exchange",
+                              "peers": [(int(a), int(b), int(c)) for a, b, c in trip]})
+                k += 3 * cnt
+        info = {"device_bytes": by[0], "store_bytes": by[1], "scratch_bytes": by[2], "staging_bytes": by[3],
+                "host_staging_bytes": by[4], "launches": int(cn[0]), "shared_fronts": int(cn[1]),
+                "owned_blocks": int(cn[2])}
+        return steps, info
+
     def project(self, nparts, tflops=52.0, gbs=100.0, lat_us=20.0):
         """Projected partitioned factorization time (s) and the one-GPU time of the same model."""
         t1 = ctypes.c_double()

@@ -8,10 +8,10 @@
     mfma128  SMLU_T128MIN=1, SMLU_SMALLK=0    every GEMM launch on k_gemm128_mfma3, the GEMM-form
                                               TRSM included (by default it runs on k_gemm_k64)
     valu64   SMLU_T128MIN=2^60, SMLU_SMALLK=0 every GEMM launch on the VALU 64x64 tile k_gemm
-    valu128  SMLU_T128MIN=1, use_mfma=0       the VALU 128x128 tile k_gemm128
-    default  as shipped (k_gemm_k64 for k <= 64 launches, fused panels with tile inverses,
-             k_urows, 64x64 tiles below the MFMA threshold)
-  (round 5 removed the rocBLAS comparison variant together with the library's vendor GEMM path)
+    default  as shipped (k_gemm_k64 for k <= 64 launches, the MFMA 64x64 tile k_gemm64_mfma for
+             k > 64 launches below the 128-tile threshold, fused panels with tile inverses, k_urows)
+  (round 5 removed the rocBLAS comparison variant together with the library's vendor GEMM path;
+  round 6 removed the comparison-only VALU 128 and MFMA v2 tiles from the library)
 * Error paths of the reference surface: SingularException from lu(A) (src/SharedMemSparseLU.jl:74)
   and lu!(F, A) (:247), lu! with a changed pattern (the reallocate branch :252-273), the
   re-pivoting refactor (a zero or weak diagonal-tile pivot re-factors with full-candidate
@@ -33,7 +33,6 @@ VARIANTS = {
     "default": ({}, {}),
     "mfma128": ({"SMLU_T128MIN": "1", "SMLU_SMALLK": "0"}, {}),
     "valu64": ({"SMLU_T128MIN": str(1 << 60), "SMLU_SMALLK": "0"}, {}),
-    "valu128": ({"SMLU_T128MIN": "1"}, {"use_mfma": False}),
 }
 
 
@@ -54,8 +53,6 @@ def check_variant_ran(F, variant):
     elif variant == "valu64":
         assert F.stat("launches_valu64") > 0
         assert F.stat("launches_mfma128") == 0 and F.stat("launches_k64") == 0
-    elif variant == "valu128":
-        assert F.stat("launches_valu128") > 0 and F.stat("launches_mfma128") == 0
     assert F.stat("vendor_calls") == 0
 
 
@@ -88,23 +85,20 @@ def test_poisson3d_32_nd_oracle(gpu, monkeypatch, variant):
 
 
 def test_mfma_and_valu_tiles_bitwise(gpu, monkeypatch):
-    # the MFMA tiles (128 x 128 and the one-shot k <= 64 tile) accumulate each C element in the
-    # same k order as the VALU 64 tile, one rounding per multiply-add: the factors are bitwise
-    # identical.  (use_mfma=0 also swaps the
-    # GEMM-form triangular solves for k_step_trsm, so valu128 agrees to rounding only.)
+    # the MFMA tiles (128 x 128, the one-shot k <= 64 tile and the 64 x 64 tile for k > 64)
+    # accumulate each C element in the same k order as the VALU 64 tile, one rounding per
+    # multiply-add: the factors are bitwise identical
     A = mats.poisson3d(20)
     Fm = make(A, "mfma128", monkeypatch)
     Fv = make(A, "valu64", monkeypatch)
-    F2 = make(A, "valu128", monkeypatch)
     Fd = make(A, "default", monkeypatch)   # k <= 64 launches on the one-shot MFMA tile
     assert Fd.stat("launches_k64") > 0
+    assert Fd.stat("launches_mfma64") > 0  # k > 64 launches below the 128 threshold: k_gemm64_mfma
     assert np.array_equal(Fv.L.indices, Fm.L.indices)
     assert np.array_equal(Fv.L.data, Fm.L.data)
     assert np.array_equal(Fv.U.data, Fm.U.data)
     assert np.array_equal(Fv.L.data, Fd.L.data)
     assert np.array_equal(Fv.U.data, Fd.U.data)
-    assert abs(F2.L - Fm.L).max() <= 1e-13
-    assert abs(F2.U - Fm.U).max() <= 1e-13 * abs(Fm.U).max()
 
 
 def _dominant_dense(n, seed):

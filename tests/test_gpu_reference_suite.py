@@ -196,6 +196,29 @@ def test_given_pattern_with_dropped_fill(gpu):
     F.close()
 
 
+def test_given_pattern_cleared_by_pattern_change(gpu):
+    # lu!(F, A_new) with a new sparsity pattern re-analyses (src/SharedMemSparseLU.jl:252-273): the
+    # handed-over UMFPACK pattern and (p, q) belong to the old A, so the new factors must come back
+    # on their own structural fill, equal to the oracle's factorization of the new matrix
+    from _parity import factor_parity
+    z, n, A, L, U = _pattern_case()
+    F = smlu.ParallelSparseLU(A, p=z["p"], q=z["q"], L_pattern=L, U_pattern=U)
+    assert F.stat("given_pattern") == 1
+    A2 = A.tolil()
+    A2[0, n - 1] = -0.25          # one new off-diagonal pair: a different pattern and new fill
+    A2[n - 1, 0] = -0.25
+    A2 = sp.csc_matrix(A2)
+    A2.sort_indices()
+    smlu.lu_(F, A2)
+    assert F.stat("given_pattern") == 0 and F.stat("pattern_dropped") == 0
+    factor_parity(A2, F)
+    b = np.random.default_rng(9).random(n)
+    x = np.empty(n)
+    smlu.ldiv_(x, F, b)
+    assert np.abs(A2 @ x - b).max() <= 1e-12 * np.abs(b).max() * 10
+    F.close()
+
+
 @pytest.mark.parametrize("bad", ["outside_fill", "no_diagonal", "upper_in_L"])
 def test_given_pattern_rejected(gpu, bad):
     z, n, A, L, U = _pattern_case()
