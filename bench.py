@@ -175,6 +175,14 @@ def gpu_configs(dev):
     F2.solve_device(x, b)
     torch.cuda.synchronize()
     t_sol = time.perf_counter() - t0
+    hv = vals[2].cpu().numpy()   # lu! with host values (smlu_refactor), median of 5
+    th = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        F2.refactor(hv)
+        torch.cuda.synchronize()
+        th.append((time.perf_counter() - t0) * 1e3)
     R = 1000
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -187,7 +195,8 @@ def gpu_configs(dev):
     Al.data = vals[(R - 1) % 8].cpu().numpy()
     xh, bh = x.cpu().numpy(), b.cpu().numpy()
     nnz2 = F2.stat("nnzLU")
-    out["c2"] = {"create_s": c2_create, "refactor_ms": t_ref * 1e3, "solve_ms": t_sol * 1e3,
+    out["c2"] = {"create_s": c2_create, "refactor_ms": t_ref * 1e3, "refactor_host_values_ms": float(np.median(th)),
+                 "solve_ms": t_sol * 1e3,
                  "factorize_plus_solve_ms": (t_ref + t_sol) * 1e3, "nnzLU": nnz2,
                  "nnzLU_per_s": nnz2 / t_ref}
     out["c5_steady_state_c2"] = {"refactors": R, "seconds": t_ss, "ms_per_refactor": t_ss / R * 1e3,
@@ -430,6 +439,22 @@ def main():
     Al.data = vals[-1].cpu().numpy()
     xh, bh = x.cpu().numpy(), b.cpu().numpy()
     solve_residual = float(np.abs(Al @ xh - bh).max() / np.abs(bh).max())
+    # lu!(F, A) with HOST values (the Julia shim's smlu_refactor: pageable upload of the values, the
+    # dominance test on the device, the factorization) -- a side figure beside the resident-values
+    # metric (within 3 % of ms_per_step)
+    refactor_host_ms = None
+    if not partitioned:
+        hv = [vals[r % len(vals)].cpu().numpy() for r in range(2)]
+        F.refactor(hv[1])
+        th = []
+        for r in range(3):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            F.refactor(hv[r % 2])
+            torch.cuda.synchronize()
+            th.append((time.perf_counter() - t1) * 1e3)
+        refactor_host_ms = float(np.median(th))
+        log(f"refactor with host values: {th} ms")
     ms_per_step = dt / args.steps * 1e3
     # per-rank evidence of the partitioned run: the communicator's own rank count and what this rank
     # moved in its last refactor (gathered to rank 0 over the gloo control plane)
@@ -537,6 +562,7 @@ def main():
             # kernel, profiles/) over this run's time per refactor
             "achieved_hbm_GBs": (hbm_refactor / (ms_per_step * 1e-3) / 1e9) if hbm_refactor else None,
             "achieved_hbm_frac": (hbm_refactor / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS) if hbm_refactor else None,
+            "refactor_host_values_ms": refactor_host_ms,
             "solve_ms": solve_ms,
             "solve_8rhs_ms": solve8_ms,
             "solve_residual": solve_residual,

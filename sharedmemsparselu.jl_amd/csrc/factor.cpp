@@ -180,8 +180,12 @@ int read_status(smlu_handle* h, const int32_t* info, int64_t nnodes, const int32
 static int finish_factor(smlu_handle* h, Timer& tm, std::chrono::steady_clock::time_point t0) {
   Plan& P = h->plan;
   long long rec[16];
-  int rs = read_status(h, h->info.p, h->nnodes, reinterpret_cast<const int32_t*>(h->growth.p), 2, rec);
+  // words: the growth maximum (growth[0]) and the dominance flags of the values (growth[1], two
+  // int32: by columns, by rows; written by k_dominance ahead of the factorization when the
+  // pivoting mode is re-decided) -- one record, one synchronisation per factorization
+  int rs = read_status(h, h->info.p, h->nnodes, reinterpret_cast<const int32_t*>(h->growth.p), 4, rec);
   if (rs != SMLU_OK) return rs;
+  h->dom_words = rec[7];
   if (rec[10] > 0) {   // an info word no factor kernel writes: never read as a pivot status
     h->bad_info_node = rec[8];
     h->bad_info_word = (int32_t)rec[9];
@@ -238,9 +242,32 @@ static int run_factor_once(smlu_handle* h) {
   return finish_factor(h, tm, t0);
 }
 
-int run_factor(smlu_handle* h) {
+static int apply_dominance(smlu_handle* h, bool dom, bool* rebuilt);
+static int launch_device_dominance(smlu_handle* h);
+
+// One factorization of the values in h->A with the re-pivoting fallback.  redecide: the pivoting
+// mode is re-decided for these values without a synchronisation of its own:
+// k_dominance runs ahead of the factorization, which goes on in the current mode, and its flags
+// come back in the factorization's status record; only when they call for another mode (rare:
+// the values changed between dominant and non-dominant, or a re-pivoted handle sees dominant
+// values again) is the schedule rebuilt and the same values factored again in that mode.
+int run_factor(smlu_handle* h, bool redecide) {
+  if (redecide) {
+    int rc = launch_device_dominance(h);
+    if (rc != SMLU_OK) return rc;
+  }
   int rc = run_factor_once(h);
   if (rc < 0) return rc;
+  if (redecide) {
+    const bool dom = (h->dom_words & 0xffffffffll) != 0 || (h->dom_words >> 32) != 0;
+    bool rebuilt = false;
+    int r2 = apply_dominance(h, dom, &rebuilt);
+    if (r2 != SMLU_OK) return r2;
+    if (rebuilt) {
+      ++h->mode_refactors;
+      return run_factor(h, false);
+    }
+  }
   const bool off = tune().no_repivot;   // test knob
   if ((rc == SMLU_SINGULAR || h->weak > 0) && h->pivmode == 0 && !off && has_tile_fronts(h) &&
       h->opts.pivot_tol > 0 && !h->plan.given_order && h->nranks == 1) {
@@ -259,11 +286,12 @@ int run_factor(smlu_handle* h) {
 
 
 // Pivoting mode per refactor: dominant values take the diagonal-tile path for
-// the mid-size fronts; a handle left in full-candidate mode by a re-pivoting refactor returns to
+// every blocked front; a handle left in full-candidate mode by a re-pivoting refactor returns to
 // the fast schedule once the values are dominant again.  The ranks of a partitioned handle agree
 // on the decision (any rank seeing non-dominant values makes it non-dominant for all): a rebuild
 // on only some ranks would split the collective schedule.
-static int apply_dominance(smlu_handle* h, bool dom) {
+static int apply_dominance(smlu_handle* h, bool dom, bool* rebuilt) {
+  *rebuilt = false;
   if (h->nranks > 1) {
     double nd = dom ? 0.0 : 1.0;
     if (h->tr.allreduce_max(h->tr.ctx, &nd, 1) != 0) return fail(h, SMLU_ERR_HIP, "transport allreduce failed (dominance)");
@@ -278,51 +306,35 @@ static int apply_dominance(smlu_handle* h, bool dom) {
     h->pivmode = 0;
     changed = true;
   }
+  *rebuilt = changed;
   return changed ? rebuild_schedule(h) : SMLU_OK;
 }
 
-// The same dominance test on values already in HBM (k_dominance: one thread per column and row,
-// the host's summation order), for device-only callers.
-static int device_dominant(smlu_handle* h, bool* dom) {
+// The dominance test of the values in HBM (k_dominance: one thread per column and row, the host
+// diagonally_dominant()'s summation order), flags into growth[1] for finish_factor's record.
+static int launch_device_dominance(smlu_handle* h) {
   const Plan& P = h->plan;
   hipStream_t st = h->stream;
-  if (!h->Acolp.p) {
-    HIPCHK(h->Acolp.upload(P.Acolptr.data(), P.Acolptr.size(), st));
-    HIPCHK(h->domflag.alloc(2));
-  }
+  if (!h->Acolp.p) HIPCHK(h->Acolp.upload(P.Acolptr.data(), P.Acolptr.size(), st));
   int rc = ensure_residual(h);   // the column of every A entry
   if (rc != SMLU_OK) return rc;
   HIPCHK(launch_dominance(st, P.n, h->Acolp.p, h->Arow.p, h->Arowptr.p, h->Arow_ent.p, h->Acol.p, h->A.p,
-                          h->domflag.p));
-  long long rec[16];
-  rc = read_status(h, nullptr, 0, h->domflag.p, 2, rec);
-  if (rc != SMLU_OK) return rc;
-  *dom = (rec[6] & 0xffffffffll) != 0 || (rec[6] >> 32) != 0;
+                          reinterpret_cast<int32_t*>(h->growth.p + 1)));
   return SMLU_OK;
 }
 
-// lu! on the values already in h->A: the pivoting mode re-decided on the device, then the
-// factorization (with the re-pivoting fallback).
+// lu! on the values already in h->A: the factorization with the pivoting mode re-decided for
+// these values (above) and the re-pivoting fallback.
 int refactor_resident(smlu_handle* h) {
-  if (!h->plan.given_order && !h->plan.matched) {
-    bool dom = false;
-    int rc = device_dominant(h, &dom);
-    if (rc == SMLU_OK) rc = apply_dominance(h, dom);
-    if (rc != SMLU_OK) return rc;
-  }
-  return run_factor(h);
+  return run_factor(h, !h->plan.given_order && !h->plan.matched);
 }
 
 int smlu_refactor(smlu_handle* h, const double* nzval) {
   if (!h || !nzval) return fail(h, SMLU_ERR_ARG, "NULL argument");
   HIPCHK(hipSetDevice(h->device));
+  // the values' upload, then the device path (dominance on the device, no host scan of the values)
   HIPCHK(hipMemcpyAsync(h->A.p, nzval, sizeof(double) * h->plan.nnzA, hipMemcpyHostToDevice, h->stream));
-  if (!h->plan.given_order && !h->plan.matched) {   // pivoting mode per refactor: re-check dominance
-    const Plan& P = h->plan;
-    int rc = apply_dominance(h, diagonally_dominant(P.n, P.Acolptr.data(), P.Arow.data(), nzval, 0));
-    if (rc != SMLU_OK) return rc;
-  }
-  return run_factor(h);   // collective on a partitioned handle
+  return refactor_resident(h);   // collective on a partitioned handle
 }
 
 // Device entry points read caller memory (values, right-hand sides) on the handle's own stream:

@@ -246,7 +246,6 @@ struct smlu_handle {
   DBuf<double> ref_b, ref_r, ref_d, ref_nrm;   // iterative refinement (allocated on first use)
   DBuf<int32_t> Acol;                          // column of each A entry (residuals, dominance check)
   DBuf<int64_t> Acolp;                         // A's colptr (device dominance check)
-  DBuf<int32_t> domflag;
   int refine_steps = 0;
   double refine_berr = -1;   // componentwise backward error at the last refinement check
   double refine_resid = -1;
@@ -332,6 +331,8 @@ struct smlu_handle {
                               //    fronts; 1: full-candidate pivoting in every blocked front (the
                               //    re-pivoting refactor after a zero or weak tile pivot)
   int64_t repivots = 0;       // re-pivoting refactors run so far
+  int64_t mode_refactors = 0; // factorizations repeated because the values called for another pivoting mode
+  long long dom_words = 0;    // dominance flags (columns | rows << 32) in the last factorization's record
   int64_t flag_node = -1;     // first flagged node of the last factorization and its info word
   int32_t flag_info = 0;
   int64_t repivot_node = -1;  // what triggered the last re-pivot: the first flagged node, its info
@@ -360,7 +361,6 @@ struct smlu_handle {
     ch_version = -1;
     Acol.free();
     Acolp.free();
-    domflag.free();
     for (auto* b : d) b->free();
     DBuf<int64_t>* l[] = {&Arowptr, &p0, &q, &posfirst};
     for (auto* b : l) b->free();
@@ -534,7 +534,7 @@ int setup_device(smlu_handle* h);                        // schedule.cpp
 int build_schedule_host(smlu_handle* h);
 int rebuild_schedule(smlu_handle* h);
 bool has_tile_fronts(const smlu_handle* h);
-int run_factor(smlu_handle* h);                          // factor.cpp
+int run_factor(smlu_handle* h, bool redecide = false);   // factor.cpp
 int read_status(smlu_handle* h, const int32_t* info, int64_t nnodes, const int32_t* words, int nwords,
                 long long out[16]);
 hipError_t after_caller(smlu_handle* h);

@@ -991,6 +991,9 @@ __global__ __launch_bounds__(256) void k_residual(int64_t n, const int64_t* __re
 // diagonally_dominant(), for smlu_refactor_device): thread i sums |column i| in CSC order and
 // |row i| over its entries in column order (Arow_ent), the host's summation order, so both take
 // the same decision; flags[0] / flags[1] are cleared when some column / row is not dominant.
+__global__ void k_dom_init(int32_t* __restrict__ flags) {
+  if (threadIdx.x < 2) flags[threadIdx.x] = 1;
+}
 __global__ __launch_bounds__(256) void k_dominance(int64_t n, const int64_t* __restrict__ colptr,
                                                    const int32_t* __restrict__ arow,
                                                    const int64_t* __restrict__ rowptr,
@@ -1328,9 +1331,7 @@ hipError_t launch_residual(hipStream_t st, int64_t n, const int64_t* rowptr, con
 hipError_t launch_dominance(hipStream_t st, int64_t n, const int64_t* colptr, const int32_t* arow,
                             const int64_t* rowptr, const int32_t* ent, const int32_t* acol, const double* a,
                             int32_t* dflags) {
-  static const int32_t ones[2] = {1, 1};
-  hipError_t e = hipMemcpyAsync(dflags, ones, sizeof(ones), hipMemcpyHostToDevice, st);
-  if (e != hipSuccess) return e;
+  k_dom_init<<<1, 64, 0, st>>>(dflags);   // (a kernel: no pageable host-to-device copy)
   if (n > 0) k_dominance<<<nblk(n, 256), 256, 0, st>>>(n, colptr, arow, rowptr, ent, acol, a, dflags);
   return hipGetLastError();
 }

@@ -111,10 +111,15 @@ static int build_schedule(smlu_handle* h) {
     for (int64_t s = 0; s < nsup; ++s) fr_ptr[s + 1] += fr_ptr[s];
     std::vector<int64_t> fp(fr_ptr.begin(), fr_ptr.end() - 1);
     for (int64_t e = 0; e < P.nnzA; ++e) fr_ent[fp[P.A_s[e]]++] = (int32_t)e;
-    for (int64_t s = 0; s < nsup; ++s)
+    // (only the fronts this rank assembles: its own and the shared ones of its groups)
+    for (int64_t s = 0; s < nsup; ++s) {
+      if (h->nranks > 1 && !(P.dist(s) ? std::binary_search(P.group[s].begin(), P.group[s].end(), h->rank)
+                                       : P.owner[s] == h->rank))
+        continue;
       std::sort(fr_ent.begin() + fr_ptr[s], fr_ent.begin() + fr_ptr[s + 1], [&](int32_t a, int32_t b) {
         return P.A_lj[a] != P.A_lj[b] ? P.A_lj[a] < P.A_lj[b] : P.A_li[a] < P.A_li[b];
       });
+    }
   }
   double* store = h->store.p;
   double* scratch = h->scratch.p;
@@ -1676,7 +1681,7 @@ int setup_device(smlu_handle* h) {
   }
   HIPCHK(h->wrk.alloc((size_t)P.n));
   HIPCHK(h->wrk2.alloc((size_t)P.n));
-  HIPCHK(h->growth.alloc(1));
+  HIPCHK(h->growth.alloc(2));   // [0] growth maximum, [1] dominance flags (factor.cpp)
   HIPCHK(h->Arowptr.upload(P.Arowptr.data(), P.Arowptr.size(), st));
   HIPCHK(h->Arow_ent.upload(P.Arow_ent.data(), P.Arow_ent.size(), st));
   HIPCHK(h->Arow.upload(P.Arow.data(), P.Arow.size(), st));

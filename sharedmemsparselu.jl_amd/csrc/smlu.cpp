@@ -225,6 +225,7 @@ double smlu_stat(const smlu_handle* h, const char* key) {
     return c;
   }
   if (k == "repivots") return (double)h->repivots;
+  if (k == "mode_refactors") return (double)h->mode_refactors;
   if (k == "repivot_node") return (double)h->repivot_node;
   if (k == "repivot_info") return (double)h->repivot_info;
   if (k == "repivot_growth") return h->repivot_growth;

@@ -247,6 +247,18 @@ class ParallelSparseLU:
         _check(L.smlu_get_fronts(self._h, None, None, None, C.ptr(rows), C.ptr(p0), None), self._h)
         return dict(first=first, parent=parent, rowptr=rowptr, rows=rows, p0=p0, mode=mode)
 
+    def refactor(self, values):
+        """lu!(F, A) with host values in A's CSC order (same pattern): smlu_refactor, the call the
+        Julia shim makes (src/SharedMemSparseLU.jl:245-279)."""
+        v = np.ascontiguousarray(values, dtype=self._dt)
+        L = C.lib()
+        rc = _check((L.smlu_refactor_z if self.is_complex else L.smlu_refactor)(self._h, C.ptr(v)), self._h)
+        self._factors = None
+        self._zfactors = None
+        if rc == C.SMLU_SINGULAR:
+            raise SingularException(L.smlu_last_error_col(self._h))
+        return rc
+
     # ---- device-resident entry points (values / vectors already in HBM) ----
     def refactor_device(self, d_values):
         """lu! with values already on the device (torch tensor or raw pointer int; complex

@@ -101,13 +101,15 @@ class Plan:
         n = ctypes.c_int64()
         by = np.zeros(5)
         cn = np.zeros(3, np.int64)
-        rc = L.smlu_plan_rank_schedule(self._h, int(nparts), int(rank), None, 0, ctypes.byref(n), C.ptr(by), C.ptr(cn))
-        if rc != 0:
-            raise RuntimeError(f"smlu_plan_rank_schedule failed ({rc}): {C.last_error(None)}")
-        ops = np.empty(max(n.value, 1), np.int64)
-        rc = L.smlu_plan_rank_schedule(self._h, int(nparts), int(rank), C.ptr(ops), n.value, ctypes.byref(n), None, None)
-        if rc != 0:
-            raise RuntimeError(f"smlu_plan_rank_schedule failed ({rc}): {C.last_error(None)}")
+        ops = np.empty(1 << 20, np.int64)   # one build when the steps fit (256^3 / 8 ranks: ~2e4 words)
+        while True:
+            rc = L.smlu_plan_rank_schedule(self._h, int(nparts), int(rank), C.ptr(ops), ops.size, ctypes.byref(n),
+                                           C.ptr(by), C.ptr(cn))
+            if rc == 0:
+                break
+            if n.value <= ops.size:
+                raise RuntimeError(f"smlu_plan_rank_schedule failed ({rc}): {C.last_error(None)}")
+            ops = np.empty(n.value, np.int64)
         steps, k, seqs = [], 0, ("fac", "fwd", "bwd")
         while k < n.value:
             q, typ, root, nbytes, cnt = (int(v) for v in ops[k:k + 5])

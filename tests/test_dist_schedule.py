@@ -122,7 +122,7 @@ def check_collective(scheds, nranks):
     return totals
 
 
-def build_all(N, nranks, workers=4):
+def build_all(N, nranks, workers=3):
     """Every rank's schedule, `workers` at a time (the library call releases the GIL; each call
     holds its own copy of the plan: 256^3 about 6 GB)."""
     from concurrent.futures import ThreadPoolExecutor
