@@ -99,7 +99,10 @@ struct Rhs {
   int64_t ldx, ldv;
 };
 constexpr int kMultiRhs = 16;   // right-hand sides per solve launch
-constexpr int kSweepWK = 4;     // k_tri_sweep: 64-row blocks (worker waves) per work item
+#ifndef SMLU_SWEEP_WK
+#define SMLU_SWEEP_WK 4
+#endif
+constexpr int kSweepWK = SMLU_SWEEP_WK;   // k_tri_sweep: 64-row blocks (worker waves) per work item
 constexpr int kSweepXB = 64;    // k_tri_sweep: external blocks x right-hand sides per run (LDS 32 KB)
 // One dense chunk of the reference's solve layout (src/SharedMemSparseLU.jl:101-243), 0-based:
 // the s x s diagonal block over x[c0, c0+s) at data[tri] (column-major, ld s) and the negated

@@ -505,7 +505,7 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_dst) {
 }
 
 
-template <bool TRSM, bool EB, bool ZI = false>
+template <bool TRSM, bool EB>
 __device__ __forceinline__ void gemm128_mfma3_interior(const GemmTask& t, int m0, int n0, Mfma3Lds& S,
                                                        const GrowthArgs& ga) {
   const int tid = threadIdx.x, lane = tid & 63;
@@ -546,23 +546,16 @@ __device__ __forceinline__ void gemm128_mfma3_interior(const GemmTask& t, int m0
     }
   };
   v4d acc[4][4];
-  if (ZI) {   // accumulate -A*B from zero; C is added once in the epilogue (no C load before the first MFMA)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+  for (int ip = 0; ip < 2; ++ip)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = v4d{0.0, 0.0, 0.0, 0.0};
-  } else {
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-    for (int ip = 0; ip < 2; ++ip)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const v2d c = ldu2(cbase(ip, j, r), c_lo);
-          acc[2 * ip][j][r] = c.x;
-          acc[2 * ip + 1][j][r] = c.y;
-        }
-  }
+      for (int r = 0; r < 4; ++r) {
+        const v2d c = ldu2(cbase(ip, j, r), c_lo);
+        acc[2 * ip][j][r] = c.x;
+        acc[2 * ip + 1][j][r] = c.y;
+      }
   // fragment addresses: A row pair wr + 32 ip + 2 li at k = 4 kq + lk; B column wc + 16 j + li at
   // k = 4 kq + lk, i.e. pair 2 kq + (lk >> 1), slot that ^ (li >> 1), element lk & 1
   const int a_off = (lk * HBM_ + wr + 2 * li);
@@ -639,39 +632,20 @@ __device__ __forceinline__ void gemm128_mfma3_interior(const GemmTask& t, int m0
     }
   }
   double gmax = 0.0;
-  if (ZI) {   // C + acc, C read in two halves (32 VGPRs of pairs in flight each)
 #pragma unroll
-    for (int ip = 0; ip < 2; ++ip) {
-      v2d cv[4][4];
+  for (int ip = 0; ip < 2; ++ip)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) cv[j][r] = ldu2(cbase(ip, j, r), c_lo);
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const v2d c = v2d{cv[j][r].x + acc[2 * ip][j][r], cv[j][r].y + acc[2 * ip + 1][j][r]};
-          stu2(cbase(ip, j, r), c_lo, c);
-          if (TRSM) gmax = fmax(gmax, fmax(fabs(c.x), fabs(c.y)));
-        }
-    }
-  } else {
-#pragma unroll
-    for (int ip = 0; ip < 2; ++ip)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const v2d c = v2d{acc[2 * ip][j][r], acc[2 * ip + 1][j][r]};
-          stu2(cbase(ip, j, r), c_lo, c);
-          if (TRSM) gmax = fmax(gmax, fmax(fabs(c.x), fabs(c.y)));
-        }
-  }
+      for (int r = 0; r < 4; ++r) {
+        const v2d c = v2d{acc[2 * ip][j][r], acc[2 * ip + 1][j][r]};
+        stu2(cbase(ip, j, r), c_lo, c);
+        if (TRSM) gmax = fmax(gmax, fmax(fabs(c.x), fabs(c.y)));
+      }
   if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
 }
 
-template <bool TRSM, bool EB = false, bool ZI = false>
+template <bool TRSM, bool EB = false>
 __global__ __launch_bounds__(256, 2) void k_gemm128_mfma3(const GemmTask* __restrict__ tasks, int ntask,
                                                           GrowthArgs ga) {
   __shared__ __attribute__((aligned(16))) double lds[sizeof(Mfma3Lds) / sizeof(double)];
@@ -681,7 +655,7 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma3(const GemmTask* __rest
   tile_rc<HBM_>(t, b - t.tile0, tm, tn);
   const int m0 = tm * HBM_, n0 = tn * HBM_;
   if (m0 + HBM_ <= t.m && n0 + HBM_ <= t.n) {
-    gemm128_mfma3_interior<TRSM, EB, ZI>(t, m0, n0, *reinterpret_cast<Mfma3Lds*>(lds), ga);
+    gemm128_mfma3_interior<TRSM, EB>(t, m0, n0, *reinterpret_cast<Mfma3Lds*>(lds), ga);
   } else {
     auto& As = *reinterpret_cast<double(*)[2][HBK_][HBM_]>(lds);
     auto& Bs = *reinterpret_cast<double(*)[2][HBK_][HLDB_]>(lds + 2 * HBK_ * HBM_);
@@ -927,8 +901,6 @@ hipError_t launch_gemm_g(hipStream_t st, int64_t ntiles, const GemmTask* tasks, 
   else if (tile == 135) k_gemm128_mfma3<false, true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 131 && trsm) k_gemm128_mfma3<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 131) k_gemm128_mfma3<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 137) k_gemm128_mfma3<false, false, true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
-  else if (tile == 139) k_gemm128_mfma3<false, true, true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 65 && trsm) k_gemm_k64<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 65) k_gemm_k64<false><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);
   else if (tile == 66 && trsm) k_gemm64_mfma<true><<<(unsigned)ntiles, 256, 0, st>>>(tasks, ntask, ga);

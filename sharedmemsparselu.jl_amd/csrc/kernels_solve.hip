@@ -703,7 +703,7 @@ __device__ __forceinline__ void sweep_mark(bool, int64_t, int, int) {}
 #endif
 
 template <bool UPPER, int NR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1)))
+__global__ __launch_bounds__(64 * kSweepWK) __attribute__((amdgpu_waves_per_eu(1, (kSweepWK + 3) / 4)))
 void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* __restrict__ tick,
                  int32_t* __restrict__ flags0, double* __restrict__ xh, int32_t* __restrict__ status,
                  const SNode* __restrict__ sn, const double* __restrict__ store, double* __restrict__ x,
@@ -729,10 +729,10 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
   // my row; blocks of other chunks (external) and of this chunk (internal, block ids in order)
   int64_t row, myblk;
   if (!UPPER) {
-    row = 256 * q + tid;
+    row = 64 * kSweepWK * q + tid;
     myblk = row < ns ? row / 64 : nblk;
   } else {
-    myblk = nblk - 1 - 4 * q - wv;
+    myblk = nblk - 1 - kSweepWK * q - wv;
     row = 64 * myblk + lane;
   }
   const bool has = UPPER ? (myblk >= 0 && row < ns) : row < M;
@@ -763,9 +763,9 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
     for (int r = 0; r < NR; ++r)
       if (r < nr) o[r] -= dot64_split(d, bw, [&](int j) { return xs[j][r]; });
   };
-  // external blocks (solved by earlier chunks): forward 0 .. min(4q, nblk)-1, backward nblk-1
-  // down to nblk-4q; every row of this chunk lies beyond them
-  const int64_t next = min<int64_t>(4 * q, nblk);
+  // external blocks (solved by earlier chunks): forward 0 .. min(WK q, nblk)-1, backward nblk-1
+  // down to nblk-WK q (WK = kSweepWK waves, one 64-row block each); every row of this chunk lies beyond them
+  const int64_t next = min<int64_t>(kSweepWK * q, nblk);
   for (int64_t e = 0; e < next; ++e) {
     const int64_t c = UPPER ? nblk - 1 - e : e;
     const int bw = (int)min<int64_t>(64, ns - 64 * c);
@@ -779,8 +779,8 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
   }
   sweep_mark(UPPER, item, wv, 1);
   // internal blocks: wave t solves block b and publishes it, the waves beyond apply it
-  for (int t = 0; t < 4; ++t) {
-    const int64_t b = UPPER ? nblk - 1 - 4 * q - t : 4 * q + t;
+  for (int t = 0; t < kSweepWK; ++t) {
+    const int64_t b = UPPER ? nblk - 1 - kSweepWK * q - t : kSweepWK * q + t;
     if (b < 0 || b >= nblk) break;
     const int bw = (int)min<int64_t>(64, ns - 64 * b);
     // rows that apply block b: the waves beyond t, and the update rows of wave t when block b is
@@ -1313,8 +1313,8 @@ hipError_t launch_tri_sweep(hipStream_t st, bool upper, int64_t nwg, const Front
   // up to 8 right-hand sides (NR-wide hand-off slots); wider batches take the per-block schedule
   if (rh.n < 1 || rh.n > 8) return hipErrorInvalidValue;
 #define SWEEP(NR)                                                                                                   \
-  (upper ? (k_tri_sweep<true, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh, spin)) \
-         : (k_tri_sweep<false, NR><<<(unsigned)nwg, 256, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh, spin)))
+  (upper ? (k_tri_sweep<true, NR><<<(unsigned)nwg, 64 * kSweepWK, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh, spin)) \
+         : (k_tri_sweep<false, NR><<<(unsigned)nwg, 64 * kSweepWK, 0, st>>>(ft, nft, tick, flags, xh, status, sn, store, x, vbuf, rh, spin)))
   if (rh.n == 1) SWEEP(1);
   else if (rh.n <= 4) SWEEP(4);
   else SWEEP(8);
