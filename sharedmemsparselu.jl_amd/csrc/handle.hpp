@@ -122,6 +122,11 @@ struct Launch {
   int64_t off = 0, cnt = 0, nwg = 0, aux = 0, aux2 = 0;
   int64_t off2 = 0, cnt2 = 0, nwg2 = 0;   // second work list (merged launches)
   double flops = 0;
+  // solves (one GPU): consecutive launches with the same grp > 0 are one level's fronts; in batched
+  // solves (the per-block schedule) the side ones (small and tiny fronts) run on the handle's side
+  // stream next to the large fronts' chain
+  int grp = 0;
+  bool side = false;
 };
 
 template <class T>

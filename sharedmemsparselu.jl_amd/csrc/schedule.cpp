@@ -405,7 +405,8 @@ static int build_schedule(smlu_handle* h) {
         // overlap group: the size classes of one level run on two streams (factor.cpp).  That is
         // race-free only because the scratch plan (plan.cpp: one F22 block per level, live until
         // the parents' level) keeps every F22 a front of this level writes disjoint from every
-        // other one and from the children's F22 the level reads -- checked below
+        // other one and from the children's F22 the level reads -- checked below.  (Round 6: the
+        // level's blocked fronts on a third stream next to them, C2 3.51 -> 4.25 ms: not kept.)
         L.aux2 = l + 1;
         if (L.cnt > 0) h->fac.push_back(L);
       }
@@ -1109,6 +1110,19 @@ static int build_schedule(smlu_handle* h) {
       (big ? bigs : tiny_front ? tiny : small).push_back(s);
     }
     std::vector<Launch> bl;
+    const size_t fwd0 = h->fwd.size();
+    // one GPU: a level's small and tiny fronts are independent of its large fronts (disjoint x rows
+    // and front vectors, children in lower levels): they run on the side stream next to the large
+    // fronts' gather / sweep chain (solve.cpp)
+    const bool overlap = h->nranks == 1 && !bigs.empty() && !(tiny.empty() && small.empty());
+    auto mark_level = [&](std::vector<Launch>& seq, size_t from) {
+      if (!overlap) return;
+      for (size_t i = from; i < seq.size(); ++i) {
+        Launch& X = seq[i];
+        X.grp = l + 1;
+        X.side = X.kind == K_FWDT || X.kind == K_FWD || X.kind == K_BWDT || X.kind == K_BWD;
+      }
+    };
     // tiny fronts: one wave per front; micro fronts (M <= 8) eight per wave for a single rhs
     for (int micro = 1; micro >= 0; --micro) {
       Launch L;
@@ -1216,6 +1230,8 @@ static int build_schedule(smlu_handle* h) {
         ssync_n += fb;
         bl.push_back(U);
         bl.push_back(B);
+        mark_level(h->fwd, fwd0);
+        mark_level(bl, 0);
         bwd_levels.push_back(bl);
         goto shared_fronts;
       }
@@ -1258,6 +1274,8 @@ static int build_schedule(smlu_handle* h) {
       bl.push_back(U);
       for (auto& b : bsteps) bl.push_back(b);
     }
+    mark_level(h->fwd, fwd0);
+    mark_level(bl, 0);
     bwd_levels.push_back(bl);
   shared_fronts:
     // forward solve of the shared front: the children's update vectors go to the first block's
@@ -1473,6 +1491,7 @@ static int build_schedule(smlu_handle* h) {
       for (int64_t t = 0; t < nb; ++t) {
         Launch F;
         F.kind = upper ? K_TRIB : K_TRIF;
+        F.grp = S.grp;
         F.step = (int)t;
         F.off = (int64_t)ft.size();
         int64_t w = 0, cnt = 0;

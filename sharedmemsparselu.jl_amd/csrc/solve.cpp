@@ -4,8 +4,7 @@
 
 // One solve launch for rh.n right-hand sides (x columns at w + r*rh.ldx, front vectors at
 // v + r*rh.ldv); the multi-GPU kinds (K_BWDU12C, K_VCOPY) are single-vector only.
-static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, double* v, Rhs rh) {
-  hipStream_t st = h->stream;
+static hipError_t run_solve_launch(smlu_handle* h, const Launch& L, double* w, double* v, Rhs rh, hipStream_t st) {
   switch (L.kind) {
     case K_FWD:
       return launch_fwd(st, (int)L.cnt, h->ilist.p + L.off, h->sn.p, h->chlist.p, h->relmap.p,
@@ -96,24 +95,46 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
   }
   HIPCHK(load_input(src, lds));
   // launches between communication steps (one GPU: a single segment each)
-  auto run_seq = [&](const std::vector<Launch>& seq, const std::vector<size_t>& seg, const std::vector<int>& cm) {
+  // overlap: a level's small fronts on the side stream next to its large fronts' per-block chain
+  // (batched right-hand sides: 8 per 128^3 solve 59.5 -> 57.4 ms).  Not next to the sync-free
+  // sweeps, whose waiting workgroups lose CUs to them (1 rhs: 13.8 -> 15.2 ms, round 6).
+  auto run_seq = [&](const std::vector<Launch>& seq, const std::vector<size_t>& seg, const std::vector<int>& cm,
+                     bool overlap) {
     for (size_t k = 0; k < seg.size(); ++k) {
       if (k > 0) {
         int rc = exec_comm(h, cm[k - 1]);
         if (rc != SMLU_OK) return rc;
       }
       const size_t hi = k + 1 < seg.size() ? seg[k + 1] : seq.size();
-      for (size_t i = seg[k]; i < hi; ++i) HIPCHK(run_solve_launch(h, seq[i], w, v, rh));
+      // a level's side launches (grp > 0, side) on the side stream: forked after everything
+      // before the level, joined before the next level
+      bool forked = false;
+      for (size_t i = seg[k]; i < hi; ++i) {
+        const Launch& L = seq[i];
+        const bool first = overlap && L.grp > 0 && (i == seg[k] || seq[i - 1].grp != L.grp);
+        const bool last = overlap && L.grp > 0 && (i + 1 == hi || seq[i + 1].grp != L.grp);
+        if (first) {
+          HIPCHK(hipEventRecord(h->fork_ev, st));
+          HIPCHK(hipStreamWaitEvent(h->side, h->fork_ev, 0));
+          forked = true;
+        }
+        HIPCHK(run_solve_launch(h, L, w, v, rh, L.side && forked ? h->side : st));
+        if (last && forked) {
+          HIPCHK(hipEventRecord(h->join_ev, h->side));
+          HIPCHK(hipStreamWaitEvent(st, h->join_ev, 0));
+          forked = false;
+        }
+      }
     }
     return (int)SMLU_OK;
   };
   auto sweeps = [&](bool steps) {   // steps: the per-block sequences instead of the sweeps
     if (mode != 2) {
-      int rc = steps ? run_seq(h->fwdm, h->fwdm_seg, h->fwd_comm) : run_seq(h->fwd, h->fwd_seg, h->fwd_comm);
+      int rc = steps ? run_seq(h->fwdm, h->fwdm_seg, h->fwd_comm, true) : run_seq(h->fwd, h->fwd_seg, h->fwd_comm, false);
       if (rc != SMLU_OK) return rc;
     }
     if (mode != 1) {
-      int rc = steps ? run_seq(h->bwdm, h->bwdm_seg, h->bwd_comm) : run_seq(h->bwd, h->bwd_seg, h->bwd_comm);
+      int rc = steps ? run_seq(h->bwdm, h->bwdm_seg, h->bwd_comm, true) : run_seq(h->bwd, h->bwd_seg, h->bwd_comm, false);
       if (rc != SMLU_OK) return rc;
     }
     return (int)SMLU_OK;
