@@ -212,6 +212,32 @@ template <bool UPPER>
 __device__ __forceinline__ double tri64_row(double xi, const double (&row)[64], double dinv, int bw) {
   return tri64_acc<UPPER>(xi, [&](int j) { return row[j]; }, dinv, bw);
 }
+// The same substitution for NR right-hand sides at once, the NR chains interleaved step by step
+// (independent readlane + fma chains keep the fp64 pipe busy: a batched chain costs about twice a
+// single one instead of NR times).  Per right-hand side the operations and their order are
+// tri64_row's, so every column is bitwise the single-vector result.
+template <bool UPPER, int NR>
+__device__ __forceinline__ void tri64_rows(double (&xi)[NR], const double (&row)[64], double dinv, int bw) {
+  if (bw == 64) {
+#pragma unroll
+    for (int jj = 0; jj < 64; ++jj) {
+      const int j = UPPER ? 63 - jj : jj;
+#pragma unroll
+      for (int r = 0; r < NR; ++r) xi[r] = fma(-row[j], readlane_f64(xi[r], j), xi[r]);
+    }
+  } else {
+#pragma unroll
+    for (int jj = 0; jj < 64; ++jj) {
+      const int j = UPPER ? 63 - jj : jj;
+      if (j < bw)
+#pragma unroll
+        for (int r = 0; r < NR; ++r) xi[r] = fma(-row[j], readlane_f64(xi[r], j), xi[r]);
+    }
+  }
+  if (UPPER)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) xi[r] *= dinv;
+}
 // row[j] *= 1/u_jj (held by lane j as dinv), j < bw: the backward row for tri64_row.
 __device__ __forceinline__ void tri64_scale_upper(double (&row)[64], double dinv, int bw) {
 #pragma unroll

@@ -406,14 +406,15 @@ __global__ __launch_bounds__(256) void k_bwd_tiny(const int32_t* __restrict__ li
 // one right-hand side: eight fronts per wave, lane group g = lane >> 3 holds front g's rows
 // (row i = lane & 7), broadcasts within the group by __shfl.  A wave per front (k_fwd_tiny) left
 // 56 of 64 lanes idle and ran at 3 waves/SIMD; these kernels keep ~32 waves per CU in flight.
-// Exactly k_fwd_tiny's / k_bwd_tiny's operations in the same order per element (bitwise equal;
-// batched solves keep the tiny kernels on the same front lists).
+// Exactly k_fwd_tiny's / k_bwd_tiny's operations in the same order per element (bitwise equal);
+// batched solves loop over their right-hand sides here with the factor rows loaded once (round 6:
+// they used to take a whole wave per micro front through the tiny kernels).
 __global__ __launch_bounds__(256) void k_fwd_micro(const int32_t* __restrict__ list, int cnt,
                                                    const SNode* __restrict__ sn, const int32_t* __restrict__ chlist,
                                                    const int32_t* __restrict__ relmap,
                                                    const int32_t* __restrict__ rowperm,
                                                    const double* __restrict__ store, double* __restrict__ x,
-                                                   double* __restrict__ vbuf) {
+                                                   double* __restrict__ vbuf, Rhs rh) {
   __shared__ double sv[32][8];
   const int lane = threadIdx.x & 63, g = threadIdx.x >> 3, i = threadIdx.x & 7;
   const int64_t f = (int64_t)blockIdx.x * 32 + g;
@@ -425,41 +426,46 @@ __global__ __launch_bounds__(256) void k_fwd_micro(const int32_t* __restrict__ l
   double l[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) l[j] = (i < M && j < ns) ? Lp[(int64_t)j * M + i] : 0.0;
-  sv[g][i] = i < ns ? x[s.first + i] : 0.0;
-  wave_lds_sync();
-  for (int c = act ? s.chbeg : 0; c < (act ? s.chend : 0); ++c) {   // parent += child, children in order
-    const SNode ch = sn[chlist[c]];
-    for (int q = i; q < ch.nu; q += 8) {
-      const int t = relmap[ch.rowptr + q];
-      sv[g][t] = sv[g][t] + vbuf[ch.voff + ch.ns + q];
+  const int pr = i < ns ? rowperm[s.first + i] : i;
+  const int gb = lane & ~7;
+  for (int r = 0; r < rh.n; ++r) {   // the factor rows loaded once for every right-hand side
+    double* xr = x + r * rh.ldx;
+    double* vr = vbuf + r * rh.ldv;
+    sv[g][i] = i < ns ? xr[s.first + i] : 0.0;
+    wave_lds_sync();
+    for (int c = act ? s.chbeg : 0; c < (act ? s.chend : 0); ++c) {   // parent += child, children in order
+      const SNode ch = sn[chlist[c]];
+      for (int q = i; q < ch.nu; q += 8) {
+        const int t = relmap[ch.rowptr + q];
+        sv[g][t] = sv[g][t] + vr[ch.voff + ch.ns + q];
+      }
+      wave_lds_sync();
     }
     wave_lds_sync();
-  }
-  wave_lds_sync();
-  const int pr = i < ns ? rowperm[s.first + i] : i;
-  double val = i < M ? sv[g][pr] : 0.0;
-  double acc = 0.0;
-  const int gb = lane & ~7;
+    double val = i < M ? sv[g][pr] : 0.0;
+    double acc = 0.0;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const double xj = __shfl(val, gb + j, 64);
-    if (j < ns) {
-      if (i > j && i < ns) val = fma(-l[j], xj, val);
-      else if (i >= ns) acc = fma(l[j], xj, acc);
+    for (int j = 0; j < 8; ++j) {
+      const double xj = __shfl(val, gb + j, 64);
+      if (j < ns) {
+        if (i > j && i < ns) val = fma(-l[j], xj, val);
+        else if (i >= ns) acc = fma(l[j], xj, acc);
+      }
     }
-  }
-  if (i < ns) {
-    x[s.first + i] = val;
-    vbuf[s.voff + i] = val;
-  } else if (i < M) {
-    vbuf[s.voff + i] = val - acc;
+    if (i < ns) {
+      xr[s.first + i] = val;
+      vr[s.voff + i] = val;
+    } else if (i < M) {
+      vr[s.voff + i] = val - acc;
+    }
+    wave_lds_sync();   // every lane read sv before the next right-hand side overwrites it
   }
 }
 
 __global__ __launch_bounds__(256) void k_bwd_micro(const int32_t* __restrict__ list, int cnt,
                                                    const SNode* __restrict__ sn, const int32_t* __restrict__ rows,
                                                    const double* __restrict__ store, double* __restrict__ x,
-                                                   double* __restrict__ vbuf) {
+                                                   double* __restrict__ vbuf, Rhs rh) {
   const int lane = threadIdx.x & 63, i = threadIdx.x & 7;
   const int64_t f = (int64_t)blockIdx.x * 32 + (threadIdx.x >> 3);
   const bool act = f < cnt;
@@ -467,30 +473,33 @@ __global__ __launch_bounds__(256) void k_bwd_micro(const int32_t* __restrict__ l
   if (act) s = sn[list[f]];
   const int ns = act ? s.ns : 0, nu = act ? s.nu : 0;
   const int64_t M = (int64_t)ns + nu;
-  // x_s - U12 x[R] (columns in order), then the upper chain
-  double acc = 0.0;
-  if (i < ns) {
-    const double* U12 = store + s.Uoff;
-    for (int j = 0; j < nu; ++j) acc = fma(U12[(int64_t)j * ns + i], x[rows[s.rowptr + j]], acc);
-  }
-  const double o = i < ns ? x[s.first + i] : 0.0;
-  double val = o - (nu > 0 ? acc : 0.0);
-  if (!(i < ns)) val = 0.0;
   const double* Lp = store + s.Loff;
   double l[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) l[j] = (i < ns && j < ns) ? Lp[(int64_t)j * M + i] : 0.0;
   const double dinv = i < ns ? recip(Lp[(int64_t)i * M + i]) : 1.0;
   const int gb = lane & ~7;
+  for (int r = 0; r < rh.n; ++r) {
+    double* xr = x + r * rh.ldx;
+    // x_s - U12 x[R] (columns in order), then the upper chain
+    double acc = 0.0;
+    if (i < ns) {
+      const double* U12 = store + s.Uoff;
+      for (int j = 0; j < nu; ++j) acc = fma(U12[(int64_t)j * ns + i], xr[rows[s.rowptr + j]], acc);
+    }
+    const double o = i < ns ? xr[s.first + i] : 0.0;
+    double val = o - (nu > 0 ? acc : 0.0);
+    if (!(i < ns)) val = 0.0;
 #pragma unroll
-  for (int j = 7; j >= 0; --j) {
-    if (j < ns && i == j) val = val * dinv;
-    const double xj = __shfl(val, gb + j, 64);
-    if (j < ns && i < j) val = fma(-l[j], xj, val);
-  }
-  if (i < ns) {
-    x[s.first + i] = val;
-    vbuf[s.voff + i] = val;
+    for (int j = 7; j >= 0; --j) {
+      if (j < ns && i == j) val = val * dinv;
+      const double xj = __shfl(val, gb + j, 64);
+      if (j < ns && i < j) val = fma(-l[j], xj, val);
+    }
+    if (i < ns) {
+      xr[s.first + i] = val;
+      vbuf[r * rh.ldv + s.voff + i] = val;
+    }
   }
 }
 
@@ -789,17 +798,20 @@ void k_tri_sweep(const FrontTile* __restrict__ ft, int nft, unsigned long long* 
     if (applies) load_tile(b, bw);
     if (wv == t) {
       sweep_mark(UPPER, item, wv, 2);
+      double y[NR];   // the NR chains interleaved (tri64_rows; per column bitwise tri64_row)
+#pragma unroll
+      for (int r = 0; r < NR; ++r) y[r] = o[r];
+      tri64_rows<UPPER, NR>(y, drow, dinv, bw);
+      const bool mine = lane < bw && has;
 #pragma unroll
       for (int r = 0; r < NR; ++r) {
         if (r < nr) {
-          const double y = tri64_row<UPPER>(o[r], drow, dinv, bw);
-          const bool mine = lane < bw && has;
-          if (mine) o[r] = y;
-          atomic_write_f64(xhf + (b * kMultiRhs + r) * 64 + lane, mine ? y : 0.0);
+          if (mine) o[r] = y[r];
+          atomic_write_f64(xhf + (b * kMultiRhs + r) * 64 + lane, mine ? y[r] : 0.0);
           if (mine) {
-            xs[lane][r] = y;
-            xf[r * rh.ldx + 64 * b + lane] = y;
-            v[r * rh.ldv + 64 * b + lane] = y;
+            xs[lane][r] = y[r];
+            xf[r * rh.ldx + 64 * b + lane] = y[r];
+            v[r * rh.ldv + 64 * b + lane] = y[r];
           }
         }
       }
@@ -1236,12 +1248,13 @@ hipError_t launch_fwd_tiny(hipStream_t st, int cnt, const int32_t* list, const S
                            const double* store, double* x, double* vbuf, Rhs rh, int micro) {
   if (cnt <= 0) return hipSuccess;
   if (rh.n < 1 || rh.n > kMaxRhs) return hipErrorInvalidValue;
-  if (micro && rh.n == 1) {   // every front of the list has M <= 8
-    k_fwd_micro<<<nblk(cnt, 32), 256, 0, st>>>(list, cnt, sn, chlist, relmap, rowperm, store, x, vbuf);
+  if (micro) {   // every front of the list has M <= 8 (batches too: the rows loaded once per front)
+    k_fwd_micro<<<nblk(cnt, 32), 256, 0, st>>>(list, cnt, sn, chlist, relmap, rowperm, store, x, vbuf, rh);
     return hipGetLastError();
   }
   const unsigned g = nblk(cnt, 4);
   if (rh.n == 1) k_fwd_tiny<1><<<g, 256, 0, st>>>(list, cnt, sn, chlist, relmap, rowperm, store, x, vbuf, rh);
+  else if (rh.n <= 8) k_fwd_tiny<8><<<g, 256, 0, st>>>(list, cnt, sn, chlist, relmap, rowperm, store, x, vbuf, rh);
   else k_fwd_tiny<kMaxRhs><<<g, 256, 0, st>>>(list, cnt, sn, chlist, relmap, rowperm, store, x, vbuf, rh);
   return hipGetLastError();
 }
@@ -1249,14 +1262,15 @@ hipError_t launch_bwd_tiny(hipStream_t st, int cnt, const int32_t* list, const S
                            const int32_t* rows, const double* store, double* x, double* vbuf, Rhs rh, int micro) {
   if (cnt <= 0) return hipSuccess;
   if (rh.n < 1 || rh.n > kMaxRhs) return hipErrorInvalidValue;
-  if (micro && rh.n == 1) {
-    k_bwd_micro<<<nblk(cnt, 32), 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf);
+  if (micro) {
+    k_bwd_micro<<<nblk(cnt, 32), 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf, rh);
     return hipGetLastError();
   }
   const unsigned g = nblk(cnt, 4);
   // the <4> instance also for a single rhs: <1> lets the compiler keep the U12 and U11 slabs live
   // together (256 VGPRs)
   if (rh.n <= 4) k_bwd_tiny<4><<<g, 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf, rh);
+  else if (rh.n <= 8) k_bwd_tiny<8><<<g, 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf, rh);
   else k_bwd_tiny<kMaxRhs><<<g, 256, 0, st>>>(list, cnt, sn, rows, store, x, vbuf, rh);
   return hipGetLastError();
 }

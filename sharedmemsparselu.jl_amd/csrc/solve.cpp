@@ -70,7 +70,9 @@ static int run_solve_dev(smlu_handle* h, const double* db, double* dx, int mode,
   }
   // batches of up to SMLU_SWEEP_MAX_RHS (<= 8) right-hand sides run the sweeps (NR-wide hand-off
   // slots), wider ones the per-block launches (fwdm / bwdm)
-  constexpr int sweep_max_rhs = 1;   // batches run the per-block schedule (the NR-wide sweep slots measured slower)
+  // batches of up to 8 run the sweeps too (round 6: the NR substitution chains interleaved,
+  // tri64_rows); wider ones the per-block schedule
+  constexpr int sweep_max_rhs = 8;
   const bool steps = rh.n > std::min(8, std::max(1, sweep_max_rhs)) && h->nranks == 1;
   // The sync-free sweeps' waits are bounded: a wait that gives up raises sstatus, which is read back
   // after every solve that ran them; the solve is then re-run on the per-block schedule (fwdm / bwdm,
