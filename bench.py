@@ -334,6 +334,9 @@ def main():
     ap.add_argument("--no-profile", action="store_true", help="skip per-kernel HIP events")
     ap.add_argument("--test-one-gpu", action="store_true",
                     help="rehearsal: all ranks on cuda:0, gloo transport (never for measurements)")
+    ap.add_argument("--one-gpu-transport", default="host", choices=["host", "device"],
+                    help="--test-one-gpu: the host-memory transport, or the RCCL calling convention "
+                         "(device buffers on the library's stream) carried over gloo")
     ap.add_argument("--check-single", action="store_true",
                     help="partitioned run: after the timed steps, rank 0 factors the last values on one GPU "
                          "and every rank's solution is compared with that one (rehearsals, VERDICT r05)")
@@ -381,7 +384,7 @@ def main():
     t0 = time.perf_counter()
     if partitioned:   # one factorization split over the ranks (subtrees + RCCL exchanges)
         F = smlu.DistributedSparseLU(A, device=local, ordering=args.ordering,
-                                     transport="host" if args.test_one_gpu else "rccl",
+                                     transport=args.one_gpu_transport if args.test_one_gpu else "rccl",
                                      **({"grid": grid} if grid else {}))
     else:
         F = smlu.ParallelSparseLU(A, grid=grid, device=local, profile=not args.no_profile)
@@ -571,7 +574,8 @@ def main():
         }
         if partitioned:
             res["rccl_nranks"] = min(r.get("rccl_nranks", 0) for r in per_rank)
-            res["transport"] = "host (gloo, one-GPU rehearsal)" if args.test_one_gpu else "rccl"
+            res["transport"] = (f"{args.one_gpu_transport} (gloo, one-GPU rehearsal)" if args.test_one_gpu
+                                else "rccl")
             if args.check_single:
                 res["x_vs_single_gpu_max_rel"] = max(r["x_vs_single_gpu_max_rel"] for r in per_rank)
         if not args.no_cpu and world == 1:

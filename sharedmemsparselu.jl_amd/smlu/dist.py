@@ -12,7 +12,8 @@ library drives every transfer itself through a transport:
   stream-ordered, no host synchronisation): rank 0 draws the RCCL unique id, torch.distributed
   only broadcasts those 128 bytes once;
 * ``gloo`` process group -> a host-memory transport implemented here with torch.distributed
-  point-to-point calls (tests; several ranks may then share one GPU).
+  point-to-point calls (tests; several ranks may then share one GPU); ``transport="device"`` runs
+  the library's device-memory (RCCL) calling convention over gloo instead.
 
     F = DistributedSparseLU(A, device=local_rank)   # analysis + allocation + first factorization
     F.refactor_device(d_values)                     # lu!(F, A), values already in HBM (collective)
@@ -90,6 +91,79 @@ class HostTransport:
             return 1
 
 
+class DeviceStagedTransport(HostTransport):
+    """The built-in RCCL transport's calling convention carried over gloo: device_memory = 1, so the
+    library hands over DEVICE buffers (its send / receive staging, the broadcast block buffer) on
+    its stream, exactly as it does to rccl_exchange / rccl_bcast, and does no host staging of its
+    own; each call here synchronises that stream, copies the messages to host memory, moves them
+    over gloo and copies the received ones back.  A one-GPU rehearsal of exec_comm's device-memory
+    path (the addressing RCCL sees) -- RCCL itself refuses two ranks on one GPU."""
+
+    def __init__(self, dist, group=None):
+        super().__init__(dist, group)
+        self.struct = C.SmluTransport(None, 1, *self._cb)
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        hip.hipMemcpy.restype = ctypes.c_int
+        hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+        hip.hipStreamSynchronize.restype = ctypes.c_int
+        self.hip = hip
+
+    def _sync(self, stream):
+        if self.hip.hipStreamSynchronize(stream) != 0:
+            raise RuntimeError("hipStreamSynchronize failed")
+
+    def _d2h(self, dev, n):
+        buf = np.empty(int(n), np.uint8)
+        if self.hip.hipMemcpy(buf.ctypes.data, dev, int(n), 2) != 0:   # hipMemcpyDeviceToHost
+            raise RuntimeError("hipMemcpy D2H failed")
+        return buf
+
+    def _h2d(self, dev, buf):
+        if self.hip.hipMemcpy(dev, buf.ctypes.data, buf.size, 1) != 0:   # hipMemcpyHostToDevice
+            raise RuntimeError("hipMemcpy H2D failed")
+
+    def _exchange(self, ctx, npeer, peer, sbuf, sbytes, rbuf, rbytes, stream):
+        try:
+            self._sync(stream)
+            works, recvs = [], []
+            for i in range(npeer):
+                if sbytes[i] > 0:
+                    works.append(self.dist.isend(self.torch.from_numpy(self._d2h(sbuf[i], sbytes[i])),
+                                                 int(peer[i]), group=self.group))
+                if rbytes[i] > 0:
+                    h = np.empty(int(rbytes[i]), np.uint8)
+                    recvs.append((rbuf[i], h))
+                    works.append(self.dist.irecv(self.torch.from_numpy(h), int(peer[i]), group=self.group))
+            for w in works:
+                w.wait()
+            for dev, h in recvs:
+                self._h2d(dev, h)
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return 1
+
+    def _bcast(self, ctx, buf, nbytes, root, gsize, group, stream):
+        try:
+            self._sync(stream)
+            me = self.dist.get_rank(self.group)
+            if me == root:
+                h = self._d2h(buf, nbytes)
+                works = [self.dist.isend(self.torch.from_numpy(h), int(group[i]), group=self.group)
+                         for i in range(gsize) if int(group[i]) != root]
+                for w in works:
+                    w.wait()
+            else:
+                h = np.empty(int(nbytes), np.uint8)
+                self.dist.irecv(self.torch.from_numpy(h), int(root), group=self.group).wait()
+                self._h2d(buf, h)
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return 1
+
+
 class DistributedSparseLU:
     """ParallelSparseLU over the ranks of a torch.distributed process group (collective)."""
 
@@ -114,7 +188,7 @@ class DistributedSparseLU:
         h = ctypes.c_void_p()
         L = C.lib()
         use_rccl = transport == "rccl" or (transport == "auto" and backend == "nccl")
-        self.transport = "rccl" if use_rccl else "host"
+        self.transport = "rccl" if use_rccl else "device" if transport == "device" else "host"
         if use_rccl:
             uid = np.zeros(128, np.uint8)
             if self.rank == 0:
@@ -126,8 +200,8 @@ class DistributedSparseLU:
             uid = np.ascontiguousarray(t.cpu().numpy())
             rc = L.smlu_dist_create_rccl(self.n, C.ptr(self._colptr), C.ptr(self._rowval), C.ptr(vals),
                                          ctypes.byref(o), self.rank, self.nranks, C.ptr(uid), ctypes.byref(h))
-        else:
-            self._tr = HostTransport(dist, group)
+        else:   # "host": host-memory transport; "device": the RCCL calling convention over gloo
+            self._tr = DeviceStagedTransport(dist, group) if transport == "device" else HostTransport(dist, group)
             rc = L.smlu_dist_create(self.n, C.ptr(self._colptr), C.ptr(self._rowval), C.ptr(vals),
                                     ctypes.byref(o), self.rank, self.nranks, ctypes.byref(self._tr.struct),
                                     ctypes.byref(h))

@@ -90,12 +90,24 @@ def _worker(rank, world, port, which, ob, q, transport="auto", gpu_per_rank=Fals
                                             (2, "poisson_big", 128), (4, "poisson_big", 64),
                                             (8, "poisson40", 64)])
 def test_dist_factor_solve_matches_single_gpu(world, which, ob):
+    _run_and_compare(world, which, ob, "auto")
+
+
+@pytest.mark.parametrize("world,which,ob", [(2, "poisson_big", 128), (4, "poisson_big", 64), (8, "poisson40", 64)])
+def test_dist_device_memory_path_matches_single_gpu(world, which, ob):
+    # the RCCL transport's calling convention (device buffers on the handle's stream, no host
+    # staging in the library: exec_comm's device-memory branch, the addressing rccl_exchange /
+    # rccl_bcast receive) with the bytes carried over gloo (smlu/dist.py DeviceStagedTransport)
+    _run_and_compare(world, which, ob, "device")
+
+
+def _run_and_compare(world, which, ob, transport):
     import scipy.sparse as sp
     import smlu
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, which, ob, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, which, ob, q, transport)) for r in range(world)]
     for p in ps:
         p.start()
     # world 8: the rank count of the driver's 8-GPU scaling run (its partition and schedule)
@@ -127,6 +139,8 @@ def test_dist_factor_solve_matches_single_gpu(world, which, ob):
     # the partition really shares fronts between ranks and moves data
     assert max(r[3]["shared_fronts"] for r in res) >= 1
     assert all(r[3]["comm_steps"] >= 1 for r in res)
+    if transport == "device":
+        assert all(r[3]["transport"] == "device" for r in res)
     for rank, (x1, x3), x2, _, _ in res:
         # every rank holds the full solution
         assert np.allclose(x3, xs3, rtol=1e-11, atol=1e-13), (rank, np.abs(x3 - xs3).max())
