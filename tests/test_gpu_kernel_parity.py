@@ -316,6 +316,9 @@ def test_refactor_device_redecides_pivoting_mode(gpu):
     F.refactor_device(dev(Dw))
     assert F.stat("dominant") == 0.0
     assert F.stat("repivots") == 1 and F.stat("pivmode") == 1 and F.stat("weak") == 0
+    # one synchronisation per refactor: the dominance flags came back in the factorization's status
+    # record, the values were factored in the old mode first and again in the new one
+    assert F.stat("mode_refactors") == 1
     b = np.random.default_rng(5).random(n)
     x = np.empty(n)
     smlu.ldiv_(x, F, b)
@@ -325,7 +328,14 @@ def test_refactor_device_redecides_pivoting_mode(gpu):
     Dd2 = _dominant_dense(n, 43)
     F.refactor_device(dev(Dd2))
     assert F.stat("dominant") == 1.0 and F.stat("pivmode") == 0
-    assert F.stat("fronts_mode2") == m2 and F.stat("repivots") == 1
+    assert F.stat("fronts_mode2") == m2 and F.stat("repivots") == 1 and F.stat("mode_refactors") == 2
+    # same values again: no mode change, no second factorization
+    F.refactor_device(dev(Dd2))
+    assert F.stat("mode_refactors") == 2
+    # lu! with host values (smlu_refactor: upload + the same device path) gives the same factors
+    Ld, Ud = F.L.copy(), F.U.copy()
+    F.refactor(sp.csc_matrix(Dd2).data)
+    assert np.array_equal(F.L.data, Ld.data) and np.array_equal(F.U.data, Ud.data)
     smlu.ldiv_(x, F, b)
     assert isapprox(x, np.linalg.solve(Dd2, b), DENSE_TOL, DENSE_TOL)
     factor_parity(sp.csc_matrix(Dd2), F, rtol=1e-11)
