@@ -645,9 +645,32 @@ __device__ __forceinline__ void gemm128_mfma3_interior(const GemmTask& t, int m0
   if (TRSM && t.gsid >= 0) tile_growth(ga, t.gsid, gmax);
 }
 
+#ifdef SMLU_CLOCK_PROBE
+// Dev build only (tools/gemm_clock.py): the shader clock the 128 tile runs at, from the
+// workgroup's own counters -- sum of delta s_memtime (shader cycles) and of delta s_memrealtime
+// (100 MHz constant clock) over every workgroup of the armed launches, per form (EB = F22, else
+// trailing/in-block), accumulated by vector atomics from lane 0.
+__device__ unsigned long long* g_clock_probe = nullptr;
+struct ClockMark {
+  unsigned long long t0, r0;
+  __device__ __forceinline__ ClockMark() : t0(__builtin_amdgcn_s_memtime()), r0(__builtin_amdgcn_s_memrealtime()) {}
+  __device__ __forceinline__ void done(int form) const {
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* p = g_clock_probe;
+    if (p && threadIdx.x == 0) {
+      atomicAdd(p + 4 * form, t1 - t0);
+      atomicAdd(p + 4 * form + 1, r1 - r0);
+      atomicAdd(p + 4 * form + 2, 1ull);
+    }
+  }
+};
+#endif
 template <bool TRSM, bool EB = false>
 __global__ __launch_bounds__(256, 2) void k_gemm128_mfma3(const GemmTask* __restrict__ tasks, int ntask,
                                                           GrowthArgs ga) {
+#ifdef SMLU_CLOCK_PROBE
+  const ClockMark mark;
+#endif
   __shared__ __attribute__((aligned(16))) double lds[sizeof(Mfma3Lds) / sizeof(double)];
   const int64_t b = xcd_window_remap(blockIdx.x, gridDim.x);
   const GemmTask t = tasks[find_gemm_task(tasks, ntask, b)];
@@ -661,6 +684,9 @@ __global__ __launch_bounds__(256, 2) void k_gemm128_mfma3(const GemmTask* __rest
     auto& Bs = *reinterpret_cast<double(*)[2][HBK_][HLDB_]>(lds + 2 * HBK_ * HBM_);
     gemm128_mfma_body<TRSM, false>(t, m0, n0, As, Bs, ga);
   }
+#ifdef SMLU_CLOCK_PROBE
+  mark.done(EB ? 0 : 1);
+#endif
 }
 
 // ------------------------------------------------------------------------------------
@@ -888,6 +914,23 @@ __global__ __launch_bounds__(256) void k_tri_inv(const int32_t* __restrict__ lis
     }
   }
 }
+
+#ifdef SMLU_CLOCK_PROBE
+// arm != 0: zero the counters and arm the probe; arm == 0: copy the 8 counters out and disarm
+extern "C" int smlu_dev_gemm_clock(int arm, unsigned long long* out) {
+  static unsigned long long* buf = nullptr;
+  if (!buf && hipMalloc(&buf, 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  unsigned long long* p = nullptr;
+  if (arm) {
+    if (hipMemset(buf, 0, 8 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    p = buf;
+  } else {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (out && hipMemcpy(out, buf, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  }
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_clock_probe), &p, sizeof p) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // ------------------------------------------------------------------------------------
 // Host-side launch wrappers (called from smlu.cpp)
