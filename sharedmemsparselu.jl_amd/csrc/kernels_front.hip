@@ -1142,14 +1142,22 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
     }
     __syncthreads();
     if (wv != blk) {   // later waves apply the block's updates; every wave replays the swaps
+      // the block's pivots and multipliers in one LDS round trip (not one pair per column)
+      int pj[CW];
+      double lj[CW];
+#pragma unroll
+      for (int j = 0; j < CW; ++j) {
+        pj[j] = s_p[buf][j];
+        lj[j] = s_l[buf][j][lane];
+      }
 #pragma unroll
       for (int j = 0; j < CW; ++j) {
         const int k = k0 + j;
         if (k < w) {
           const int q = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(who, k));
-          const int p = __builtin_amdgcn_readfirstlane(s_p[buf][j]);
+          const int p = __builtin_amdgcn_readfirstlane(pj[j]);
           if (wv > blk) {
-            const double l = s_l[buf][j][lane];
+            const double l = lj[j];
             if (l != 0.0) {
 #pragma unroll
               for (int jj = 0; jj < CW; ++jj) x[jj] = fma(-l, readlane_f64(x[jj], p), x[jj]);
