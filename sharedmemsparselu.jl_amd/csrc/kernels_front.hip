@@ -890,8 +890,16 @@ __device__ __forceinline__ void pmark(long long idx, int k) {
   if (idx >= 0 && threadIdx.x == 0) g_panel_trace.buf[idx * 16 + k] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 #define PMARK(k) pmark(s_pidx, k)
+// slots 8..15: shader-clock cycles (s_memtime) at the hand-off of blocks 7 and 8 between waves:
+// owner start / owner end (before the barrier) / next wave past the barrier / next wave applied
+__device__ __forceinline__ void pmarkc(long long idx, int k, bool who) {
+  if (idx >= 0 && who && (threadIdx.x & 63) == 0) g_panel_trace.buf[idx * 16 + k] = (long long)__builtin_amdgcn_s_memtime();
+}
+#define PMARKB(blk, k, who) \
+  do { if ((blk) == 7 || (blk) == 8) pmarkc(s_pidx, 8 + 4 * ((blk) - 7) + (k), (who)); } while (0)
 #else
 #define PMARK(k) ((void)0)
+#define PMARKB(blk, k, who) ((void)0)
 #endif
 // Tail of the fused panel (k_panel_blk<NWV, true>): the finished tile (x, row positions pos)
 // goes to LDS as k_tri_inv reads it from HBM ([col][row], ld 65, identity outside w x w), wave v
@@ -1093,6 +1101,7 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
     if (k0 >= w) break;
     const int buf = blk & 1;
     if (wv == blk) {   // the owner factors its block
+      PMARKB(blk, 0, true);
 #pragma unroll
       for (int j = 0; j < CW; ++j) {
         const int k = k0 + j;
@@ -1139,8 +1148,10 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
           transpose(k, p, q);
         }
       }
+      PMARKB(blk, 1, true);
     }
     __syncthreads();
+    PMARKB(blk, 2, wv == blk + 1);
     if (wv != blk) {   // later waves apply the block's updates; every wave replays the swaps
       // the block's pivots and multipliers in one LDS round trip (not one pair per column)
       int pj[CW];
@@ -1166,6 +1177,7 @@ __global__ __launch_bounds__(64 * NWV) void k_panel_blk(const int32_t* __restric
           transpose(k, p, q);
         }
       }
+      PMARKB(blk, 3, wv == blk + 1);
     }
   }
   if (has) {

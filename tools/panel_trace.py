@@ -49,6 +49,17 @@ def main():
             print(f"  {names[k]:30s} median {np.median(col):7.2f} us  p90 {np.percentile(col, 90):7.2f}")
     tot = t[:, 7] - t[:, 0]
     print(f"  total (mark 0 -> 7)            median {np.median(tot):7.2f} us")
+    # block hand-off (shader cycles, slots 8..15): blocks 7 and 8 of launches with >= 9 blocks
+    c = out.reshape(n, 16)[:, 8:].astype(np.float64)
+    c = c[(c[:, 0] > 0) & (c[:, 7] > 0)]
+    if len(c):
+        print(f"block hand-off, shader cycles (median over {len(c)} launches):")
+        for b in range(2):
+            o = 4 * b
+            print(f"  block {7 + b}: owner factors {np.median(c[:, o + 1] - c[:, o]):6.0f}, "
+                  f"owner end -> next wave past barrier {np.median(c[:, o + 2] - c[:, o + 1]):6.0f}, "
+                  f"next wave applies {np.median(c[:, o + 3] - c[:, o + 2]):6.0f}")
+        print(f"  block 7 owner start -> block 8 owner start {np.median(c[:, 4] - c[:, 0]):6.0f}")
     F.close()
 
 
