@@ -26,6 +26,10 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* libsmlu.so is built with -fvisibility=hidden: exactly the functions declared here are exported */
+#if defined(__GNUC__)
+#pragma GCC visibility push(default)
+#endif
 
 /* ---- status codes ---------------------------------------------------------------- */
 #define SMLU_OK                 0
@@ -368,6 +372,9 @@ int smlu_dev_copy(smlu_handle* h, int which, int64_t off, int64_t cnt, double* o
 /* Library version string. */
 const char* smlu_version(void);
 
+#if defined(__GNUC__)
+#pragma GCC visibility pop
+#endif
 #ifdef __cplusplus
 }
 #endif

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def header_functions():
     src = open(os.path.join(ROOT, "include", "smlu.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    names = re.findall(r"\b(smlu_[a-z_]+)\s*\(", src)
+    names = re.findall(r"\b(smlu_[a-z0-9_]+)\s*\(", src)
     return sorted(set(names))
 
 
@@ -40,6 +40,10 @@ def test_nm_exports_are_c_abi():
     out = subprocess.run(["nm", "-D", "--defined-only", C.LIB_PATH], capture_output=True, text=True).stdout
     for name in header_functions():
         assert re.search(rf"\bT {name}$", out, flags=re.M), f"{name} not an unmangled export"
+    # and nothing else: the library is built with -fvisibility=hidden, so the internal C++
+    # functions (launch wrappers, plan, schedule) stay inside it
+    exported = set(re.findall(r"^\S+ T (\S+)$", out, flags=re.M))
+    assert exported == set(header_functions()), sorted(exported ^ set(header_functions()))
 
 
 def test_version_and_defaults():
