@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round-6 A/B 11 (via gpurun from the repo root): fused panel with the barrier-free column hand-off
+# (var/pfl.so) vs the committed build (var/base4.so): factor hashes (bitwise check), panel trace,
+# C2, the 128^3 bench, kernel parity tests.
+set -o pipefail
+mkdir -p gpurun_out
+for v in base4 pfl; do
+  SMLU_LIB=$PWD/var/$v.so timeout -k 10 300 python tools/factor_hash.py > gpurun_out/r6_hash_$v.txt 2>gpurun_out/r6_hash_$v.log || { echo hash $v FAIL; tail -5 gpurun_out/r6_hash_$v.log; exit 1; }
+  echo "== $v"; cat gpurun_out/r6_hash_$v.txt
+done
+SMLU_LIB=$PWD/sharedmemsparselu.jl_amd/build_trace/libsmlu_ptrace.so timeout -k 10 300 python tools/panel_trace.py > gpurun_out/panel_trace3.txt 2>gpurun_out/panel_trace3.log || exit 1
+tail -5 gpurun_out/panel_trace3.txt
+for v in base4 pfl; do
+  SMLU_LIB=$PWD/var/$v.so timeout -k 10 120 python tools/c2_bench.py > gpurun_out/r6_c2_$v.json 2>/dev/null || { echo C2 $v FAIL; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/r6_c2_$v.json')); print('c2 $v', round(d['refactor_ms_median'],3), round(d['solve_ms_median'],3))"
+done
+bash tools/ab_libs.sh "var/base4.so var/pfl.so var/base4.so var/pfl.so" || exit 1
+SMLU_LIB=$PWD/var/pfl.so timeout -k 10 500 python -u -m pytest tests/test_gpu_kernel_parity.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -q --timeout 300 --timeout-method thread > gpurun_out/r6_pfl_tests.log 2>&1
+rc=$?
+tail -3 gpurun_out/r6_pfl_tests.log
+exit $rc
