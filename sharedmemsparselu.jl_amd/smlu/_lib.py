@@ -125,6 +125,13 @@ def lib():
             raise RuntimeError(
                 f"libsmlu.so not found at {LIB_PATH}; build it with `make -C {_PKG}` "
                 "(there is no CPU fallback)")
+        # torch (when installed) first: its wheel carries its own HIP runtime under the same
+        # soname as /opt/rocm's, and whichever is loaded first serves the process -- loaded after
+        # libsmlu.so, torch finds its device layer bound to the system runtime and reports no GPU
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(L, name)

@@ -1,6 +1,7 @@
-"""Dev: sha1 of the exported factors (L, U values and the row permutation) of a few matrices, to
-check that a kernel change leaves the factorization bitwise unchanged: run once per library
-(SMLU_LIB=...) and compare the lines.
+"""Dev: sha1 of the exported factors (L, U values and the row permutation) and of device solves
+(one and eight right-hand sides) of a few matrices, to check that a kernel change leaves the
+factorization and the solves bitwise unchanged: run once per library (SMLU_LIB=...) and compare
+the lines.
 
     SMLU_LIB=... python tools/factor_hash.py
 """
@@ -30,7 +31,17 @@ def main():
         h = hashlib.sha1()
         for arr in (F.L.data, F.U.data, np.asarray(F.p)):
             h.update(np.ascontiguousarray(arr).tobytes())
-        print(name, h.hexdigest()[:16], "repivots", F.stat("repivots") if hasattr(F, "stat") else "")
+        # solutions: one right-hand side and a batch of eight (device solves)
+        import torch
+        n = M.shape[0]
+        B = torch.from_numpy(np.random.default_rng(11).standard_normal((8, n))).cuda()
+        X = torch.empty_like(B)
+        F.solve_multi_device(X, B)
+        x1 = torch.empty_like(B[0])
+        F.solve_device(x1, B[0].contiguous())
+        torch.cuda.synchronize()
+        hs = hashlib.sha1(X.cpu().numpy().tobytes() + x1.cpu().numpy().tobytes()).hexdigest()[:16]
+        print(name, h.hexdigest()[:16], "solves", hs, "repivots", F.stat("repivots"))
         F.close()
 
 
